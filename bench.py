@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark of the MI355X-native HCCL reduce path.
+
+Metric (BASELINE.json): "device-resident reduce GiB/s (fp32 sum) vs HBM peak; ring all-reduce bus GB/s".
+
+  N = 1  (default): config C2 — the local reduce primitive HcclAmdLocalReduce (dst = src + dst, the hcomm
+         HcommLocalReduceOnThread replacement) over two 1 GiB fp32 buffers already resident in HBM.
+         A step = one launch over the whole 2 x 1 GiB pair; bytes per step = 3 GiB (read src, read dst, write dst).
+         value = GiB/s = 3 GiB x K / timed region.
+  N > 1  (torchrun, one process per GPU): config C3 — HcclAllReduce fp32 SUM, 4 GiB per rank, over the RCCL
+         communicator built from HcclGetRootInfo / HcclCommInitRootInfo. A step = one AllReduce.
+         value = whole-job reduced input GiB/s = N x 4 GiB x K / max-over-ranks time; bus GB/s is reported beside it.
+
+Every run prints exactly one JSON line on rank 0 (extra diagnostics go to stderr).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import hccl_amd as H  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters"
+C2_COUNT = 1 << 28      # 268,435,456 fp32 = 1 GiB per buffer
+C3_BYTES = 4 << 30      # 4 GiB per rank
+GIB = float(1 << 30)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline_c2(budget_s: float = 12.0) -> dict:
+    """The reference's CPU reduce (AicpuReduceTemplate<float> SUM, one core, -O3 no fast-math; restated in
+    oracle/hccl_oracle.c) over the full C2 workload, repeated within a bounded time budget."""
+    from oracle import oracle as O  # checker / baseline only
+
+    rng = np.random.default_rng(0x5EED0002)
+    src = rng.random(C2_COUNT, dtype=np.float32)
+    dst = rng.random(C2_COUNT, dtype=np.float32)
+    times = []
+    t_end = time.perf_counter() + budget_s
+    while len(times) < 3 or (time.perf_counter() < t_end and len(times) < 20):
+        t0 = time.perf_counter()
+        ret = O.aicpu_reduce(O.FP32, O.SUM, dst, src)
+        times.append(time.perf_counter() - t0)
+        assert ret == 0
+    med = float(np.median(times))
+    return {
+        "value": round(3 * C2_COUNT * 4 / med / GIB, 3),
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"full C2 workload (dst = src + dst over 2 x 1 GiB fp32), {len(times)} passes, median; "
+                  f"host {cpu_model()}, nproc {os.cpu_count()}",
+    }
+
+
+def load_pmc_traffic(name: str):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary (profiles/), if one exists for this kernel."""
+    path = os.path.join(ROOT, "profiles", name)
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def bench_local(args) -> dict:
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0x5EED0002)
+    src = torch.rand(C2_COUNT, device=dev, generator=g).mul_(2).sub_(1)
+    dst = torch.rand(C2_COUNT, device=dev, generator=g).mul_(2).sub_(1)
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        H.local_reduce(dst, src, H.HcclReduceOp.SUM, stream)
+    torch.cuda.synchronize()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    t0 = time.perf_counter()
+    evs[0].record(stream)
+    for k in range(args.steps):
+        H.local_reduce(dst, src, H.HcclReduceOp.SUM, stream)
+        evs[k + 1].record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    per = [evs[k].elapsed_time(evs[k + 1]) / 1e3 for k in range(args.steps)]
+    total = evs[0].elapsed_time(evs[-1]) / 1e3
+    bytes_step = 3 * C2_COUNT * 4
+    value = bytes_step * args.steps / total / GIB
+    kavg = float(np.mean(per))
+    achieved = bytes_step / kavg / 1e9
+    log(f"[bench] C2 local reduce: {value:.1f} GiB/s  kernel avg {kavg*1e6:.1f} us  min {min(per)*1e6:.1f} us  "
+        f"max {max(per)*1e6:.1f} us  host wall {wall:.3f} s")
+    res = {
+        "metric": "device-resident reduce GiB/s (fp32 sum) vs HBM peak; ring all-reduce bus GB/s",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(total / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (uniform [-1,1) fp32, device-generated)",
+        "config": {
+            "workload": "C2: 1-GPU local reduce dst = src + dst (HcclAmdLocalReduce), 2 x 1 GiB fp32 in HBM",
+            "count": C2_COUNT,
+            "bytes_per_step": bytes_step,
+            "parallelism": "single GPU",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": load_pmc_traffic("r01_pmc_local_reduce.json"),
+            "kernel": "k_reduce2<EFp<float>, SUM>",
+            "algorithmic_bytes_per_launch": bytes_step,
+            "kernel_avg_us": round(kavg * 1e6, 2),
+        },
+    }
+    if not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline_c2(args.cpu_budget)
+    return res
+
+
+def bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # root info out of band, exactly as the reference's callers do (examples/.../01_allreduce/main.cc:122-136)
+    obj = [H.get_root_info() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    comm = H.comm_init_root_info(world, obj[0], rank)
+    count = C3_BYTES // 4
+    g = torch.Generator(device=dev).manual_seed(0x5EED0003 + rank)
+    send = torch.rand(count, device=dev, generator=g).mul_(2).sub_(1)
+    recv = torch.empty_like(send)
+    if args.algo:
+        comm.set_algo(H.Algo[args.algo.upper()])
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        comm.all_reduce(send, recv, H.HcclReduceOp.SUM, stream)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        comm.all_reduce(send, recv, H.HcclReduceOp.SUM, stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    dist.barrier()
+    wall = time.perf_counter() - t0
+    t = torch.tensor([e0.elapsed_time(e1) / 1e3, wall], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t[0])
+    per_step = elapsed / args.steps
+    algbw = C3_BYTES / per_step / 1e9
+    busbw = algbw * 2 * (world - 1) / world
+    value = world * C3_BYTES * args.steps / elapsed / GIB
+    algo = comm.last_algo
+    comm.destroy()
+    dist.destroy_process_group()
+    res = {
+        "metric": "device-resident reduce GiB/s (fp32 sum) vs HBM peak; ring all-reduce bus GB/s",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(per_step * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (uniform [-1,1) fp32, device-generated)",
+        "config": {
+            "workload": "C3: HcclAllReduce fp32 SUM, 4 GiB per rank, RCCL send/recv over xGMI + HIP reduce kernels",
+            "bytes_per_rank": C3_BYTES,
+            "parallelism": f"allreduce x{world}",
+            "algorithm": H.Algo(algo).name if algo >= 0 else None,
+        },
+        "busbw_GBps": round(busbw, 2),
+        "algbw_GBps": round(algbw, 2),
+        "roofline": {
+            "bound": "xgmi",
+            "achieved": round(busbw, 2),
+            "peak": 7 * 153.6 / 2,
+            "unit": "GB/s",
+            "frac": round(busbw / (7 * 153.6 / 2), 4),
+            "traffic": None,
+            "note": "busbw = algbw*2(n-1)/n against 7 xGMI links x 76.8 GB/s per direction",
+        },
+    }
+    return res if rank == 0 else None
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-budget", type=float, default=12.0)
+    p.add_argument("--algo", default="", help="force an AllReduce schedule (mesh_oneshot/mesh_twoshot/ring/rhd)")
+    args = p.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        rank = int(os.environ["RANK"])
+        res = bench_allreduce(args, rank, world, int(os.environ.get("LOCAL_RANK", rank)))
+    else:
+        res = bench_local(args)
+    if res is not None:
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,180 @@
+"""hccl_amd — MI355X-native HCCL reduce path (HcclAllReduce / HcclReduceScatter / HcclReduce).
+
+The product is libhccl_amd.so: HIP kernels for gfx950 plus a C++ runtime (schedules, executor, RCCL transport)
+behind the reference's C ABI (include/hccl.h). This Python module is a thin ctypes mirror of that ABI for tests
+and benchmarks; torch supplies device memory and streams only. Names, argument meaning and return codes are the
+C ABI's; every call raises HcclError on a non-success code.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence
+
+import torch
+
+from ._lib import (  # noqa: F401
+    Algo,
+    HcclAmdIrOp,
+    HcclDataType,
+    HcclError,
+    HcclReduceOp,
+    HcclResult,
+    HcclRootInfo,
+    IrKind,
+    OpType,
+    HCCL_ROOT_INFO_BYTES,
+    IR_MAX_SRC,
+    LIB_PATH,
+    SIGNATURES,
+    check,
+    lib,
+)
+
+TORCH_TO_HCCL = {
+    torch.int8: HcclDataType.INT8,
+    torch.int16: HcclDataType.INT16,
+    torch.int32: HcclDataType.INT32,
+    torch.int64: HcclDataType.INT64,
+    torch.uint64: HcclDataType.UINT64,
+    torch.float16: HcclDataType.FP16,
+    torch.bfloat16: HcclDataType.BFP16,
+    torch.float32: HcclDataType.FP32,
+    torch.float64: HcclDataType.FP64,
+}
+
+
+def hccl_dtype(t: torch.Tensor) -> HcclDataType:
+    try:
+        return TORCH_TO_HCCL[t.dtype]
+    except KeyError:
+        raise TypeError(f"no HcclDataType for {t.dtype}") from None
+
+
+def _stream(stream: Optional[torch.cuda.Stream]) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+# ----------------------------------------------------------------------------------------- local reduce primitive
+
+
+def local_reduce(dst: torch.Tensor, src: torch.Tensor, op: int = HcclReduceOp.SUM, stream=None) -> None:
+    """dst = src (op) dst on the GPU (HcclAmdLocalReduce = HcommLocalReduceOnThread)."""
+    assert dst.numel() == src.numel() and dst.dtype == src.dtype
+    check("HcclAmdLocalReduce",
+          lib.HcclAmdLocalReduce(_ptr(dst), _ptr(src), dst.numel(), hccl_dtype(dst), int(op), _stream(stream)))
+
+
+def local_reduce2(out: torch.Tensor, src: torch.Tensor, dst: torch.Tensor, op: int = HcclReduceOp.SUM,
+                  stream=None) -> None:
+    """out = src (op) dst."""
+    assert out.numel() == src.numel() == dst.numel()
+    check("HcclAmdLocalReduce2",
+          lib.HcclAmdLocalReduce2(_ptr(out), _ptr(src), _ptr(dst), out.numel(), hccl_dtype(out), int(op),
+                                  _stream(stream)))
+
+
+def local_reduce_n(out: torch.Tensor, srcs: Sequence[torch.Tensor], op: int = HcclReduceOp.SUM, stream=None) -> None:
+    """acc = srcs[0]; acc = srcs[j] (op) acc; out = acc."""
+    arr = (ctypes.c_void_p * len(srcs))(*[s.data_ptr() for s in srcs])
+    check("HcclAmdLocalReduceN",
+          lib.HcclAmdLocalReduceN(_ptr(out), arr, len(srcs), out.numel(), hccl_dtype(out), int(op), _stream(stream)))
+
+
+def set_reduce_launch(blocks_per_cu: int = 0, unroll: int = 0, cache_policy: int = 0) -> None:
+    """0 restores each default; see HcclAmdSetReduceLaunch in include/hccl_amd.h."""
+    check("HcclAmdSetReduceLaunch", lib.HcclAmdSetReduceLaunch(blocks_per_cu, unroll, cache_policy))
+
+
+# ----------------------------------------------------------------------------------------- schedules
+
+
+def build_schedule(op_type: int, algo: int, n_ranks: int, rank: int, count: int, dtype: int, root: int = 0,
+                   piece_bytes: int = 0):
+    """Returns (ops: ctypes array of HcclAmdIrOp, algo_used, scratch_elems)."""
+    nops = ctypes.c_uint64(0)
+    used = ctypes.c_int32(-1)
+    scratch = ctypes.c_uint64(0)
+    check("HcclAmdBuildSchedule",
+          lib.HcclAmdBuildSchedule(op_type, algo, n_ranks, rank, count, int(dtype), root, piece_bytes, None, 0,
+                                   ctypes.byref(nops), ctypes.byref(used), ctypes.byref(scratch)))
+    arr = (HcclAmdIrOp * max(1, nops.value))()
+    check("HcclAmdBuildSchedule",
+          lib.HcclAmdBuildSchedule(op_type, algo, n_ranks, rank, count, int(dtype), root, piece_bytes, arr,
+                                   nops.value, ctypes.byref(nops), ctypes.byref(used), ctypes.byref(scratch)))
+    return arr, nops.value, used.value, scratch.value
+
+
+# ----------------------------------------------------------------------------------------- communicators
+
+
+class Comm:
+    """An HcclComm handle (RCCL-backed, or one rank of a loopback world)."""
+
+    def __init__(self, handle: int):
+        self.handle = ctypes.c_void_p(handle)
+
+    @property
+    def rank(self) -> int:
+        v = ctypes.c_uint32(0)
+        check("HcclGetRankId", lib.HcclGetRankId(self.handle, ctypes.byref(v)))
+        return v.value
+
+    @property
+    def size(self) -> int:
+        v = ctypes.c_uint32(0)
+        check("HcclGetRankSize", lib.HcclGetRankSize(self.handle, ctypes.byref(v)))
+        return v.value
+
+    def set_algo(self, algo: int) -> None:
+        check("HcclAmdCommSetAlgo", lib.HcclAmdCommSetAlgo(self.handle, int(algo)))
+
+    def set_piece_bytes(self, nbytes: int) -> None:
+        check("HcclAmdCommSetPieceBytes", lib.HcclAmdCommSetPieceBytes(self.handle, nbytes))
+
+    @property
+    def last_algo(self) -> int:
+        return lib.HcclAmdCommLastAlgo(self.handle)
+
+    def all_reduce(self, send: torch.Tensor, recv: torch.Tensor, op: int = HcclReduceOp.SUM, stream=None) -> None:
+        check("HcclAllReduce", lib.HcclAllReduce(_ptr(send), _ptr(recv), send.numel(), hccl_dtype(send), int(op),
+                                                 self.handle, _stream(stream)))
+
+    def reduce_scatter(self, send: torch.Tensor, recv: torch.Tensor, op: int = HcclReduceOp.SUM,
+                       stream=None) -> None:
+        check("HcclReduceScatter", lib.HcclReduceScatter(_ptr(send), _ptr(recv), recv.numel(), hccl_dtype(send),
+                                                         int(op), self.handle, _stream(stream)))
+
+    def reduce(self, send: torch.Tensor, recv: torch.Tensor, root: int, op: int = HcclReduceOp.SUM,
+               stream=None) -> None:
+        check("HcclReduce", lib.HcclReduce(_ptr(send), _ptr(recv), send.numel(), hccl_dtype(send), int(op), root,
+                                           self.handle, _stream(stream)))
+
+    def destroy(self) -> None:
+        if self.handle:
+            check("HcclCommDestroy", lib.HcclCommDestroy(self.handle))
+            self.handle = ctypes.c_void_p(0)
+
+
+def get_root_info() -> bytes:
+    ri = HcclRootInfo()
+    check("HcclGetRootInfo", lib.HcclGetRootInfo(ctypes.byref(ri)))
+    return bytes(ctypes.string_at(ctypes.addressof(ri), HCCL_ROOT_INFO_BYTES))
+
+
+def comm_init_root_info(n_ranks: int, root_info: bytes, rank: int) -> Comm:
+    ri = HcclRootInfo()
+    ctypes.memmove(ctypes.addressof(ri), root_info, HCCL_ROOT_INFO_BYTES)
+    h = ctypes.c_void_p(0)
+    check("HcclCommInitRootInfo", lib.HcclCommInitRootInfo(n_ranks, ctypes.byref(ri), rank, ctypes.byref(h)))
+    return Comm(h.value)
+
+
+def loopback_world(n_ranks: int) -> List[Comm]:
+    arr = (ctypes.c_void_p * n_ranks)()
+    check("HcclAmdCommInitLoopback", lib.HcclAmdCommInitLoopback(n_ranks, arr))
+    return [Comm(arr[i]) for i in range(n_ranks)]

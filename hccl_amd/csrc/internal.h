@@ -1,0 +1,60 @@
+// internal.h — shared declarations of libhccl_amd.so (not installed; the public ABI is include/*.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+#include "../../include/hccl.h"
+#include "../../include/hccl_amd.h"
+
+namespace hccl_amd {
+
+// Reduce ops in the same numbering as HcclReduceOp.
+enum ROp : int { R_SUM = 0, R_PROD = 1, R_MAX = 2, R_MIN = 3 };
+
+// Element size of each HcclDataType (alg_param.h:43-61 DATATYPE_SIZE_TABLE); 0 = unknown.
+uint32_t DataTypeSize(HcclDataType dt);
+
+// True for the dtypes the reduce ops accept (op_common.cc:2913-2957 CheckDataType(needReduce=true)).
+bool IsReduceDataType(HcclDataType dt);
+
+// ---- streaming reduce kernels (reduce_kernels.hip)
+// out = src (op) dst, element-wise.
+HcclResult LaunchReduce2(void* out, const void* src, const void* dst, uint64_t count, HcclDataType dt,
+                         HcclReduceOp op, hipStream_t stream);
+// out = fold(srcs[0..n)) with acc = srcs[j] (op) acc.
+HcclResult LaunchReduceN(void* out, const void* const* srcs, uint32_t n, uint64_t count, HcclDataType dt,
+                         HcclReduceOp op, hipStream_t stream);
+HcclResult SetReduceLaunch(uint32_t blocksPerCu, uint32_t unroll, uint32_t cachePolicy);
+
+// ---- logging
+bool DebugEnabled();
+
+}  // namespace hccl_amd
+
+#define HCCL_AMD_LOG(fmt, ...)                                                                   \
+    do {                                                                                         \
+        if (hccl_amd::DebugEnabled()) {                                                          \
+            std::fprintf(stderr, "[hccl_amd] %s:%d " fmt "\n", __FILE__, __LINE__, ##__VA_ARGS__); \
+        }                                                                                        \
+    } while (0)
+
+#define HCCL_AMD_ERR(fmt, ...) std::fprintf(stderr, "[hccl_amd][ERROR] %s:%d " fmt "\n", __FILE__, __LINE__, ##__VA_ARGS__)
+
+#define HIP_CHK(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess) {                                                            \
+            HCCL_AMD_ERR("%s failed: %s", #expr, hipGetErrorString(e_));                   \
+            return HCCL_E_RUNTIME;                                                         \
+        }                                                                                  \
+    } while (0)
+
+#define HCCL_CHK(expr)                     \
+    do {                                   \
+        HcclResult r_ = (expr);            \
+        if (r_ != HCCL_SUCCESS) return r_; \
+    } while (0)

@@ -1,0 +1,628 @@
+// reduce_kernels.hip — the element-wise reduce at the bottom of every HCCL reducing schedule, for CDNA4 (gfx950).
+//
+// Replaces:
+//   AicpuReduceTemplate<T> / AicpuReduceFp16 / AicpuReduce  alg_data_trans_wrapper.cc:1232-1353 (CPU scalar loop)
+//   LocalReduce -> HcommLocalReduceOnThread                  alg_data_trans_wrapper.cc:901-928 (external SDMA task)
+//   AivCommBase::CpGM2GM(atomic) / Reduce64                  aiv_communication_base_v2.h:527-616 (AIV vector core)
+//
+// This is a pure HBM stream (1 flop per 12 B for fp32), so the design is about bytes in flight, not math:
+//   * every lane moves 16-B vectors (global_load_dwordx4 / global_store_dwordx4), a wave 1 KiB per instruction;
+//   * each lane issues all U loads of both operands of a tile before the first combine (2*U*16 B in flight per lane);
+//   * a persistent grid of blocksPerCu x CUs workgroups of 256 threads walks the tiles (grid-stride), so the launch
+//     is a fixed ~1-2k workgroups whatever the size;
+//   * optional non-temporal loads/stores (nt bit) for once-touched streams;
+//   * no LDS: staging a pure stream through LDS adds a round trip and buys no reuse (measured in DESIGN.md).
+// Element rules are AicpuReduceTemplate's: dst = src (op) dst with std::max/std::min operand semantics (ties and NaN
+// yield src), integer SUM/PROD wrap, fp16/bf16 computed as fp32 then rounded to nearest even. No fast-math: fp32
+// denormals are preserved (checked in the code object: .amdhsa_float_denorm_mode_32 = 3).
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstring>
+#include <mutex>
+
+#include "internal.h"
+
+namespace hccl_amd {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------------ element rules
+
+template <typename T, typename W>
+struct EInt {
+    using S = T;
+    template <int OP>
+    static __device__ __forceinline__ T ap(T s, T d)
+    {
+        if constexpr (OP == R_SUM) {
+            return static_cast<T>(static_cast<W>(static_cast<W>(s) + static_cast<W>(d)));
+        } else if constexpr (OP == R_PROD) {
+            return static_cast<T>(static_cast<W>(static_cast<W>(s) * static_cast<W>(d)));
+        } else if constexpr (OP == R_MAX) {
+            return (s < d) ? d : s;
+        } else {
+            return (d < s) ? d : s;
+        }
+    }
+};
+
+template <typename T>
+struct EFp {
+    using S = T;
+    template <int OP>
+    static __device__ __forceinline__ T ap(T s, T d)
+    {
+        if constexpr (OP == R_SUM) {
+            return s + d;
+        } else if constexpr (OP == R_PROD) {
+            return s * d;
+        } else if constexpr (OP == R_MAX) {
+            return (s < d) ? d : s;
+        } else {
+            return (d < s) ? d : s;
+        }
+    }
+};
+
+// fp16: a native half add/mul is correctly rounded, which equals the reference's fp32-compute + RNE narrowing
+// (11-bit significands: 24 >= 2*11+2, so the double rounding is innocuous; products are exact in fp32).
+// MAX/MIN compare (exact) and return the selected operand's bits, as the reference's round trip does.
+struct EF16 {
+    using S = uint16_t;
+    template <int OP>
+    static __device__ __forceinline__ uint16_t ap(uint16_t s, uint16_t d)
+    {
+        _Float16 hs = __builtin_bit_cast(_Float16, s);
+        _Float16 hd = __builtin_bit_cast(_Float16, d);
+        if constexpr (OP == R_SUM) {
+            return __builtin_bit_cast(uint16_t, static_cast<_Float16>(hs + hd));
+        } else if constexpr (OP == R_PROD) {
+            return __builtin_bit_cast(uint16_t, static_cast<_Float16>(hs * hd));
+        } else if constexpr (OP == R_MAX) {
+            return (hs < hd) ? d : s;
+        } else {
+            return (hd < hs) ? d : s;
+        }
+    }
+};
+
+// bf16: fp32 compute, round to nearest even (no in-tree reference arithmetic: parity unpinned, SURVEY §8a').
+struct EBF16 {
+    using S = uint16_t;
+    static __device__ __forceinline__ float widen(uint16_t b) { return __builtin_bit_cast(float, uint32_t(b) << 16); }
+    static __device__ __forceinline__ uint16_t narrow(float f)
+    {
+        uint32_t u = __builtin_bit_cast(uint32_t, f);
+        if ((u & 0x7FFFFFFFu) > 0x7F800000u) {
+            return static_cast<uint16_t>((u >> 16) | 0x0040u);
+        }
+        u += 0x7FFFu + ((u >> 16) & 1u);
+        return static_cast<uint16_t>(u >> 16);
+    }
+    template <int OP>
+    static __device__ __forceinline__ uint16_t ap(uint16_t s, uint16_t d)
+    {
+        float fs = widen(s);
+        float fd = widen(d);
+        if constexpr (OP == R_SUM) {
+            return narrow(fs + fd);
+        } else if constexpr (OP == R_PROD) {
+            return narrow(fs * fd);
+        } else if constexpr (OP == R_MAX) {
+            return (fs < fd) ? d : s;
+        } else {
+            return (fd < fs) ? d : s;
+        }
+    }
+};
+
+template <class E, int OP>
+__device__ __forceinline__ u32x4 combine(u32x4 s, u32x4 d)
+{
+    using S = typename E::S;
+    constexpr int N = 16 / sizeof(S);
+    S a[N];
+    S b[N];
+    __builtin_memcpy(a, &s, 16);
+    __builtin_memcpy(b, &d, 16);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        a[i] = E::template ap<OP>(a[i], b[i]);
+    }
+    u32x4 r;
+    __builtin_memcpy(&r, a, 16);
+    return r;
+}
+
+// NT is a bit set: bit 0 = non-temporal loads, bit 1 = non-temporal stores.
+template <int NT>
+__device__ __forceinline__ u32x4 ld(const u32x4* p)
+{
+    if constexpr ((NT & 1) != 0) {
+        return __builtin_nontemporal_load(p);
+    } else {
+        return *p;
+    }
+}
+
+template <int NT>
+__device__ __forceinline__ void st(u32x4* p, u32x4 v)
+{
+    if constexpr ((NT & 2) != 0) {
+        __builtin_nontemporal_store(v, p);
+    } else {
+        *p = v;
+    }
+}
+
+// Scalar elements outside the 16-B aligned body (head < 16 B before it, tail < 16 B after it): done by block 0.
+struct Edges {
+    uint32_t head;  // elements before the vector body
+    uint32_t tail;  // elements after it
+    uint64_t tailStart;
+};
+
+constexpr int kBlock = 256;
+
+// ------------------------------------------------------------------------------------------------ out = src (op) dst
+
+// ORD 0: tiles dealt round-robin to the persistent grid (the chip-wide access front stays a few MiB wide);
+// ORD 1: each workgroup walks one contiguous run of tiles.
+template <int ORD>
+struct TileRange {
+    uint64_t begin, end, step;
+    __device__ TileRange(uint64_t fullTiles)
+    {
+        if constexpr (ORD == 0) {
+            begin = blockIdx.x;
+            end = fullTiles;
+            step = gridDim.x;
+        } else {
+            uint64_t per = (fullTiles + gridDim.x - 1) / gridDim.x;
+            begin = uint64_t(blockIdx.x) * per;
+            end = begin + per < fullTiles ? begin + per : fullTiles;
+            step = 1;
+        }
+    }
+};
+
+template <class E, int OP, int U, int NT, int ORD>
+__global__ __launch_bounds__(kBlock) void k_reduce2(typename E::S* out, const typename E::S* src,
+                                                      const typename E::S* dst, uint64_t nvec, Edges edges)
+{
+    constexpr uint64_t kTile = uint64_t(kBlock) * U;
+    // vector body starts after the head elements
+    u32x4* vout = reinterpret_cast<u32x4*>(out + edges.head);
+    const u32x4* vsrc = reinterpret_cast<const u32x4*>(src + edges.head);
+    const u32x4* vdst = reinterpret_cast<const u32x4*>(dst + edges.head);
+    const uint64_t fullTiles = nvec / kTile;
+    const TileRange<ORD> tr(fullTiles);
+    for (uint64_t t = tr.begin; t < tr.end; t += tr.step) {
+        const uint64_t base = t * kTile + threadIdx.x;
+        u32x4 a[U];
+        u32x4 b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            a[u] = ld<NT>(vsrc + base + u * kBlock);
+            b[u] = ld<NT>(vdst + base + u * kBlock);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            st<NT>(vout + base + u * kBlock, combine<E, OP>(a[u], b[u]));
+        }
+    }
+    for (uint64_t i = fullTiles * kTile + uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < nvec;
+         i += uint64_t(gridDim.x) * kBlock) {
+        st<NT>(vout + i, combine<E, OP>(ld<NT>(vsrc + i), ld<NT>(vdst + i)));
+    }
+    if (blockIdx.x == 0) {
+        uint32_t tid = threadIdx.x;
+        if (tid < edges.head) {
+            out[tid] = E::template ap<OP>(src[tid], dst[tid]);
+        } else if (tid >= 64 && tid - 64 < edges.tail) {
+            uint64_t i = edges.tailStart + (tid - 64);
+            out[i] = E::template ap<OP>(src[i], dst[i]);
+        }
+    }
+}
+
+// Fallback when the three pointers are not congruent modulo 16 B: one element per lane, grid-stride.
+template <class E, int OP>
+__global__ __launch_bounds__(kBlock) void k_reduce2_scalar(typename E::S* out, const typename E::S* src,
+                                                             const typename E::S* dst, uint64_t count)
+{
+    for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < count; i += uint64_t(gridDim.x) * kBlock) {
+        out[i] = E::template ap<OP>(src[i], dst[i]);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ ordered n-ary fold
+
+struct SrcPack {
+    const void* p[HCCL_AMD_IR_MAX_SRC];
+};
+
+template <class E, int OP, int U, int NT>
+__global__ __launch_bounds__(kBlock) void k_reduceN(typename E::S* out, SrcPack srcs, int nsrc, uint64_t nvec,
+                                                      Edges edges)
+{
+    using S = typename E::S;
+    constexpr uint64_t kTile = uint64_t(kBlock) * U;
+    u32x4* vout = reinterpret_cast<u32x4*>(out + edges.head);
+    const uint64_t fullTiles = nvec / kTile;
+    for (uint64_t t = blockIdx.x; t < fullTiles; t += gridDim.x) {
+        const uint64_t base = t * kTile + threadIdx.x;
+        u32x4 acc[U];
+        const u32x4* p0 = reinterpret_cast<const u32x4*>(static_cast<const S*>(srcs.p[0]) + edges.head);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            acc[u] = ld<NT>(p0 + base + u * kBlock);
+        }
+        for (int j = 1; j < nsrc; ++j) {
+            const u32x4* pj = reinterpret_cast<const u32x4*>(static_cast<const S*>(srcs.p[j]) + edges.head);
+            u32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                v[u] = ld<NT>(pj + base + u * kBlock);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                acc[u] = combine<E, OP>(v[u], acc[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            st<NT>(vout + base + u * kBlock, acc[u]);
+        }
+    }
+    for (uint64_t i = fullTiles * kTile + uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < nvec;
+         i += uint64_t(gridDim.x) * kBlock) {
+        u32x4 acc = ld<NT>(reinterpret_cast<const u32x4*>(static_cast<const S*>(srcs.p[0]) + edges.head) + i);
+        for (int j = 1; j < nsrc; ++j) {
+            acc = combine<E, OP>(ld<NT>(reinterpret_cast<const u32x4*>(static_cast<const S*>(srcs.p[j]) + edges.head) + i),
+                                 acc);
+        }
+        st<NT>(vout + i, acc);
+    }
+    if (blockIdx.x == 0) {
+        uint32_t tid = threadIdx.x;
+        uint64_t i;
+        bool act = false;
+        if (tid < edges.head) {
+            i = tid;
+            act = true;
+        } else if (tid >= 64 && tid - 64 < edges.tail) {
+            i = edges.tailStart + (tid - 64);
+            act = true;
+        }
+        if (act) {
+            S acc = static_cast<const S*>(srcs.p[0])[i];
+            for (int j = 1; j < nsrc; ++j) {
+                acc = E::template ap<OP>(static_cast<const S*>(srcs.p[j])[i], acc);
+            }
+            out[i] = acc;
+        }
+    }
+}
+
+template <class E, int OP>
+__global__ __launch_bounds__(kBlock) void k_reduceN_scalar(typename E::S* out, SrcPack srcs, int nsrc, uint64_t count)
+{
+    using S = typename E::S;
+    for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < count; i += uint64_t(gridDim.x) * kBlock) {
+        S acc = static_cast<const S*>(srcs.p[0])[i];
+        for (int j = 1; j < nsrc; ++j) {
+            acc = E::template ap<OP>(static_cast<const S*>(srcs.p[j])[i], acc);
+        }
+        out[i] = acc;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ host launch
+
+namespace {
+
+// Launch shape of one kernel family: workgroups per CU in the persistent grid, 16-B vectors per lane per
+// operand per iteration (U), cache policy bits (NT) and tile order (ORD).
+struct LaunchCfg {
+    uint32_t blocksPerCu;
+    uint32_t unroll;
+    uint32_t nt;
+    uint32_t order;
+};
+
+// 0 = "use the default" for every field.
+std::atomic<uint32_t> g_blocksPerCu{0};
+std::atomic<uint32_t> g_unroll{0};
+std::atomic<uint32_t> g_policy{0};
+std::atomic<uint32_t> g_order{0};
+
+// Defaults from the interleaved launch sweep on MI355X (tools/sweep_local.py): the HBM stream
+// peaks with ~16 KiB of loads in flight per CU (2 workgroups x 256 lanes x 2 operands x 16 B) and nt loads+stores;
+// more bytes in flight lowers throughput.
+constexpr LaunchCfg kDefault2{2, 1, 3, 0};
+constexpr LaunchCfg kDefaultN{2, 2, 3, 0};
+
+LaunchCfg CurrentCfg(const LaunchCfg& dflt)
+{
+    LaunchCfg c;
+    c.blocksPerCu = g_blocksPerCu.load(std::memory_order_relaxed);
+    c.unroll = g_unroll.load(std::memory_order_relaxed);
+    uint32_t pol = g_policy.load(std::memory_order_relaxed);
+    uint32_t ord = g_order.load(std::memory_order_relaxed);
+    if (c.blocksPerCu == 0) c.blocksPerCu = dflt.blocksPerCu;
+    if (c.unroll == 0) c.unroll = dflt.unroll;
+    c.nt = pol == 0 ? dflt.nt : pol - 1;
+    c.order = ord == 0 ? dflt.order : ord - 1;
+    return c;
+}
+
+int CuCount()
+{
+    static std::mutex mu;
+    static int cached[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+        return 256;
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    if (cached[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) {
+            n = 256;
+        }
+        cached[dev] = n;
+    }
+    return cached[dev];
+}
+
+uint32_t GridFor(uint64_t work, uint32_t perBlock, const LaunchCfg& cfg)
+{
+    uint64_t need = (work + perBlock - 1) / perBlock;
+    uint64_t cap = uint64_t(CuCount()) * cfg.blocksPerCu;
+    if (need > cap) need = cap;
+    if (need == 0) need = 1;
+    return static_cast<uint32_t>(need);
+}
+
+// Split [0, count) into head / 16-B vector body / tail for pointers that share one alignment phase.
+template <typename S>
+bool SplitAligned(const void* const* ptrs, int n, uint64_t count, Edges* e, uint64_t* nvec)
+{
+    constexpr uint64_t kVec = 16 / sizeof(S);
+    uintptr_t phase = reinterpret_cast<uintptr_t>(ptrs[0]) & 15u;
+    for (int i = 1; i < n; ++i) {
+        if ((reinterpret_cast<uintptr_t>(ptrs[i]) & 15u) != phase) return false;
+    }
+    if (phase % sizeof(S) != 0) return false;
+    uint64_t head = phase == 0 ? 0 : (16 - phase) / sizeof(S);
+    if (head > count) head = count;
+    uint64_t rest = count - head;
+    *nvec = rest / kVec;
+    e->head = static_cast<uint32_t>(head);
+    e->tailStart = head + *nvec * kVec;
+    e->tail = static_cast<uint32_t>(count - e->tailStart);
+    return true;
+}
+
+template <class E, int OP, int U, int NT, int ORD = 0>
+hipError_t Run2Variant(void* out, const void* src, const void* dst, uint64_t nvec, Edges edges, uint32_t grid,
+                       hipStream_t stream)
+{
+    using S = typename E::S;
+    hipLaunchKernelGGL((k_reduce2<E, OP, U, NT, ORD>), dim3(grid), dim3(kBlock), 0, stream, static_cast<S*>(out),
+                       static_cast<const S*>(src), static_cast<const S*>(dst), nvec, edges);
+    return hipGetLastError();
+}
+
+template <class E, int OP, int U, int NT>
+hipError_t RunNVariant(void* out, const SrcPack& pk, int n, uint64_t nvec, Edges edges, uint32_t grid,
+                       hipStream_t stream)
+{
+    using S = typename E::S;
+    hipLaunchKernelGGL((k_reduceN<E, OP, U, NT>), dim3(grid), dim3(kBlock), 0, stream, static_cast<S*>(out), pk, n,
+                       nvec, edges);
+    return hipGetLastError();
+}
+
+// fp32 SUM (the headline path) carries every tuning variant; other (dtype, op) pairs are built at the default.
+template <class E, int OP>
+constexpr bool kTunable = std::is_same<E, EFp<float>>::value && OP == R_SUM;
+
+template <class E, int OP, int U>
+hipError_t Run2U(const LaunchCfg& c, void* out, const void* src, const void* dst, uint64_t nvec, Edges edges,
+                 uint32_t grid, hipStream_t stream)
+{
+    switch (c.nt + 4 * c.order) {
+        case 0: return Run2Variant<E, OP, U, 0, 0>(out, src, dst, nvec, edges, grid, stream);
+        case 1: return Run2Variant<E, OP, U, 1, 0>(out, src, dst, nvec, edges, grid, stream);
+        case 2: return Run2Variant<E, OP, U, 2, 0>(out, src, dst, nvec, edges, grid, stream);
+        case 3: return Run2Variant<E, OP, U, 3, 0>(out, src, dst, nvec, edges, grid, stream);
+        case 7: return Run2Variant<E, OP, U, 3, 1>(out, src, dst, nvec, edges, grid, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <class E, int OP>
+hipError_t Run2(void* out, const void* src, const void* dst, uint64_t count, hipStream_t stream)
+{
+    using S = typename E::S;
+    LaunchCfg cfg = CurrentCfg(kDefault2);
+    const void* ptrs[3] = {out, src, dst};
+    Edges edges{};
+    uint64_t nvec = 0;
+    if (!SplitAligned<S>(ptrs, 3, count, &edges, &nvec)) {
+        uint32_t grid = GridFor(count, kBlock * 4, cfg);
+        hipLaunchKernelGGL((k_reduce2_scalar<E, OP>), dim3(grid), dim3(kBlock), 0, stream, static_cast<S*>(out),
+                           static_cast<const S*>(src), static_cast<const S*>(dst), count);
+        return hipGetLastError();
+    }
+    if constexpr (kTunable<E, OP>) {
+        uint32_t grid = GridFor(nvec, kBlock * cfg.unroll, cfg);
+        switch (cfg.unroll) {
+            case 1: return Run2U<E, OP, 1>(cfg, out, src, dst, nvec, edges, grid, stream);
+            case 2: return Run2U<E, OP, 2>(cfg, out, src, dst, nvec, edges, grid, stream);
+            case 4: return Run2U<E, OP, 4>(cfg, out, src, dst, nvec, edges, grid, stream);
+            case 8: return Run2U<E, OP, 8>(cfg, out, src, dst, nvec, edges, grid, stream);
+            default: return hipErrorInvalidValue;
+        }
+    } else {
+        uint32_t grid = GridFor(nvec, kBlock * kDefault2.unroll, cfg);
+        return Run2Variant<E, OP, kDefault2.unroll, kDefault2.nt>(out, src, dst, nvec, edges, grid, stream);
+    }
+}
+
+template <class E, int OP>
+hipError_t RunN(void* out, const void* const* srcs, uint32_t n, uint64_t count, hipStream_t stream)
+{
+    using S = typename E::S;
+    LaunchCfg cfg = CurrentCfg(kDefaultN);
+    SrcPack pk{};
+    const void* ptrs[HCCL_AMD_IR_MAX_SRC + 1];
+    ptrs[0] = out;
+    for (uint32_t j = 0; j < n; ++j) {
+        pk.p[j] = srcs[j];
+        ptrs[j + 1] = srcs[j];
+    }
+    Edges edges{};
+    uint64_t nvec = 0;
+    if (!SplitAligned<S>(ptrs, int(n) + 1, count, &edges, &nvec)) {
+        uint32_t grid = GridFor(count, kBlock * 4, cfg);
+        hipLaunchKernelGGL((k_reduceN_scalar<E, OP>), dim3(grid), dim3(kBlock), 0, stream, static_cast<S*>(out), pk,
+                           int(n), count);
+        return hipGetLastError();
+    }
+    if constexpr (kTunable<E, OP>) {
+        uint32_t grid = GridFor(nvec, kBlock * cfg.unroll, cfg);
+        switch (cfg.unroll * 4 + cfg.nt) {
+            case 4 + 0: return RunNVariant<E, OP, 1, 0>(out, pk, int(n), nvec, edges, grid, stream);
+            case 4 + 3: return RunNVariant<E, OP, 1, 3>(out, pk, int(n), nvec, edges, grid, stream);
+            case 8 + 0: return RunNVariant<E, OP, 2, 0>(out, pk, int(n), nvec, edges, grid, stream);
+            case 8 + 3: return RunNVariant<E, OP, 2, 3>(out, pk, int(n), nvec, edges, grid, stream);
+            case 16 + 0: return RunNVariant<E, OP, 4, 0>(out, pk, int(n), nvec, edges, grid, stream);
+            case 16 + 3: return RunNVariant<E, OP, 4, 3>(out, pk, int(n), nvec, edges, grid, stream);
+            default: return hipErrorInvalidValue;
+        }
+    } else {
+        uint32_t grid = GridFor(nvec, kBlock * kDefaultN.unroll, cfg);
+        return RunNVariant<E, OP, kDefaultN.unroll, kDefaultN.nt>(out, pk, int(n), nvec, edges, grid, stream);
+    }
+}
+
+template <class E>
+hipError_t Dispatch2(int op, void* out, const void* src, const void* dst, uint64_t count, hipStream_t s)
+{
+    switch (op) {
+        case R_SUM: return Run2<E, R_SUM>(out, src, dst, count, s);
+        case R_PROD: return Run2<E, R_PROD>(out, src, dst, count, s);
+        case R_MAX: return Run2<E, R_MAX>(out, src, dst, count, s);
+        default: return Run2<E, R_MIN>(out, src, dst, count, s);
+    }
+}
+
+template <class E>
+hipError_t DispatchN(int op, void* out, const void* const* srcs, uint32_t n, uint64_t count, hipStream_t s)
+{
+    switch (op) {
+        case R_SUM: return RunN<E, R_SUM>(out, srcs, n, count, s);
+        case R_PROD: return RunN<E, R_PROD>(out, srcs, n, count, s);
+        case R_MAX: return RunN<E, R_MAX>(out, srcs, n, count, s);
+        default: return RunN<E, R_MIN>(out, srcs, n, count, s);
+    }
+}
+
+using EI8 = EInt<int8_t, uint32_t>;
+using EI16 = EInt<int16_t, uint32_t>;
+using EI32 = EInt<int32_t, uint32_t>;
+using EI64 = EInt<int64_t, uint64_t>;
+using EU64 = EInt<uint64_t, uint64_t>;
+using EF32 = EFp<float>;
+using EF64 = EFp<double>;
+
+bool ValidOp(HcclReduceOp op) { return op >= HCCL_REDUCE_SUM && op <= HCCL_REDUCE_MIN; }
+
+}  // namespace
+
+HcclResult SetReduceLaunch(uint32_t blocksPerCu, uint32_t unroll, uint32_t cachePolicy)
+{
+    // cachePolicy: 0 = default, 1 = plain, 2 = nt loads, 3 = nt stores, 4 = nt loads + stores,
+    //              5 = nt loads + stores with contiguous per-workgroup tile runs (ORD 1)
+    if (blocksPerCu > 32 || (unroll != 0 && unroll != 1 && unroll != 2 && unroll != 4 && unroll != 8) ||
+        cachePolicy > 5) {
+        return HCCL_E_PARA;
+    }
+    g_blocksPerCu.store(blocksPerCu);
+    g_unroll.store(unroll);
+    if (cachePolicy == 5) {
+        g_policy.store(4);
+        g_order.store(2);
+    } else {
+        g_policy.store(cachePolicy);
+        g_order.store(cachePolicy == 0 ? 0 : 1);
+    }
+    return HCCL_SUCCESS;
+}
+
+HcclResult LaunchReduce2(void* out, const void* src, const void* dst, uint64_t count, HcclDataType dt,
+                         HcclReduceOp op, hipStream_t stream)
+{
+    if (count == 0) return HCCL_SUCCESS;
+    if (!ValidOp(op)) return HCCL_E_PARA;
+    hipError_t e;
+    switch (dt) {
+        case HCCL_DATA_TYPE_INT8: e = Dispatch2<EI8>(op, out, src, dst, count, stream); break;
+        case HCCL_DATA_TYPE_INT16: e = Dispatch2<EI16>(op, out, src, dst, count, stream); break;
+        case HCCL_DATA_TYPE_INT32: e = Dispatch2<EI32>(op, out, src, dst, count, stream); break;
+        case HCCL_DATA_TYPE_INT64: e = Dispatch2<EI64>(op, out, src, dst, count, stream); break;
+        case HCCL_DATA_TYPE_UINT64: e = Dispatch2<EU64>(op, out, src, dst, count, stream); break;
+        case HCCL_DATA_TYPE_FP16: e = Dispatch2<EF16>(op, out, src, dst, count, stream); break;
+        case HCCL_DATA_TYPE_BFP16: e = Dispatch2<EBF16>(op, out, src, dst, count, stream); break;
+        case HCCL_DATA_TYPE_FP32: e = Dispatch2<EF32>(op, out, src, dst, count, stream); break;
+        case HCCL_DATA_TYPE_FP64: e = Dispatch2<EF64>(op, out, src, dst, count, stream); break;
+        default: return HCCL_E_NOT_SUPPORT;
+    }
+    if (e != hipSuccess) {
+        HCCL_AMD_ERR("reduce launch failed: %s", hipGetErrorString(e));
+        return HCCL_E_RUNTIME;
+    }
+    return HCCL_SUCCESS;
+}
+
+HcclResult LaunchReduceN(void* out, const void* const* srcs, uint32_t n, uint64_t count, HcclDataType dt,
+                         HcclReduceOp op, hipStream_t stream)
+{
+    if (count == 0) return HCCL_SUCCESS;
+    if (!ValidOp(op) || n == 0 || n > HCCL_AMD_IR_MAX_SRC) return HCCL_E_PARA;
+    if (n == 1) {
+        if (out == srcs[0]) return HCCL_SUCCESS;
+        uint32_t es = DataTypeSize(dt);
+        if (es == 0) return HCCL_E_NOT_SUPPORT;
+        HIP_CHK(hipMemcpyAsync(out, srcs[0], count * es, hipMemcpyDeviceToDevice, stream));
+        return HCCL_SUCCESS;
+    }
+    if (n == 2) {
+        // acc = srcs[1] (op) srcs[0]
+        return LaunchReduce2(out, srcs[1], srcs[0], count, dt, op, stream);
+    }
+    hipError_t e;
+    switch (dt) {
+        case HCCL_DATA_TYPE_INT8: e = DispatchN<EI8>(op, out, srcs, n, count, stream); break;
+        case HCCL_DATA_TYPE_INT16: e = DispatchN<EI16>(op, out, srcs, n, count, stream); break;
+        case HCCL_DATA_TYPE_INT32: e = DispatchN<EI32>(op, out, srcs, n, count, stream); break;
+        case HCCL_DATA_TYPE_INT64: e = DispatchN<EI64>(op, out, srcs, n, count, stream); break;
+        case HCCL_DATA_TYPE_UINT64: e = DispatchN<EU64>(op, out, srcs, n, count, stream); break;
+        case HCCL_DATA_TYPE_FP16: e = DispatchN<EF16>(op, out, srcs, n, count, stream); break;
+        case HCCL_DATA_TYPE_BFP16: e = DispatchN<EBF16>(op, out, srcs, n, count, stream); break;
+        case HCCL_DATA_TYPE_FP32: e = DispatchN<EF32>(op, out, srcs, n, count, stream); break;
+        case HCCL_DATA_TYPE_FP64: e = DispatchN<EF64>(op, out, srcs, n, count, stream); break;
+        default: return HCCL_E_NOT_SUPPORT;
+    }
+    if (e != hipSuccess) {
+        HCCL_AMD_ERR("reduceN launch failed: %s", hipGetErrorString(e));
+        return HCCL_E_RUNTIME;
+    }
+    return HCCL_SUCCESS;
+}
+
+}  // namespace hccl_amd

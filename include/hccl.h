@@ -1,0 +1,54 @@
+/*
+ * hccl.h — MI355X-native drop-in for the reducing half of HCCL's operator surface.
+ *
+ * Each entry point below keeps the exact name, argument order, argument meaning and
+ * return-code behaviour of the reference's declaration, so a caller linked against
+ * HCCL links against libhccl_amd.so unchanged:
+ *
+ *   HcclAllReduce      replaces /root/reference/include/hccl.h:35-37  (impl all_reduce_op.cc:23-52)
+ *   HcclReduceScatter  replaces /root/reference/include/hccl.h:67-69  (impl reduce_scatter_op.cc:23-72)
+ *   HcclReduce         replaces /root/reference/include/hccl.h:245-247 (impl reduce_op.cc:23-54)
+ *
+ * The communicator calls are the hcomm functions the reference's callers use
+ * (examples/02_collectives/01_allreduce/main.cc:75,100,122; test/st/.../all_reduce_testcase.cc:80);
+ * they are external to the reference repo and are implemented here over RCCL:
+ *
+ *   HcclGetRootInfo, HcclCommInitRootInfo, HcclCommDestroy, HcclGetRankSize, HcclGetRankId
+ *
+ * Semantics: stream-ordered and asynchronous with respect to the host, like the reference
+ * (op_common.cc:962-970): work is enqueued behind everything already on `stream`, internal
+ * streams are joined back into `stream` before return, and the host never blocks.
+ */
+#ifndef HCCL_AMD_HCCL_H_
+#define HCCL_AMD_HCCL_H_
+
+#include "hccl_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* AllReduce: recvBuf[i] = op over ranks of sendBuf[i], count elements. In-place allowed. */
+extern HcclResult HcclAllReduce(void* sendBuf, void* recvBuf, uint64_t count, HcclDataType dataType,
+                                HcclReduceOp op, HcclComm comm, aclrtStream stream);
+
+/* ReduceScatter: sendBuf holds rankSize blocks of recvCount; rank r receives the reduce of block r. */
+extern HcclResult HcclReduceScatter(void* sendBuf, void* recvBuf, uint64_t recvCount, HcclDataType dataType,
+                                    HcclReduceOp op, HcclComm comm, aclrtStream stream);
+
+/* Reduce: recvBuf on `root` receives the reduce of every rank's sendBuf (recvBuf must be non-null everywhere). */
+extern HcclResult HcclReduce(void* sendBuf, void* recvBuf, uint64_t count, HcclDataType dataType, HcclReduceOp op,
+                             uint32_t root, HcclComm comm, aclrtStream stream);
+
+/* Communicator management (hcomm surface used by the reference's callers). */
+extern HcclResult HcclGetRootInfo(HcclRootInfo* rootInfo);
+extern HcclResult HcclCommInitRootInfo(uint32_t nRanks, const HcclRootInfo* rootInfo, uint32_t rank,
+                                       HcclComm* comm);
+extern HcclResult HcclCommDestroy(HcclComm comm);
+extern HcclResult HcclGetRankSize(HcclComm comm, uint32_t* rankSize);
+extern HcclResult HcclGetRankId(HcclComm comm, uint32_t* rank);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HCCL_AMD_HCCL_H_ */

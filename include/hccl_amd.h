@@ -1,0 +1,127 @@
+/*
+ * hccl_amd.h — extension C ABI of libhccl_amd.so (everything that is not in the reference's hccl.h).
+ *
+ * 1. The inner reduce primitive. In the reference every reducing schedule ends in
+ *    LocalReduce (/root/reference/src/ops/op_common/template/wrapper/alg_data_trans_wrapper.cc:901-928),
+ *    which enqueues hcomm's HcommLocalReduceOnThread(thread, dst, src, count, dtype, op) = "dst = src (+) dst"
+ *    (call site :924-926; stub semantics test/st/algorithm/utils/src/hccl_proxy/hccl_stub.cc:648-677), or, for
+ *    64-bit dtypes and PROD, runs AicpuReduce on the AICPU core (:1254-1353). HcclAmdLocalReduce replaces both
+ *    with one HIP kernel family on a HIP stream. Element rule, identical to AicpuReduceTemplate (:1313-1353):
+ *        SUM  dst = src + dst          PROD dst = src * dst   (integers wrap, two's complement)
+ *        MAX  dst = (src < dst) ? dst : src    (std::max(src, dst): ties and NaN give src)
+ *        MIN  dst = (dst < src) ? dst : src    (std::min(src, dst): ties and NaN give src)
+ *    fp16 is computed through fp32 with round-to-nearest-even (AicpuReduceFp16, :1232-1252); bf16 the same way.
+ *
+ * 2. The schedule IR. Every collective is compiled to a per-rank list of HcclAmdIrOp records. The same records
+ *    are executed by the HIP/RCCL executor and replayed by the CPU oracle (oracle/), so the association order of
+ *    every reduced element is fixed by the IR and checked bit-for-bit.
+ *
+ * 3. A loopback world: nRanks communicators inside one process on the current device whose "links" are
+ *    device-to-device copies. It runs the exact executor the RCCL path runs and is how the multi-rank schedules
+ *    are tested on a single MI355X (the reference's analogue is its host simulator, test/st/algorithm).
+ */
+#ifndef HCCL_AMD_EXT_H_
+#define HCCL_AMD_EXT_H_
+
+#include "hccl_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- local reduce primitive */
+
+/* dst[i] = src[i] (op) dst[i], i < count. Mirrors HcommLocalReduceOnThread(thread, dst, src, count, dt, op). */
+extern HcclResult HcclAmdLocalReduce(void* dst, const void* src, uint64_t count, HcclDataType dataType,
+                                     HcclReduceOp op, aclrtStream stream);
+
+/* out[i] = src[i] (op) dst[i]: the out-of-place form (3 streams: 2 reads, 1 write). out may alias dst or src. */
+extern HcclResult HcclAmdLocalReduce2(void* out, const void* src, const void* dst, uint64_t count,
+                                      HcclDataType dataType, HcclReduceOp op, aclrtStream stream);
+
+/* Ordered n-ary fold in one pass: acc = srcs[0]; for j = 1..nsrc-1: acc = srcs[j] (op) acc; out = acc.
+ * 1 <= nsrc <= HCCL_AMD_IR_MAX_SRC. out may alias any srcs[j]. */
+extern HcclResult HcclAmdLocalReduceN(void* out, const void* const* srcs, uint32_t nsrc, uint64_t count,
+                                      HcclDataType dataType, HcclReduceOp op, aclrtStream stream);
+
+/* Tuning knobs for the streaming reduce kernels (process-wide; 0 = default for every field).
+ * blocksPerCu: workgroups of 256 threads per CU in the persistent grid. unroll: 16-B vectors per lane per
+ * iteration (1, 2, 4 or 8). cachePolicy: 1 = plain, 2 = nt loads, 3 = nt stores, 4 = nt loads + stores,
+ * 5 = nt loads + stores with contiguous per-workgroup tile runs. */
+extern HcclResult HcclAmdSetReduceLaunch(uint32_t blocksPerCu, uint32_t unroll, uint32_t cachePolicy);
+
+/* Byte size of one element of dataType, 0 if unknown (DATATYPE_SIZE_TABLE, alg_param.h:43-61). */
+extern uint32_t HcclAmdDataTypeSize(HcclDataType dataType);
+
+extern const char* HcclAmdGetErrorString(HcclResult code);
+
+/* ---------------------------------------------------------------- schedule IR */
+
+#define HCCL_AMD_IR_MAX_SRC 16
+
+typedef enum {
+    HCCL_AMD_IR_COPY = 0,   /* dst <- src[0] */
+    HCCL_AMD_IR_REDUCE = 1, /* dst <- fold(src[0..nsrc)) with the LocalReduceN order */
+    HCCL_AMD_IR_SEND = 2,   /* send src[0] (count elements) to peer */
+    HCCL_AMD_IR_RECV = 3    /* receive count elements from peer into dst */
+} HcclAmdIrKind;
+
+typedef enum {
+    HCCL_AMD_BUF_INPUT = 0,   /* user sendBuf */
+    HCCL_AMD_BUF_OUTPUT = 1,  /* user recvBuf */
+    HCCL_AMD_BUF_SCRATCH = 2  /* per-communicator staging ("CCL buffer") */
+} HcclAmdBuf;
+
+typedef struct {
+    int32_t kind;   /* HcclAmdIrKind */
+    int32_t peer;   /* SEND / RECV peer rank, else -1 */
+    int32_t nsrc;   /* number of valid src entries */
+    int32_t group;  /* SEND/RECV records with equal group are posted together (one RCCL group) */
+    uint64_t count; /* elements */
+    int32_t dstBuf; /* HcclAmdBuf, -1 for SEND */
+    int32_t reserved;
+    uint64_t dstOff; /* element offset */
+    int32_t srcBuf[HCCL_AMD_IR_MAX_SRC];
+    uint64_t srcOff[HCCL_AMD_IR_MAX_SRC];
+} HcclAmdIrOp;
+
+typedef enum {
+    HCCL_AMD_OP_ALLREDUCE = 0,
+    HCCL_AMD_OP_REDUCE_SCATTER = 1,
+    HCCL_AMD_OP_REDUCE = 2
+} HcclAmdOpType;
+
+typedef enum {
+    HCCL_AMD_ALGO_AUTO = 0,         /* reference selector policy (all_reduce_auto_selector.cc:517-550) */
+    HCCL_AMD_ALGO_MESH_ONESHOT = 1, /* order O1: own input first, then ascending ranks */
+    HCCL_AMD_ALGO_MESH_TWOSHOT = 2, /* AllReduce: order O2 (ascending from rank 0); RS/Reduce: O1 */
+    HCCL_AMD_ALGO_RING = 3,         /* ring reduce-scatter (+ ring all-gather) */
+    HCCL_AMD_ALGO_RHD = 4           /* recursive halving / doubling (power-of-two rank counts) */
+} HcclAmdAlgo;
+
+/* Build rank `rank`'s schedule. If ops == NULL only *numOps is written. scratchElems receives the number of
+ * scratch elements the schedule addresses. pieceBytes = 0 picks the default pipelining granule. */
+extern HcclResult HcclAmdBuildSchedule(int32_t opType, int32_t algo, uint32_t nRanks, uint32_t rank, uint64_t count,
+                                       HcclDataType dataType, uint32_t root, uint64_t pieceBytes, HcclAmdIrOp* ops,
+                                       uint64_t capacity, uint64_t* numOps, int32_t* algoUsed,
+                                       uint64_t* scratchElems);
+
+/* ---------------------------------------------------------------- communicator extensions */
+
+/* nRanks communicators on the current HIP device, joined by device-to-device copies. comms[r] is rank r.
+ * Each rank must be driven from its own host thread (collectives rendezvous like real ranks). */
+extern HcclResult HcclAmdCommInitLoopback(uint32_t nRanks, HcclComm* comms);
+
+/* Force the schedule family for subsequent collectives on comm (HCCL_AMD_ALGO_AUTO restores the selector). */
+extern HcclResult HcclAmdCommSetAlgo(HcclComm comm, int32_t algo);
+
+/* Pipelining granule (bytes per piece) for subsequent collectives on comm; 0 restores the default. */
+extern HcclResult HcclAmdCommSetPieceBytes(HcclComm comm, uint64_t pieceBytes);
+
+/* Algorithm the last collective on comm executed (HcclAmdAlgo), or -1. */
+extern int32_t HcclAmdCommLastAlgo(HcclComm comm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HCCL_AMD_EXT_H_ */
