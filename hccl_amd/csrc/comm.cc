@@ -1,0 +1,259 @@
+// comm.cc — communicator lifetime, RCCL transport (xGMI), loopback transport (single-device test world).
+#include "comm.h"
+
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cstring>
+
+namespace hccl_amd {
+
+// ------------------------------------------------------------------------------------------------ Comm
+
+Comm* AsComm(HcclComm c)
+{
+    Comm* p = static_cast<Comm*>(c);
+    if (p == nullptr || p->magic != 0x48434C41) return nullptr;
+    return p;
+}
+
+uint64_t ScratchBytesDefault()
+{
+    // HCCL_BUFFSIZE is in MB, as in HCCL; the default is sized for 288 GB HBM (reference: 200 MB).
+    const char* e = std::getenv("HCCL_BUFFSIZE");
+    uint64_t mb = 256;
+    if (e != nullptr && e[0] != '\0') {
+        char* end = nullptr;
+        unsigned long long v = std::strtoull(e, &end, 10);
+        if (end != e && v > 0) mb = v;
+    }
+    return mb << 20;
+}
+
+HcclResult Comm::Init(int dev)
+{
+    device = dev;
+    HIP_CHK(hipSetDevice(dev));
+    int lo = 0, hi = 0;
+    HIP_CHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    // the link stream gets the higher priority: its kernels are short and gate every peer
+    HIP_CHK(hipStreamCreateWithPriority(&commStream, hipStreamNonBlocking, hi));
+    HIP_CHK(hipStreamCreateWithPriority(&reduceStream, hipStreamNonBlocking, lo));
+    if (nRanks > 1) {
+        scratchBytes = ScratchBytesDefault();
+        HIP_CHK(hipMalloc(&scratch, scratchBytes));
+    }
+    return HCCL_SUCCESS;
+}
+
+HcclResult Comm::NextEvent(hipEvent_t* e)
+{
+    if (nextEvent == events.size()) {
+        hipEvent_t ev;
+        HIP_CHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        events.push_back(ev);
+    }
+    *e = events[nextEvent++];
+    return HCCL_SUCCESS;
+}
+
+Comm::~Comm()
+{
+    magic = 0;
+    if (commStream != nullptr || reduceStream != nullptr) {
+        (void)hipSetDevice(device);
+    }
+    if (commStream != nullptr) (void)hipStreamSynchronize(commStream);
+    if (reduceStream != nullptr) (void)hipStreamSynchronize(reduceStream);
+    transport.reset();
+    for (hipEvent_t e : events) (void)hipEventDestroy(e);
+    if (scratch != nullptr) (void)hipFree(scratch);
+    if (commStream != nullptr) (void)hipStreamDestroy(commStream);
+    if (reduceStream != nullptr) (void)hipStreamDestroy(reduceStream);
+}
+
+// ------------------------------------------------------------------------------------------------ RCCL transport
+
+namespace {
+
+HcclResult FromNccl(ncclResult_t r, const char* what)
+{
+    if (r == ncclSuccess) return HCCL_SUCCESS;
+    HCCL_AMD_ERR("%s: %s", what, ncclGetErrorString(r));
+    switch (r) {
+        case ncclInvalidArgument:
+        case ncclInvalidUsage: return HCCL_E_PARA;
+        case ncclSystemError: return HCCL_E_SYSCALL;
+        case ncclRemoteError: return HCCL_E_REMOTE;
+        default: return HCCL_E_INTERNAL;
+    }
+}
+
+class RcclTransport : public Transport {
+public:
+    ncclComm_t comm = nullptr;
+    ~RcclTransport() override
+    {
+        if (comm != nullptr) (void)ncclCommDestroy(comm);
+    }
+    HcclResult Group(const std::vector<P2pOp>& ops, hipStream_t stream) override
+    {
+        ncclResult_t r = ncclGroupStart();
+        if (r != ncclSuccess) return FromNccl(r, "ncclGroupStart");
+        for (const P2pOp& o : ops) {
+            r = o.isSend ? ncclSend(o.ptr, o.bytes, ncclUint8, static_cast<int>(o.peer), comm, stream)
+                         : ncclRecv(o.ptr, o.bytes, ncclUint8, static_cast<int>(o.peer), comm, stream);
+            if (r != ncclSuccess) {
+                (void)ncclGroupEnd();
+                return FromNccl(r, o.isSend ? "ncclSend" : "ncclRecv");
+            }
+        }
+        return FromNccl(ncclGroupEnd(), "ncclGroupEnd");
+    }
+    const char* Name() const override { return "rccl"; }
+};
+
+}  // namespace
+
+HcclResult RcclGetUniqueId(void* id128)
+{
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId id;
+    HcclResult r = FromNccl(ncclGetUniqueId(&id), "ncclGetUniqueId");
+    if (r != HCCL_SUCCESS) return r;
+    std::memcpy(id128, &id, sizeof id);
+    return HCCL_SUCCESS;
+}
+
+std::unique_ptr<Transport> MakeRcclTransport(void* uniqueId, uint32_t nRanks, uint32_t rank, HcclResult* err)
+{
+    auto t = std::make_unique<RcclTransport>();
+    ncclUniqueId id;
+    std::memcpy(&id, uniqueId, sizeof id);
+    *err = FromNccl(ncclCommInitRank(&t->comm, static_cast<int>(nRanks), id, static_cast<int>(rank)),
+                    "ncclCommInitRank");
+    if (*err != HCCL_SUCCESS) {
+        t->comm = nullptr;
+        return nullptr;
+    }
+    return t;
+}
+
+// ------------------------------------------------------------------------------------------------ loopback
+
+// nRanks ranks in one process on one device. A send posts {source, bytes, ready event} into the (from, to) FIFO;
+// the receiver's stream waits for `ready`, copies device-to-device and records `done`; the sender's stream then
+// waits for `done`, so a group completes exactly when an RCCL group would. Ranks rendezvous on the host like real
+// ranks, so each must be driven from its own thread.
+class LoopbackWorld {
+public:
+    struct Entry {
+        const void* src = nullptr;
+        uint64_t bytes = 0;
+        hipEvent_t ready = nullptr;
+        hipEvent_t done = nullptr;
+        bool consumed = false;
+        bool failed = false;
+    };
+    explicit LoopbackWorld(uint32_t n) : n_(n), boxes_(size_t(n) * n) {}
+    uint32_t n_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::vector<std::deque<std::shared_ptr<Entry>>> boxes_;
+};
+
+namespace {
+
+constexpr auto kRendezvousTimeout = std::chrono::seconds(600);
+
+class LoopbackTransport : public Transport {
+public:
+    LoopbackTransport(std::shared_ptr<LoopbackWorld> w, uint32_t rank) : w_(std::move(w)), me_(rank) {}
+    const char* Name() const override { return "loopback"; }
+
+    HcclResult Group(const std::vector<P2pOp>& ops, hipStream_t stream) override
+    {
+        LoopbackWorld& w = *w_;
+        std::vector<std::shared_ptr<LoopbackWorld::Entry>> posted;
+        for (const P2pOp& o : ops) {
+            if (!o.isSend) continue;
+            auto e = std::make_shared<LoopbackWorld::Entry>();
+            e->src = o.ptr;
+            e->bytes = o.bytes;
+            HIP_CHK(hipEventCreateWithFlags(&e->ready, hipEventDisableTiming));
+            HIP_CHK(hipEventRecord(e->ready, stream));
+            {
+                std::lock_guard<std::mutex> lk(w.mu_);
+                w.boxes_[size_t(me_) * w.n_ + o.peer].push_back(e);
+            }
+            w.cv_.notify_all();
+            posted.push_back(std::move(e));
+        }
+        HcclResult result = HCCL_SUCCESS;
+        for (const P2pOp& o : ops) {
+            if (o.isSend) continue;
+            std::shared_ptr<LoopbackWorld::Entry> e;
+            {
+                std::unique_lock<std::mutex> lk(w.mu_);
+                auto& box = w.boxes_[size_t(o.peer) * w.n_ + me_];
+                if (!w.cv_.wait_for(lk, kRendezvousTimeout, [&] { return !box.empty(); })) {
+                    HCCL_AMD_ERR("loopback rank %u: no send from rank %u", me_, o.peer);
+                    return HCCL_E_TIMEOUT;
+                }
+                e = box.front();
+                box.pop_front();
+            }
+            hipEvent_t done = nullptr;
+            bool ok = e->bytes == o.bytes;
+            if (!ok) {
+                HCCL_AMD_ERR("loopback rank %u: recv of %llu B matched a send of %llu B from rank %u", me_,
+                             (unsigned long long)o.bytes, (unsigned long long)e->bytes, o.peer);
+                result = HCCL_E_INTERNAL;
+            } else {
+                ok = hipStreamWaitEvent(stream, e->ready, 0) == hipSuccess &&
+                     hipMemcpyAsync(o.ptr, e->src, o.bytes, hipMemcpyDeviceToDevice, stream) == hipSuccess &&
+                     hipEventCreateWithFlags(&done, hipEventDisableTiming) == hipSuccess &&
+                     hipEventRecord(done, stream) == hipSuccess;
+                if (!ok) result = HCCL_E_RUNTIME;
+            }
+            {
+                std::lock_guard<std::mutex> lk(w.mu_);
+                e->done = done;
+                e->failed = !ok;
+                e->consumed = true;
+            }
+            w.cv_.notify_all();
+        }
+        for (auto& e : posted) {
+            {
+                std::unique_lock<std::mutex> lk(w.mu_);
+                if (!w.cv_.wait_for(lk, kRendezvousTimeout, [&] { return e->consumed; })) {
+                    HCCL_AMD_ERR("loopback rank %u: send never received", me_);
+                    return HCCL_E_TIMEOUT;
+                }
+            }
+            if (e->failed) result = HCCL_E_INTERNAL;
+            if (e->done != nullptr) {
+                if (hipStreamWaitEvent(stream, e->done, 0) != hipSuccess) result = HCCL_E_RUNTIME;
+                (void)hipEventDestroy(e->done);
+            }
+            (void)hipEventDestroy(e->ready);
+        }
+        return result;
+    }
+
+private:
+    std::shared_ptr<LoopbackWorld> w_;
+    uint32_t me_;
+};
+
+}  // namespace
+
+std::shared_ptr<LoopbackWorld> MakeLoopbackWorld(uint32_t nRanks) { return std::make_shared<LoopbackWorld>(nRanks); }
+
+std::unique_ptr<Transport> MakeLoopbackTransport(std::shared_ptr<LoopbackWorld> world, uint32_t rank)
+{
+    return std::make_unique<LoopbackTransport>(std::move(world), rank);
+}
+
+}  // namespace hccl_amd

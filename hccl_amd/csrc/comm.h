@@ -1,0 +1,78 @@
+// comm.h — communicator, transports and executor of libhccl_amd.so.
+//
+// HcclComm (opaque in include/hccl_types.h) is a Comm*. One Comm per rank and device, like the reference's
+// communicator (SURVEY.md §8b "Threading"). Its resources mirror what the reference's op layer allocates per
+// communicator (op_common.cc:1203 HcclGetAlgRes): a staging "CCL buffer" (aiv_defines.h:44, 200 MiB there),
+// helper streams (the reference's slave "threads") and events (its notifies).
+#pragma once
+
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "internal.h"
+#include "schedule.h"
+
+namespace hccl_amd {
+
+struct P2pOp {
+    bool isSend;
+    uint32_t peer;
+    void* ptr;
+    uint64_t bytes;
+};
+
+// Posts one group of sends and receives on `stream`. The group is complete (in stream order) when every send's
+// source may be overwritten and every receive's destination holds the data.
+class Transport {
+public:
+    virtual ~Transport() = default;
+    virtual HcclResult Group(const std::vector<P2pOp>& ops, hipStream_t stream) = 0;
+    virtual const char* Name() const = 0;
+};
+
+std::unique_ptr<Transport> MakeRcclTransport(void* uniqueId, uint32_t nRanks, uint32_t rank, HcclResult* err);
+HcclResult RcclGetUniqueId(void* id128);
+
+class LoopbackWorld;
+std::unique_ptr<Transport> MakeLoopbackTransport(std::shared_ptr<LoopbackWorld> world, uint32_t rank);
+std::shared_ptr<LoopbackWorld> MakeLoopbackWorld(uint32_t nRanks);
+
+struct Comm {
+    uint32_t magic = 0x48434C41;  // "HCLA"
+    uint32_t rank = 0;
+    uint32_t nRanks = 1;
+    int device = 0;
+    std::unique_ptr<Transport> transport;
+    hipStream_t commStream = nullptr;
+    hipStream_t reduceStream = nullptr;
+    void* scratch = nullptr;
+    uint64_t scratchBytes = 0;
+    int32_t algoOverride = HCCL_AMD_ALGO_AUTO;
+    uint64_t pieceBytes = 0;
+    int32_t lastAlgo = -1;
+    std::mutex mu;  // one collective at a time per communicator
+
+    // event pool, recycled per collective
+    std::vector<hipEvent_t> events;
+    size_t nextEvent = 0;
+
+    HcclResult Init(int dev);
+    HcclResult NextEvent(hipEvent_t* e);
+    ~Comm();
+};
+
+Comm* AsComm(HcclComm c);
+
+// Staging bytes per communicator: HCCL_BUFFSIZE (MB) if set, else 256 MB. Must be equal on every rank: the
+// pipelining granule is derived from it.
+uint64_t ScratchBytesDefault();
+
+// Runs one rank's schedule. bufs = {sendBuf, recvBuf, scratch}. Stream-ordered after `user`; `user` waits for the
+// whole schedule before anything enqueued later on it runs.
+HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const bufs[3], HcclDataType dt,
+                   HcclReduceOp op, hipStream_t user);
+
+}  // namespace hccl_amd

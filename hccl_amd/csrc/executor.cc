@@ -1,0 +1,154 @@
+// executor.cc — runs one rank's schedule IR on two HIP streams.
+//
+// Replaces the reference's per-step orchestration (executors' OrchestrateLoop + templates' KernelRun, which post
+// hcomm tasks on a main "thread" and slave threads joined by notifies: alg_data_trans_wrapper.cc:1005-1073,
+// SURVEY.md §8a rows R5, R8). Here:
+//   * SEND/RECV records with one group id become one transport group on the link stream (RCCL over xGMI);
+//   * REDUCE and COPY records go to the reduce stream (HIP kernels of reduce_kernels.hip / a DMA copy);
+//   * dependencies are not written by hand: every record's byte ranges (absolute device addresses, so in-place
+//     buffers alias correctly) are checked against the earlier units of the OTHER stream, and the latest
+//     conflicting unit (RAW, WAR or WAW) becomes a hipStreamWaitEvent. Same-stream order is program order.
+// This is the reference ST's memory-conflict rule (test/st/algorithm/.../mem_conflict_check) turned into the
+// synchronisation itself. The host never blocks (except loopback rendezvous); the user stream is joined at the end.
+#include <algorithm>
+
+#include "comm.h"
+
+namespace hccl_amd {
+
+namespace {
+
+struct Range {
+    uintptr_t lo;
+    uintptr_t hi;
+    bool write;
+};
+
+struct Unit {
+    int stream;  // 0 = link, 1 = reduce
+    hipEvent_t ev;
+    std::vector<Range> ranges;
+};
+
+bool Conflicts(const std::vector<Range>& a, const std::vector<Range>& b)
+{
+    for (const Range& x : a) {
+        for (const Range& y : b) {
+            if ((x.write || y.write) && x.lo < y.hi && y.lo < x.hi) return true;
+        }
+    }
+    return false;
+}
+
+}  // namespace
+
+HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const bufs[3], HcclDataType dt,
+                   HcclReduceOp op, hipStream_t user)
+{
+    const uint64_t es = DataTypeSize(dt);
+    hipStream_t streams[2] = {c.commStream, c.reduceStream};
+    c.nextEvent = 0;
+    hipEvent_t start;
+    HCCL_CHK(c.NextEvent(&start));
+    HIP_CHK(hipEventRecord(start, user));
+    HIP_CHK(hipStreamWaitEvent(c.commStream, start, 0));
+    HIP_CHK(hipStreamWaitEvent(c.reduceStream, start, 0));
+
+    auto addr = [&](int32_t buf, uint64_t off) -> uintptr_t {
+        return reinterpret_cast<uintptr_t>(bufs[buf]) + off * es;
+    };
+
+    std::vector<Unit> units;
+    units.reserve(ops.size());
+    std::vector<size_t> onStream[2];
+    // synced[x][y]: index into onStream[y] of the last unit stream x has already waited for (+1)
+    size_t synced[2][2] = {{0, 0}, {0, 0}};
+    bool used[2] = {false, false};
+
+    size_t i = 0;
+    std::vector<P2pOp> p2p;
+    while (i < ops.size()) {
+        Unit u;
+        p2p.clear();
+        const HcclAmdIrOp& first = ops[i];
+        const bool isComm = first.kind == HCCL_AMD_IR_SEND || first.kind == HCCL_AMD_IR_RECV;
+        u.stream = isComm ? 0 : 1;
+        if (isComm) {
+            const int32_t g = first.group;
+            while (i < ops.size() && (ops[i].kind == HCCL_AMD_IR_SEND || ops[i].kind == HCCL_AMD_IR_RECV) &&
+                   ops[i].group == g) {
+                const HcclAmdIrOp& o = ops[i];
+                const uint64_t bytes = o.count * es;
+                if (o.kind == HCCL_AMD_IR_SEND) {
+                    uintptr_t a = addr(o.srcBuf[0], o.srcOff[0]);
+                    u.ranges.push_back({a, a + bytes, false});
+                    p2p.push_back({true, static_cast<uint32_t>(o.peer), reinterpret_cast<void*>(a), bytes});
+                } else {
+                    uintptr_t a = addr(o.dstBuf, o.dstOff);
+                    u.ranges.push_back({a, a + bytes, true});
+                    p2p.push_back({false, static_cast<uint32_t>(o.peer), reinterpret_cast<void*>(a), bytes});
+                }
+                ++i;
+            }
+        } else {
+            const HcclAmdIrOp& o = first;
+            const uint64_t bytes = o.count * es;
+            uintptr_t d = addr(o.dstBuf, o.dstOff);
+            u.ranges.push_back({d, d + bytes, true});
+            for (int j = 0; j < o.nsrc; ++j) {
+                uintptr_t s = addr(o.srcBuf[j], o.srcOff[j]);
+                u.ranges.push_back({s, s + bytes, false});
+            }
+            ++i;
+        }
+
+        // cross-stream hazards: wait for the latest conflicting unit on the other stream
+        const int x = u.stream;
+        const int y = 1 - x;
+        for (size_t k = onStream[y].size(); k > synced[x][y]; --k) {
+            const Unit& prior = units[onStream[y][k - 1]];
+            if (Conflicts(prior.ranges, u.ranges)) {
+                HIP_CHK(hipStreamWaitEvent(streams[x], prior.ev, 0));
+                synced[x][y] = k;
+                break;
+            }
+        }
+
+        if (isComm) {
+            HCCL_CHK(c.transport->Group(p2p, streams[x]));
+        } else {
+            const HcclAmdIrOp& o = first;
+            void* dst = reinterpret_cast<void*>(addr(o.dstBuf, o.dstOff));
+            if (o.kind == HCCL_AMD_IR_COPY) {
+                const void* src = reinterpret_cast<const void*>(addr(o.srcBuf[0], o.srcOff[0]));
+                if (src != dst) {
+                    HIP_CHK(hipMemcpyAsync(dst, src, o.count * es, hipMemcpyDeviceToDevice, streams[x]));
+                }
+            } else if (o.kind == HCCL_AMD_IR_REDUCE) {
+                const void* srcs[HCCL_AMD_IR_MAX_SRC];
+                for (int j = 0; j < o.nsrc; ++j) {
+                    srcs[j] = reinterpret_cast<const void*>(addr(o.srcBuf[j], o.srcOff[j]));
+                }
+                HCCL_CHK(LaunchReduceN(dst, srcs, static_cast<uint32_t>(o.nsrc), o.count, dt, op, streams[x]));
+            } else {
+                return HCCL_E_INTERNAL;
+            }
+        }
+        HCCL_CHK(c.NextEvent(&u.ev));
+        HIP_CHK(hipEventRecord(u.ev, streams[x]));
+        used[x] = true;
+        onStream[x].push_back(units.size());
+        units.push_back(std::move(u));
+    }
+
+    for (int s = 0; s < 2; ++s) {
+        if (!used[s]) continue;
+        hipEvent_t end;
+        HCCL_CHK(c.NextEvent(&end));
+        HIP_CHK(hipEventRecord(end, streams[s]));
+        HIP_CHK(hipStreamWaitEvent(user, end, 0));
+    }
+    return HCCL_SUCCESS;
+}
+
+}  // namespace hccl_amd

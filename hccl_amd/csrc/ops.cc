@@ -1,0 +1,267 @@
+// ops.cc — the operator surface of include/hccl.h plus the communicator extensions of include/hccl_amd.h.
+//
+// Each entry point keeps the reference's validation order and return codes:
+//   HcclAllReduce      all_reduce_op.cc:23-52, AllReduceInitAndCheck :107-133, CheckAllReduceInputPara :135-157
+//   HcclReduceScatter  reduce_scatter_op.cc:23-72, CheckReduceScatterInputPara
+//   HcclReduce         reduce_op.cc:23-54, ReduceInitAndCheck, CheckReduceInputPara :106-127
+//   CheckCount / CheckDataType / CheckReduceOp / SingleRankProc   op_common.cc:2902-3098
+// then build this rank's schedule (schedule.cc) and run it (executor.cc).
+#include <cstring>
+
+#include "comm.h"
+
+namespace hccl_amd {
+
+namespace {
+
+constexpr uint64_t kSysMaxCount = 0x7FFFFFFFFull;  // SYS_MAX_COUNT, hccl_common.h:42
+
+HcclResult CheckCount(uint64_t count) { return count > kSysMaxCount ? HCCL_E_PARA : HCCL_SUCCESS; }
+
+// CheckDataType(dataType, needReduce = true), op_common.cc:2913-2950
+HcclResult CheckReduceDataType(HcclDataType dt) { return IsReduceDataType(dt) ? HCCL_SUCCESS : HCCL_E_NOT_SUPPORT; }
+
+// CheckReduceOp, op_common.cc:2977-2998: PROD only on INT8/INT32/INT64/UINT64/FP16/FP32/FP64. An op outside
+// {SUM, PROD, MAX, MIN} has no reference check at the entry (it fails deep in the template); it is HCCL_E_PARA here.
+HcclResult CheckReduceOp(HcclDataType dt, HcclReduceOp op)
+{
+    if (op == HCCL_REDUCE_PROD) {
+        switch (dt) {
+            case HCCL_DATA_TYPE_INT8:
+            case HCCL_DATA_TYPE_INT32:
+            case HCCL_DATA_TYPE_INT64:
+            case HCCL_DATA_TYPE_UINT64:
+            case HCCL_DATA_TYPE_FP16:
+            case HCCL_DATA_TYPE_FP32:
+            case HCCL_DATA_TYPE_FP64: return HCCL_SUCCESS;
+            default: return HCCL_E_NOT_SUPPORT;
+        }
+    }
+    if (op != HCCL_REDUCE_SUM && op != HCCL_REDUCE_MAX && op != HCCL_REDUCE_MIN) return HCCL_E_PARA;
+    return HCCL_SUCCESS;
+}
+
+HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, uint64_t count, HcclDataType dt,
+                         HcclReduceOp op, uint32_t root, hipStream_t stream)
+{
+    std::lock_guard<std::mutex> lk(c.mu);
+    HIP_CHK(hipSetDevice(c.device));
+    const uint32_t es = DataTypeSize(dt);
+    if (c.nRanks == 1) {
+        // SingleRankProc (op_common.cc:3042-3098): copy in -> out unless they are the same buffer.
+        c.lastAlgo = HCCL_AMD_ALGO_AUTO;
+        if (sendBuf != recvBuf) {
+            HIP_CHK(hipMemcpyAsync(recvBuf, sendBuf, count * es, hipMemcpyDeviceToDevice, stream));
+        }
+        return HCCL_SUCCESS;
+    }
+    ScheduleParams p;
+    p.opType = opType;
+    p.algo = c.algoOverride;
+    p.nRanks = c.nRanks;
+    p.rank = c.rank;
+    p.count = count;
+    p.elemSize = es;
+    p.root = root;
+    p.pieceBytes = c.pieceBytes;
+    p.scratchCapBytes = c.scratchBytes;
+    Schedule s;
+    HcclResult r = static_cast<HcclResult>(BuildSchedule(p, &s));
+    if (r != HCCL_SUCCESS) return r;
+    if (s.scratchElems * es > c.scratchBytes) {
+        HCCL_AMD_ERR("schedule needs %llu B of staging, communicator has %llu B",
+                     (unsigned long long)(s.scratchElems * es), (unsigned long long)c.scratchBytes);
+        return HCCL_E_INTERNAL;
+    }
+    c.lastAlgo = s.algo;
+    HCCL_AMD_LOG("rank %u op %d algo %d count %llu ops %zu", c.rank, opType, s.algo, (unsigned long long)count,
+                 s.ops.size());
+    void* bufs[3] = {sendBuf, recvBuf, c.scratch};
+    return Execute(c, s.ops, bufs, dt, op, stream);
+}
+
+}  // namespace
+
+}  // namespace hccl_amd
+
+using namespace hccl_amd;
+
+extern "C" {
+
+// ------------------------------------------------------------------------------------------------ operators
+
+HcclResult HcclAllReduce(void* sendBuf, void* recvBuf, uint64_t count, HcclDataType dataType, HcclReduceOp op,
+                         HcclComm comm, aclrtStream stream)
+{
+    if (count == 0) return HCCL_SUCCESS;  // all_reduce_op.cc:37
+    if (stream == nullptr || comm == nullptr || sendBuf == nullptr || recvBuf == nullptr) return HCCL_E_PTR;
+    Comm* c = AsComm(comm);
+    if (c == nullptr) return HCCL_E_PARA;
+    if (c->rank >= c->nRanks) return HCCL_E_PARA;  // HcomCheckUserRank
+    HCCL_CHK(CheckCount(count));
+    HCCL_CHK(CheckReduceDataType(dataType));
+    HCCL_CHK(CheckReduceOp(dataType, op));
+    return RunCollective(*c, HCCL_AMD_OP_ALLREDUCE, sendBuf, recvBuf, count, dataType, op, 0,
+                         static_cast<hipStream_t>(stream));
+}
+
+HcclResult HcclReduceScatter(void* sendBuf, void* recvBuf, uint64_t recvCount, HcclDataType dataType,
+                             HcclReduceOp op, HcclComm comm, aclrtStream stream)
+{
+    if (recvCount == 0) return HCCL_SUCCESS;  // reduce_scatter_op.cc:47
+    if (stream == nullptr || comm == nullptr || sendBuf == nullptr || recvBuf == nullptr) return HCCL_E_PTR;
+    Comm* c = AsComm(comm);
+    if (c == nullptr) return HCCL_E_PARA;
+    if (c->rank >= c->nRanks) return HCCL_E_PARA;
+    HCCL_CHK(CheckCount(recvCount));
+    HCCL_CHK(CheckReduceDataType(dataType));
+    HCCL_CHK(CheckReduceOp(dataType, op));
+    return RunCollective(*c, HCCL_AMD_OP_REDUCE_SCATTER, sendBuf, recvBuf, recvCount, dataType, op, 0,
+                         static_cast<hipStream_t>(stream));
+}
+
+HcclResult HcclReduce(void* sendBuf, void* recvBuf, uint64_t count, HcclDataType dataType, HcclReduceOp op,
+                      uint32_t root, HcclComm comm, aclrtStream stream)
+{
+    if (count == 0) return HCCL_SUCCESS;  // reduce_op.cc:42
+    // CheckReduceInputPara order: comm, sendBuf, recvBuf, stream (reduce_op.cc:106-127)
+    if (comm == nullptr || sendBuf == nullptr || recvBuf == nullptr || stream == nullptr) return HCCL_E_PTR;
+    Comm* c = AsComm(comm);
+    if (c == nullptr) return HCCL_E_PARA;
+    HCCL_CHK(CheckCount(count));
+    HCCL_CHK(CheckReduceDataType(dataType));
+    HCCL_CHK(CheckReduceOp(dataType, op));
+    if (root >= c->nRanks) return HCCL_E_PARA;     // HcomCheckUserRank(rankSize, root)
+    if (c->rank >= c->nRanks) return HCCL_E_PARA;  // HcomCheckUserRank(rankSize, userRank)
+    return RunCollective(*c, HCCL_AMD_OP_REDUCE, sendBuf, recvBuf, count, dataType, op, root,
+                         static_cast<hipStream_t>(stream));
+}
+
+// ------------------------------------------------------------------------------------------------ communicators
+
+static const char kRootMagic[8] = {'H', 'C', 'C', 'L', 'A', 'M', 'D', '1'};
+
+HcclResult HcclGetRootInfo(HcclRootInfo* rootInfo)
+{
+    if (rootInfo == nullptr) return HCCL_E_PTR;
+    std::memset(rootInfo->internal, 0, sizeof rootInfo->internal);
+    std::memcpy(rootInfo->internal, kRootMagic, sizeof kRootMagic);
+    return RcclGetUniqueId(rootInfo->internal + 8);
+}
+
+HcclResult HcclCommInitRootInfo(uint32_t nRanks, const HcclRootInfo* rootInfo, uint32_t rank, HcclComm* comm)
+{
+    if (rootInfo == nullptr || comm == nullptr) return HCCL_E_PTR;
+    if (nRanks == 0 || rank >= nRanks || nRanks > HCCL_AMD_IR_MAX_SRC) return HCCL_E_PARA;
+    if (std::memcmp(rootInfo->internal, kRootMagic, sizeof kRootMagic) != 0) return HCCL_E_PARA;
+    int dev = 0;
+    HIP_CHK(hipGetDevice(&dev));
+    auto c = std::make_unique<Comm>();
+    c->rank = rank;
+    c->nRanks = nRanks;
+    HCCL_CHK(c->Init(dev));
+    HcclResult err = HCCL_SUCCESS;
+    c->transport = MakeRcclTransport(const_cast<char*>(rootInfo->internal + 8), nRanks, rank, &err);
+    if (c->transport == nullptr) return err == HCCL_SUCCESS ? HCCL_E_INTERNAL : err;
+    *comm = c.release();
+    return HCCL_SUCCESS;
+}
+
+HcclResult HcclCommDestroy(HcclComm comm)
+{
+    Comm* c = AsComm(comm);
+    if (c == nullptr) return HCCL_E_PTR;
+    delete c;
+    return HCCL_SUCCESS;
+}
+
+HcclResult HcclGetRankSize(HcclComm comm, uint32_t* rankSize)
+{
+    Comm* c = AsComm(comm);
+    if (c == nullptr || rankSize == nullptr) return HCCL_E_PTR;
+    *rankSize = c->nRanks;
+    return HCCL_SUCCESS;
+}
+
+HcclResult HcclGetRankId(HcclComm comm, uint32_t* rank)
+{
+    Comm* c = AsComm(comm);
+    if (c == nullptr || rank == nullptr) return HCCL_E_PTR;
+    *rank = c->rank;
+    return HCCL_SUCCESS;
+}
+
+HcclResult HcclAmdCommInitLoopback(uint32_t nRanks, HcclComm* comms)
+{
+    if (comms == nullptr) return HCCL_E_PTR;
+    if (nRanks == 0 || nRanks > HCCL_AMD_IR_MAX_SRC) return HCCL_E_PARA;
+    int dev = 0;
+    HIP_CHK(hipGetDevice(&dev));
+    auto world = MakeLoopbackWorld(nRanks);
+    std::vector<std::unique_ptr<Comm>> made;
+    for (uint32_t r = 0; r < nRanks; ++r) {
+        auto c = std::make_unique<Comm>();
+        c->rank = r;
+        c->nRanks = nRanks;
+        HCCL_CHK(c->Init(dev));
+        c->transport = MakeLoopbackTransport(world, r);
+        made.push_back(std::move(c));
+    }
+    for (uint32_t r = 0; r < nRanks; ++r) comms[r] = made[r].release();
+    return HCCL_SUCCESS;
+}
+
+HcclResult HcclAmdCommSetAlgo(HcclComm comm, int32_t algo)
+{
+    Comm* c = AsComm(comm);
+    if (c == nullptr) return HCCL_E_PTR;
+    if (algo < HCCL_AMD_ALGO_AUTO || algo > HCCL_AMD_ALGO_RHD) return HCCL_E_PARA;
+    c->algoOverride = algo;
+    return HCCL_SUCCESS;
+}
+
+HcclResult HcclAmdCommSetPieceBytes(HcclComm comm, uint64_t pieceBytes)
+{
+    Comm* c = AsComm(comm);
+    if (c == nullptr) return HCCL_E_PTR;
+    c->pieceBytes = pieceBytes;
+    return HCCL_SUCCESS;
+}
+
+int32_t HcclAmdCommLastAlgo(HcclComm comm)
+{
+    Comm* c = AsComm(comm);
+    return c == nullptr ? -1 : c->lastAlgo;
+}
+
+HcclResult HcclAmdBuildSchedule(int32_t opType, int32_t algo, uint32_t nRanks, uint32_t rank, uint64_t count,
+                                HcclDataType dataType, uint32_t root, uint64_t pieceBytes, HcclAmdIrOp* ops,
+                                uint64_t capacity, uint64_t* numOps, int32_t* algoUsed, uint64_t* scratchElems)
+{
+    if (numOps == nullptr) return HCCL_E_PTR;
+    uint32_t es = DataTypeSize(dataType);
+    if (es == 0) return HCCL_E_NOT_SUPPORT;
+    ScheduleParams p;
+    p.opType = opType;
+    p.algo = algo;
+    p.nRanks = nRanks;
+    p.rank = rank;
+    p.count = count;
+    p.elemSize = es;
+    p.root = root;
+    p.pieceBytes = pieceBytes;
+    p.scratchCapBytes = ScratchBytesDefault();
+    Schedule s;
+    HcclResult r = static_cast<HcclResult>(BuildSchedule(p, &s));
+    if (r != HCCL_SUCCESS) return r;
+    *numOps = s.ops.size();
+    if (algoUsed != nullptr) *algoUsed = s.algo;
+    if (scratchElems != nullptr) *scratchElems = s.scratchElems;
+    if (ops != nullptr) {
+        if (capacity < s.ops.size()) return HCCL_E_PARA;
+        std::memcpy(ops, s.ops.data(), s.ops.size() * sizeof(HcclAmdIrOp));
+    }
+    return HCCL_SUCCESS;
+}
+
+}  // extern "C"

@@ -1,0 +1,533 @@
+// schedule.cc — schedule IR generators (see schedule.h).
+//
+// Association orders, per element, with "acc = src (op) acc" as in LocalReduce:
+//   one-shot AllReduce, mesh ReduceScatter, Reduce   O1: acc = x_me, then x_r for r ascending, r != me
+//       ins_temp_all_reduce_mesh_1D_one_shot.cc:211-226, ins_temp_reduce_scatter_mesh_1D.cc:165-203,
+//       reduce_mesh_1D.cc:232-246, reduce_mesh_1D_two_shot.cc:226-247
+//   two-shot AllReduce                               O2: acc = x_0, then x_1 .. x_{n-1}
+//       ins_temp_all_reduce_mesh_1D_two_shot.cc:312-338
+//   ring (build-side; the reference has no ring AllReduce template)   chunk c: acc = x_{c+1}, then x_{c+2} .. x_c
+//   RHD (docs/zh/user_guide/coll_algo_intro/RHD.md)  pairwise tree, partner = rank ^ d, d = n/2, n/4, .., 1
+//
+// Data movement: a rank's data leaves it through SEND/RECV records grouped into one RCCL group per pipeline step;
+// every schedule is cut into pieces ("pipelining granule") so that the transfer of piece t+1 overlaps the reduce
+// of piece t, and the staging ("CCL buffer", SCRATCH) holds only a bounded number of pieces. The executor derives
+// every cross-stream dependency from the byte ranges the records touch, so the generators only have to emit a
+// correct program order.
+#include "schedule.h"
+
+#include <algorithm>
+
+namespace hccl_amd {
+
+namespace {
+
+constexpr uint64_t kAlignBytes = 128;  // HCCL_MIN_SLICE_ALIGN, alg_template_base.h:34
+constexpr uint64_t kOneShotMaxBytes = 8ull << 20;
+
+struct Ref {
+    int32_t buf;
+    uint64_t off;
+};
+
+class Builder {
+public:
+    std::vector<HcclAmdIrOp> ops;
+    uint64_t scratchHigh = 0;
+    int32_t group = 0;
+
+    void Copy(Ref dst, Ref src, uint64_t count)
+    {
+        if (count == 0) return;
+        HcclAmdIrOp o = Blank(HCCL_AMD_IR_COPY, count);
+        SetDst(o, dst, count);
+        AddSrc(o, src, count);
+        ops.push_back(o);
+    }
+    void Reduce(Ref dst, const std::vector<Ref>& srcs, uint64_t count)
+    {
+        if (count == 0) return;
+        HcclAmdIrOp o = Blank(HCCL_AMD_IR_REDUCE, count);
+        SetDst(o, dst, count);
+        for (const Ref& s : srcs) AddSrc(o, s, count);
+        ops.push_back(o);
+    }
+    void Send(uint32_t peer, Ref src, uint64_t count)
+    {
+        if (count == 0) return;
+        HcclAmdIrOp o = Blank(HCCL_AMD_IR_SEND, count);
+        o.peer = static_cast<int32_t>(peer);
+        o.group = group;
+        AddSrc(o, src, count);
+        ops.push_back(o);
+    }
+    void Recv(uint32_t peer, Ref dst, uint64_t count)
+    {
+        if (count == 0) return;
+        HcclAmdIrOp o = Blank(HCCL_AMD_IR_RECV, count);
+        o.peer = static_cast<int32_t>(peer);
+        o.group = group;
+        SetDst(o, dst, count);
+        ops.push_back(o);
+    }
+    void EndGroup() { group++; }
+
+private:
+    static HcclAmdIrOp Blank(int32_t kind, uint64_t count)
+    {
+        HcclAmdIrOp o{};
+        o.kind = kind;
+        o.peer = -1;
+        o.nsrc = 0;
+        o.group = -1;
+        o.count = count;
+        o.dstBuf = -1;
+        for (int i = 0; i < HCCL_AMD_IR_MAX_SRC; ++i) o.srcBuf[i] = -1;
+        return o;
+    }
+    void Track(Ref r, uint64_t count)
+    {
+        if (r.buf == HCCL_AMD_BUF_SCRATCH) scratchHigh = std::max(scratchHigh, r.off + count);
+    }
+    void SetDst(HcclAmdIrOp& o, Ref r, uint64_t count)
+    {
+        o.dstBuf = r.buf;
+        o.dstOff = r.off;
+        Track(r, count);
+    }
+    void AddSrc(HcclAmdIrOp& o, Ref r, uint64_t count)
+    {
+        o.srcBuf[o.nsrc] = r.buf;
+        o.srcOff[o.nsrc] = r.off;
+        o.nsrc++;
+        Track(r, count);
+    }
+};
+
+uint64_t AlignUp(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+uint64_t CeilDiv(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+// A contiguous element range [begin, begin + len).
+struct Span {
+    uint64_t begin;
+    uint64_t len;
+};
+
+// Chunk c of n for a buffer of `count` elements: ceil(count / n) rounded up to the 128-B slice alignment
+// (two-shot slicing, ins_temp_all_reduce_mesh_1D_two_shot.cc:170-202, with HCCL_MIN_SLICE_ALIGN); trailing chunks
+// may be short or empty.
+Span Chunk(uint64_t count, uint32_t n, uint32_t c, uint64_t alignElems)
+{
+    uint64_t sc = AlignUp(CeilDiv(count, n), alignElems);
+    uint64_t b = std::min<uint64_t>(count, uint64_t(c) * sc);
+    uint64_t e = std::min<uint64_t>(count, b + sc);
+    return {b, e - b};
+}
+
+// Piece p of a span cut into pieces of pe elements (the last may be short, those past the end are empty).
+Span Piece(Span s, uint64_t pe, uint64_t p)
+{
+    uint64_t b = std::min<uint64_t>(s.len, p * pe);
+    uint64_t e = std::min<uint64_t>(s.len, b + pe);
+    return {s.begin + b, e - b};
+}
+
+// Granule choice: the requested piece size, else about a quarter of the per-peer slice within [256 KiB, 16 MiB];
+// then shrunk until `slotsNeeded` staging pieces fit the scratch capacity.
+uint64_t PieceElems(const ScheduleParams& p, uint64_t sliceElems, uint64_t slotsNeeded)
+{
+    const uint64_t es = p.elemSize;
+    const uint64_t alignElems = std::max<uint64_t>(1, kAlignBytes / es);
+    uint64_t bytes = p.pieceBytes;
+    if (bytes == 0) {
+        bytes = std::clamp<uint64_t>(sliceElems * es / 4, 256ull << 10, 16ull << 20);
+    }
+    if (p.scratchCapBytes != 0 && slotsNeeded != 0) {
+        uint64_t capPer = p.scratchCapBytes / slotsNeeded;
+        capPer = capPer / kAlignBytes * kAlignBytes;
+        if (capPer == 0) capPer = kAlignBytes;
+        bytes = std::min(bytes, capPer);
+    }
+    uint64_t pe = std::max<uint64_t>(alignElems, bytes / es / alignElems * alignElems);
+    return pe;
+}
+
+Ref In(uint64_t off) { return {HCCL_AMD_BUF_INPUT, off}; }
+Ref Out(uint64_t off) { return {HCCL_AMD_BUF_OUTPUT, off}; }
+Ref Scr(uint64_t off) { return {HCCL_AMD_BUF_SCRATCH, off}; }
+
+// Peer visiting order for mesh steps: me+1, me+2, ... (each rank starts on a different link).
+std::vector<uint32_t> PeerOrder(uint32_t n, uint32_t me)
+{
+    std::vector<uint32_t> v;
+    for (uint32_t i = 1; i < n; ++i) v.push_back((me + i) % n);
+    return v;
+}
+
+// Index of peer q among the n-1 peers in ascending rank order (slot layout of the staging area).
+uint32_t PeerSlot(uint32_t q, uint32_t me) { return q < me ? q : q - 1; }
+
+// ------------------------------------------------------------------------------------------- AllReduce
+
+// One-shot (O1): every rank sends its whole input to every peer; each rank folds own + peers ascending.
+void AllReduceOneShot(const ScheduleParams& p, Builder& b)
+{
+    const uint32_t n = p.nRanks, me = p.rank;
+    const uint64_t kSlots = 2;
+    const uint64_t pe = PieceElems(p, p.count, kSlots * (n - 1));
+    const uint64_t np = CeilDiv(p.count, pe);
+    auto slot = [&](uint64_t t, uint32_t q) { return Scr(((t % kSlots) * (n - 1) + PeerSlot(q, me)) * pe); };
+    for (uint64_t t = 0; t < np; ++t) {
+        Span s = Piece({0, p.count}, pe, t);
+        for (uint32_t q : PeerOrder(n, me)) {
+            b.Send(q, In(s.begin), s.len);
+            b.Recv(q, slot(t, q), s.len);
+        }
+        b.EndGroup();
+        std::vector<Ref> srcs{In(s.begin)};
+        for (uint32_t q = 0; q < n; ++q) {
+            if (q != me) srcs.push_back(slot(t, q));
+        }
+        b.Reduce(Out(s.begin), srcs, s.len);
+    }
+}
+
+// Two-shot (O2): mesh reduce-scatter of n chunks, fold of chunk `me` in rank order 0..n-1, mesh all-gather.
+// Step t posts the scatter of piece t together with the gather of piece t-2 in one group, so the reduce of piece
+// t-1 runs while both transfers are on the links.
+void AllReduceTwoShot(const ScheduleParams& p, Builder& b)
+{
+    const uint32_t n = p.nRanks, me = p.rank;
+    const uint64_t alignElems = std::max<uint64_t>(1, kAlignBytes / p.elemSize);
+    const uint64_t kSlots = 2;
+    const Span mine = Chunk(p.count, n, me, alignElems);
+    const uint64_t maxChunk = Chunk(p.count, n, 0, alignElems).len;
+    const uint64_t pe = PieceElems(p, maxChunk, kSlots * (n - 1));
+    const uint64_t np = std::max<uint64_t>(1, CeilDiv(maxChunk, pe));
+    auto slot = [&](uint64_t t, uint32_t q) { return Scr(((t % kSlots) * (n - 1) + PeerSlot(q, me)) * pe); };
+    for (uint64_t t = 0; t < np + 2; ++t) {
+        if (t < np) {
+            Span rs = Piece(mine, pe, t);
+            for (uint32_t q : PeerOrder(n, me)) {
+                Span out = Piece(Chunk(p.count, n, q, alignElems), pe, t);
+                b.Send(q, In(out.begin), out.len);
+                b.Recv(q, slot(t, q), rs.len);
+            }
+        }
+        if (t >= 2) {
+            uint64_t g = t - 2;
+            Span mineP = Piece(mine, pe, g);
+            for (uint32_t q : PeerOrder(n, me)) {
+                Span theirs = Piece(Chunk(p.count, n, q, alignElems), pe, g);
+                b.Send(q, Out(mineP.begin), mineP.len);
+                b.Recv(q, Out(theirs.begin), theirs.len);
+            }
+        }
+        b.EndGroup();
+        if (t < np) {
+            Span rs = Piece(mine, pe, t);
+            std::vector<Ref> srcs;
+            for (uint32_t q = 0; q < n; ++q) srcs.push_back(q == me ? In(rs.begin) : slot(t, q));
+            b.Reduce(Out(rs.begin), srcs, rs.len);
+        }
+    }
+}
+
+// Ring: n-1 reduce-scatter steps (rank r receives chunk r-s-2 from r-1 and folds it into its own copy), then n-1
+// all-gather steps; rank r owns chunk r. Pieces pipeline the steps.
+void AllReduceRing(const ScheduleParams& p, Builder& b)
+{
+    const uint32_t n = p.nRanks, me = p.rank;
+    const uint64_t alignElems = std::max<uint64_t>(1, kAlignBytes / p.elemSize);
+    const uint64_t kSlots = 4;
+    const uint64_t maxChunk = Chunk(p.count, n, 0, alignElems).len;
+    const uint64_t pe = PieceElems(p, maxChunk, kSlots);
+    const uint64_t np = std::max<uint64_t>(1, CeilDiv(maxChunk, pe));
+    const uint32_t next = (me + 1) % n, prev = (me + n - 1) % n;
+    uint64_t unit = 0;
+    for (uint32_t s = 0; s + 1 < n; ++s) {
+        const uint32_t cs = (me + 2 * n - s - 1) % n;
+        const uint32_t cr = (me + 2 * n - s - 2) % n;
+        for (uint64_t t = 0; t < np; ++t, ++unit) {
+            Span snd = Piece(Chunk(p.count, n, cs, alignElems), pe, t);
+            Span rcv = Piece(Chunk(p.count, n, cr, alignElems), pe, t);
+            Ref stage = Scr((unit % kSlots) * pe);
+            b.Send(next, s == 0 ? In(snd.begin) : Out(snd.begin), snd.len);
+            b.Recv(prev, stage, rcv.len);
+            b.EndGroup();
+            b.Reduce(Out(rcv.begin), {In(rcv.begin), stage}, rcv.len);
+        }
+    }
+    for (uint32_t s = 0; s + 1 < n; ++s) {
+        const uint32_t cs = (me + n - s) % n;
+        const uint32_t cr = (me + 2 * n - s - 1) % n;
+        for (uint64_t t = 0; t < np; ++t) {
+            Span snd = Piece(Chunk(p.count, n, cs, alignElems), pe, t);
+            Span rcv = Piece(Chunk(p.count, n, cr, alignElems), pe, t);
+            b.Send(next, Out(snd.begin), snd.len);
+            b.Recv(prev, Out(rcv.begin), rcv.len);
+            b.EndGroup();
+        }
+    }
+}
+
+// Recursive halving (reduce-scatter) then recursive doubling (all-gather), power-of-two n. Region = chunk range
+// [lo, hi); at distance d the rank keeps the half selected by bit d of its rank and exchanges the other half with
+// rank ^ d. Ends with rank r owning chunk r.
+void AllReduceRhd(const ScheduleParams& p, Builder& b)
+{
+    const uint32_t n = p.nRanks, me = p.rank;
+    const uint64_t alignElems = std::max<uint64_t>(1, kAlignBytes / p.elemSize);
+    const uint64_t kSlots = 4;
+    auto range = [&](uint32_t lo, uint32_t hi) {
+        Span a = Chunk(p.count, n, lo, alignElems);
+        Span z = Chunk(p.count, n, hi - 1, alignElems);
+        return Span{a.begin, z.begin + z.len - a.begin};
+    };
+    const uint64_t pe = PieceElems(p, range(0, n / 2).len, kSlots);
+    uint64_t unit = 0;
+    uint32_t lo = 0, hi = n;
+    bool first = true;
+    for (uint32_t d = n / 2; d >= 1; d /= 2) {
+        const uint32_t partner = me ^ d;
+        const uint32_t mid = lo + d;
+        const bool keepLow = (me & d) == 0;
+        const Span keep = keepLow ? range(lo, mid) : range(mid, hi);
+        const Span give = keepLow ? range(mid, hi) : range(lo, mid);
+        const uint64_t np = std::max<uint64_t>(1, CeilDiv(std::max(keep.len, give.len), pe));
+        for (uint64_t t = 0; t < np; ++t, ++unit) {
+            Span g = Piece(give, pe, t);
+            Span k = Piece(keep, pe, t);
+            Ref stage = Scr((unit % kSlots) * pe);
+            b.Send(partner, first ? In(g.begin) : Out(g.begin), g.len);
+            b.Recv(partner, stage, k.len);
+            b.EndGroup();
+            b.Reduce(Out(k.begin), {first ? In(k.begin) : Out(k.begin), stage}, k.len);
+        }
+        if (keepLow) {
+            hi = mid;
+        } else {
+            lo = mid;
+        }
+        first = false;
+        if (d == 1) break;
+    }
+    for (uint32_t d = 1; d < n; d *= 2) {
+        const uint32_t partner = me ^ d;
+        // my region is [lo, lo + d) chunks; the partner's is the adjacent block of d chunks
+        const uint32_t plo = (me & d) == 0 ? lo + d : lo - d;
+        const Span mine = range(lo, lo + d);
+        const Span theirs = range(plo, plo + d);
+        const uint64_t np = std::max<uint64_t>(1, CeilDiv(std::max(mine.len, theirs.len), pe));
+        for (uint64_t t = 0; t < np; ++t) {
+            Span m = Piece(mine, pe, t);
+            Span th = Piece(theirs, pe, t);
+            b.Send(partner, Out(m.begin), m.len);
+            b.Recv(partner, Out(th.begin), th.len);
+            b.EndGroup();
+        }
+        lo = std::min(lo, plo);
+    }
+}
+
+// ------------------------------------------------------------------------------------------- ReduceScatter
+
+// Mesh (O1): every rank sends block q to rank q; rank me folds its own block first, then peers ascending
+// (ins_temp_reduce_scatter_mesh_1D.cc:138-206). count = recvCount, input block q at q * count.
+void ReduceScatterMesh(const ScheduleParams& p, Builder& b)
+{
+    const uint32_t n = p.nRanks, me = p.rank;
+    const uint64_t rc = p.count;
+    const uint64_t kSlots = 2;
+    const uint64_t pe = PieceElems(p, rc, kSlots * (n - 1));
+    const uint64_t np = std::max<uint64_t>(1, CeilDiv(rc, pe));
+    auto slot = [&](uint64_t t, uint32_t q) { return Scr(((t % kSlots) * (n - 1) + PeerSlot(q, me)) * pe); };
+    for (uint64_t t = 0; t < np; ++t) {
+        Span s = Piece({0, rc}, pe, t);
+        for (uint32_t q : PeerOrder(n, me)) {
+            b.Send(q, In(uint64_t(q) * rc + s.begin), s.len);
+            b.Recv(q, slot(t, q), s.len);
+        }
+        b.EndGroup();
+        std::vector<Ref> srcs{In(uint64_t(me) * rc + s.begin)};
+        for (uint32_t q = 0; q < n; ++q) {
+            if (q != me) srcs.push_back(slot(t, q));
+        }
+        b.Reduce(Out(s.begin), srcs, s.len);
+    }
+}
+
+// Ring reduce-scatter: step s, rank r sends block r-s-1 (its partial) to r+1 and folds block r-s-2 received from
+// r-1 into its own input; partials live in staging slots until forwarded, the last step writes recvBuf. Rounds of
+// kRound pieces bound the staging to 2 * kRound pieces.
+void ReduceScatterRing(const ScheduleParams& p, Builder& b)
+{
+    const uint32_t n = p.nRanks, me = p.rank;
+    const uint64_t rc = p.count;
+    const uint64_t kRound = 4;
+    const uint64_t pe = PieceElems(p, rc, 2 * kRound);
+    const uint64_t np = std::max<uint64_t>(1, CeilDiv(rc, pe));
+    const uint32_t next = (me + 1) % n, prev = (me + n - 1) % n;
+    for (uint64_t r0 = 0; r0 < np; r0 += kRound) {
+        const uint64_t r1 = std::min(np, r0 + kRound);
+        for (uint32_t s = 0; s + 1 < n; ++s) {
+            const uint32_t cs = (me + 2 * n - s - 1) % n;
+            const uint32_t cr = (me + 2 * n - s - 2) % n;
+            for (uint64_t t = r0; t < r1; ++t) {
+                Span piece = Piece({0, rc}, pe, t);
+                Ref cur = Scr(((s % 2) * kRound + (t - r0)) * pe);
+                Ref prevSlot = Scr((((s + 1) % 2) * kRound + (t - r0)) * pe);
+                b.Send(next, s == 0 ? In(uint64_t(cs) * rc + piece.begin) : prevSlot, piece.len);
+                b.Recv(prev, cur, piece.len);
+                b.EndGroup();
+                Ref dst = (s + 2 == n) ? Out(piece.begin) : cur;
+                b.Reduce(dst, {In(uint64_t(cr) * rc + piece.begin), cur}, piece.len);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------- Reduce
+
+// Mesh one-shot (O1, me = root): peers send their whole input to the root, which folds own + peers ascending
+// (reduce_mesh_1D.cc:136-249). Non-root recvBuf is not touched.
+void ReduceOneShot(const ScheduleParams& p, Builder& b)
+{
+    const uint32_t n = p.nRanks, me = p.rank, root = p.root;
+    const uint64_t kSlots = 2;
+    const uint64_t pe = PieceElems(p, p.count, kSlots * (n - 1));
+    const uint64_t np = CeilDiv(p.count, pe);
+    auto slot = [&](uint64_t t, uint32_t q) { return Scr(((t % kSlots) * (n - 1) + PeerSlot(q, root)) * pe); };
+    for (uint64_t t = 0; t < np; ++t) {
+        Span s = Piece({0, p.count}, pe, t);
+        if (me != root) {
+            b.Send(root, In(s.begin), s.len);
+            b.EndGroup();
+            continue;
+        }
+        for (uint32_t q : PeerOrder(n, me)) b.Recv(q, slot(t, q), s.len);
+        b.EndGroup();
+        std::vector<Ref> srcs{In(s.begin)};
+        for (uint32_t q = 0; q < n; ++q) {
+            if (q != me) srcs.push_back(slot(t, q));
+        }
+        b.Reduce(Out(s.begin), srcs, s.len);
+    }
+}
+
+// Two-shot: mesh reduce-scatter with O1 per chunk owner (reduce_mesh_1D_two_shot.cc:209-249), then the owners send
+// their reduced chunks to the root. Non-roots fold into a staging slot, so their recvBuf is not touched.
+void ReduceTwoShot(const ScheduleParams& p, Builder& b)
+{
+    const uint32_t n = p.nRanks, me = p.rank, root = p.root;
+    const uint64_t alignElems = std::max<uint64_t>(1, kAlignBytes / p.elemSize);
+    const uint64_t kSlots = 2;
+    const Span mine = Chunk(p.count, n, me, alignElems);
+    const uint64_t maxChunk = Chunk(p.count, n, 0, alignElems).len;
+    // slots: kSlots x (n-1) receive pieces + kSlots reduced pieces (non-root)
+    const uint64_t pe = PieceElems(p, maxChunk, kSlots * n);
+    const uint64_t np = std::max<uint64_t>(1, CeilDiv(maxChunk, pe));
+    auto slot = [&](uint64_t t, uint32_t q) { return Scr(((t % kSlots) * (n - 1) + PeerSlot(q, me)) * pe); };
+    auto red = [&](uint64_t t) { return Scr((kSlots * (n - 1) + (t % kSlots)) * pe); };
+    for (uint64_t t = 0; t < np + 2; ++t) {
+        if (t < np) {
+            Span rs = Piece(mine, pe, t);
+            for (uint32_t q : PeerOrder(n, me)) {
+                Span out = Piece(Chunk(p.count, n, q, alignElems), pe, t);
+                b.Send(q, In(out.begin), out.len);
+                b.Recv(q, slot(t, q), rs.len);
+            }
+        }
+        if (t >= 2) {
+            uint64_t g = t - 2;
+            if (me == root) {
+                for (uint32_t q : PeerOrder(n, me)) {
+                    Span theirs = Piece(Chunk(p.count, n, q, alignElems), pe, g);
+                    b.Recv(q, Out(theirs.begin), theirs.len);
+                }
+            } else {
+                b.Send(root, red(g), Piece(mine, pe, g).len);
+            }
+        }
+        b.EndGroup();
+        if (t < np) {
+            Span rs = Piece(mine, pe, t);
+            std::vector<Ref> srcs{In(rs.begin)};
+            for (uint32_t q = 0; q < n; ++q) {
+                if (q != me) srcs.push_back(slot(t, q));
+            }
+            b.Reduce(me == root ? Out(rs.begin) : red(t), srcs, rs.len);
+        }
+    }
+}
+
+bool IsPow2(uint32_t n) { return n != 0 && (n & (n - 1)) == 0; }
+
+}  // namespace
+
+int32_t SelectAlgo(int32_t opType, uint32_t nRanks, uint64_t bytes)
+{
+    switch (opType) {
+        case HCCL_AMD_OP_ALLREDUCE:
+            return bytes <= kOneShotMaxBytes ? HCCL_AMD_ALGO_MESH_ONESHOT : HCCL_AMD_ALGO_MESH_TWOSHOT;
+        case HCCL_AMD_OP_REDUCE_SCATTER: return HCCL_AMD_ALGO_MESH_ONESHOT;
+        case HCCL_AMD_OP_REDUCE:
+            return bytes < kOneShotMaxBytes ? HCCL_AMD_ALGO_MESH_ONESHOT : HCCL_AMD_ALGO_MESH_TWOSHOT;
+        default: return HCCL_AMD_ALGO_AUTO;
+    }
+}
+
+int BuildSchedule(const ScheduleParams& p, Schedule* out)
+{
+    if (p.nRanks == 0 || p.rank >= p.nRanks || p.elemSize == 0 || p.nRanks > HCCL_AMD_IR_MAX_SRC) {
+        return HCCL_E_PARA;
+    }
+    if (p.opType == HCCL_AMD_OP_REDUCE && p.root >= p.nRanks) return HCCL_E_PARA;
+    Builder b;
+    int32_t algo = p.algo;
+    uint64_t bytes = p.count * p.elemSize;
+    if (algo == HCCL_AMD_ALGO_AUTO) algo = SelectAlgo(p.opType, p.nRanks, bytes);
+    if (p.nRanks == 1) {
+        // SingleRankProc (op_common.cc:3042-3098): a copy when the buffers differ.
+        b.Copy(Out(0), In(0), p.count);
+        out->ops = std::move(b.ops);
+        out->algo = algo;
+        out->scratchElems = 0;
+        return HCCL_SUCCESS;
+    }
+    switch (p.opType) {
+        case HCCL_AMD_OP_ALLREDUCE:
+            if (algo == HCCL_AMD_ALGO_RHD && !IsPow2(p.nRanks)) algo = HCCL_AMD_ALGO_RING;
+            switch (algo) {
+                case HCCL_AMD_ALGO_MESH_ONESHOT: AllReduceOneShot(p, b); break;
+                case HCCL_AMD_ALGO_MESH_TWOSHOT: AllReduceTwoShot(p, b); break;
+                case HCCL_AMD_ALGO_RING: AllReduceRing(p, b); break;
+                case HCCL_AMD_ALGO_RHD: AllReduceRhd(p, b); break;
+                default: return HCCL_E_PARA;
+            }
+            break;
+        case HCCL_AMD_OP_REDUCE_SCATTER:
+            if (algo == HCCL_AMD_ALGO_MESH_TWOSHOT || algo == HCCL_AMD_ALGO_RHD) algo = HCCL_AMD_ALGO_MESH_ONESHOT;
+            switch (algo) {
+                case HCCL_AMD_ALGO_MESH_ONESHOT: ReduceScatterMesh(p, b); break;
+                case HCCL_AMD_ALGO_RING: ReduceScatterRing(p, b); break;
+                default: return HCCL_E_PARA;
+            }
+            break;
+        case HCCL_AMD_OP_REDUCE:
+            if (algo == HCCL_AMD_ALGO_RING || algo == HCCL_AMD_ALGO_RHD) algo = HCCL_AMD_ALGO_MESH_TWOSHOT;
+            switch (algo) {
+                case HCCL_AMD_ALGO_MESH_ONESHOT: ReduceOneShot(p, b); break;
+                case HCCL_AMD_ALGO_MESH_TWOSHOT: ReduceTwoShot(p, b); break;
+                default: return HCCL_E_PARA;
+            }
+            break;
+        default: return HCCL_E_PARA;
+    }
+    out->ops = std::move(b.ops);
+    out->algo = algo;
+    out->scratchElems = b.scratchHigh;
+    return HCCL_SUCCESS;
+}
+
+}  // namespace hccl_amd

@@ -1,0 +1,43 @@
+// schedule.h — per-rank schedule IR generators for the reducing collectives.
+//
+// A schedule is the list of HcclAmdIrOp records one rank executes (include/hccl_amd.h). It plays the role of the
+// reference's algorithm templates (src/ops/*/template/aicpu/*.cc): which slices are sent to
+// which peer, and which slices are folded in which order. Everything here is host-only integer logic; the same
+// records are executed by the HIP/RCCL executor (executor.cc) and replayed by the CPU oracle.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "../../include/hccl_amd.h"
+
+namespace hccl_amd {
+
+struct ScheduleParams {
+    int32_t opType = HCCL_AMD_OP_ALLREDUCE;
+    int32_t algo = HCCL_AMD_ALGO_AUTO;
+    uint32_t nRanks = 1;
+    uint32_t rank = 0;
+    uint64_t count = 0;  // AllReduce/Reduce: elements per rank; ReduceScatter: recvCount
+    uint32_t elemSize = 4;
+    uint32_t root = 0;
+    uint64_t pieceBytes = 0;        // 0 = default
+    uint64_t scratchCapBytes = 0;   // 0 = unbounded
+};
+
+struct Schedule {
+    std::vector<HcclAmdIrOp> ops;
+    int32_t algo = -1;
+    uint64_t scratchElems = 0;
+};
+
+// Reference selector policy for a single-node full mesh (Level0Shape::MESH_1D):
+//   AllReduce  <= 8 MiB one-shot, else two-shot      all_reduce_auto_selector.cc:517-550
+//   ReduceScatter mesh                               reduce_scatter_auto_selector.cc:473-500
+//   Reduce     <  8 MiB one-shot mesh, else two-shot reduce_auto_selector.cc:312-324
+int32_t SelectAlgo(int32_t opType, uint32_t nRanks, uint64_t bytes);
+
+// Returns HCCL_E_PARA for an invalid combination, HCCL_SUCCESS otherwise.
+int BuildSchedule(const ScheduleParams& p, Schedule* out);
+
+}  // namespace hccl_amd

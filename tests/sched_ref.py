@@ -1,0 +1,145 @@
+"""Closed-form expected results of every schedule, written independently of the C++ generators.
+
+Each function returns, for every rank, the output buffer the collective must produce, built from the
+association orders of SURVEY.md Appendix A with the oracle's element rule (acc = src (op) dst, where the incoming
+or later operand is src, as in the reference's LocalReduce / write-reduce / read-reduce conventions):
+
+  O1  one-shot AllReduce, mesh ReduceScatter, Reduce:  acc = x_me; acc = x_q (op) acc, q ascending, q != me
+  O2  two-shot AllReduce:                              acc = x_0;  acc = x_q (op) acc, q = 1 .. n-1
+  ring (chunk c, owner c):   acc = x_{c+1}; acc = acc (op) x_{c+k}   (the travelling partial is src)
+  RHD  pairwise: at distance d the kept half becomes partner_partial (op) my_partial
+"""
+import numpy as np
+
+from oracle import oracle as O
+
+ALIGN = 128
+
+
+def chunk_bounds(count, n, es):
+    align = max(1, ALIGN // es)
+    sc = -(-count // n)
+    sc = -(-sc // align) * align
+    out = []
+    for c in range(n):
+        b = min(count, c * sc)
+        e = min(count, b + sc)
+        out.append((b, e))
+    return out
+
+
+def fold(dtype, op, arrays):
+    return O.reduce_n(dtype, op, [np.ascontiguousarray(a) for a in arrays])
+
+
+def apply(dtype, op, src, dst):
+    """dst' = src (op) dst, returns a new array."""
+    return O.local_reduce(dtype, op, np.ascontiguousarray(dst).copy(), np.ascontiguousarray(src))
+
+
+def allreduce_o1(dtype, op, xs):
+    n = len(xs)
+    return [fold(dtype, op, [xs[me]] + [xs[q] for q in range(n) if q != me]) for me in range(n)]
+
+
+def allreduce_o2(dtype, op, xs):
+    r = fold(dtype, op, xs)
+    return [r.copy() for _ in xs]
+
+
+def ring_chunk(dtype, op, xs, c, sl):
+    n = len(xs)
+    acc = xs[(c + 1) % n][sl].copy()
+    for k in range(2, n + 1):
+        acc = apply(dtype, op, acc, xs[(c + k) % n][sl])
+    return acc
+
+
+def allreduce_ring(dtype, op, xs):
+    n = len(xs)
+    es = xs[0].itemsize
+    out = np.empty_like(xs[0])
+    for c, (b, e) in enumerate(chunk_bounds(xs[0].size, n, es)):
+        if e > b:
+            out[b:e] = ring_chunk(dtype, op, xs, c, slice(b, e))
+    return [out.copy() for _ in xs]
+
+
+def allreduce_rhd(dtype, op, xs):
+    n = len(xs)
+    es = xs[0].itemsize
+    bounds = chunk_bounds(xs[0].size, n, es)
+    part = [x.copy() for x in xs]  # each rank's running partial (only its kept region is meaningful)
+    lo = [0] * n
+    hi = [n] * n
+    d = n // 2
+    while d >= 1:
+        new = [p.copy() for p in part]
+        for r in range(n):
+            partner = r ^ d
+            mid = lo[r] + d
+            keep = (lo[r], mid) if (r & d) == 0 else (mid, hi[r])
+            b, e = bounds[keep[0]][0], bounds[keep[1] - 1][1]
+            if e > b:
+                new[r][b:e] = apply(dtype, op, part[partner][b:e], part[r][b:e])
+        for r in range(n):
+            if (r & d) == 0:
+                hi[r] = lo[r] + d
+            else:
+                lo[r] = lo[r] + d
+        part = new
+        d //= 2
+    out = np.empty_like(xs[0])
+    for c, (b, e) in enumerate(bounds):
+        if e > b:
+            out[b:e] = part[c][b:e]
+    return [out.copy() for _ in xs]
+
+
+def reduce_scatter_o1(dtype, op, xs, rc):
+    n = len(xs)
+    blk = lambda r, q: xs[r][q * rc:(q + 1) * rc]  # noqa: E731
+    return [fold(dtype, op, [blk(me, me)] + [blk(q, me) for q in range(n) if q != me]) for me in range(n)]
+
+
+def reduce_scatter_ring(dtype, op, xs, rc):
+    n = len(xs)
+    outs = []
+    for me in range(n):
+        blocks = [x[me * rc:(me + 1) * rc] for x in xs]
+        acc = blocks[(me + 1) % n].copy()
+        for k in range(2, n + 1):
+            acc = apply(dtype, op, acc, blocks[(me + k) % n])
+        outs.append(acc)
+    return outs
+
+
+def reduce_oneshot(dtype, op, xs, root):
+    n = len(xs)
+    return fold(dtype, op, [xs[root]] + [xs[q] for q in range(n) if q != root])
+
+
+def reduce_twoshot(dtype, op, xs, root):
+    n = len(xs)
+    es = xs[0].itemsize
+    out = np.empty_like(xs[0])
+    for c, (b, e) in enumerate(chunk_bounds(xs[0].size, n, es)):
+        if e > b:
+            out[b:e] = fold(dtype, op, [xs[c][b:e]] + [xs[q][b:e] for q in range(n) if q != c])
+    return out
+
+
+ALGO_ONESHOT, ALGO_TWOSHOT, ALGO_RING, ALGO_RHD = 1, 2, 3, 4
+
+
+def expected(op_type, algo, dtype, op, xs, count, root=0):
+    """Per-rank expected outputs (Reduce: only the root's entry is meaningful; others are None)."""
+    if op_type == 0:
+        return {ALGO_ONESHOT: allreduce_o1, ALGO_TWOSHOT: allreduce_o2, ALGO_RING: allreduce_ring,
+                ALGO_RHD: allreduce_rhd}[algo](dtype, op, xs)
+    if op_type == 1:
+        return {ALGO_ONESHOT: reduce_scatter_o1, ALGO_RING: reduce_scatter_ring}[algo](dtype, op, xs, count)
+    if op_type == 2:
+        r = {ALGO_ONESHOT: reduce_oneshot, ALGO_TWOSHOT: reduce_twoshot}[algo](dtype, op, xs, root)
+        return [r if q == root else None for q in range(len(xs))]
+    raise ValueError(op_type)

@@ -1,0 +1,144 @@
+"""Schedule IR (libhccl_amd.so, host-only code) replayed by the CPU oracle — no GPU needed.
+
+For every collective x algorithm x rank count the per-rank programs from HcclAmdBuildSchedule are replayed by
+orc_replay (one "sim world", the reference ST's idea with real data: test/st/algorithm/testcase/*.cc) and the
+outputs are compared bit-for-bit with closed-form association orders written independently (tests/sched_ref.py).
+This pins, e.g., that the two-shot AllReduce reproduces the reference's O2 order and the one-shot its O1 order.
+It also covers config C1 (2 ranks, 1 MiB fp32 AllReduce on the host).
+"""
+import time
+
+import numpy as np
+import pytest
+
+import hccl_amd as H
+from oracle import oracle as O
+from tests import sched_ref as R
+
+AR, RS, RED = 0, 1, 2
+
+
+def programs(op_type, algo, n, count, dtype, root=0, piece_bytes=0):
+    progs, used = [], set()
+    scratch = 0
+    for r in range(n):
+        arr, nops, algo_used, se = H.build_schedule(op_type, algo, n, r, count, dtype, root, piece_bytes)
+        progs.append((arr, nops))
+        used.add(algo_used)
+        scratch = max(scratch, se)
+    assert len(used) == 1
+    return progs, used.pop(), scratch
+
+
+def run(op_type, algo, n, count, dtype, op, root=0, piece_bytes=0, inplace=False, seed=0):
+    progs, used, scratch = programs(op_type, algo, n, count, dtype, root, piece_bytes)
+    in_count = count * n if op_type == RS else count
+    st = O.NP_STORAGE[dtype]
+    xs = [O.random_operands(dtype, in_count, seed=seed * 100 + r, edge=False, small_ints=True) for r in range(n)]
+    bufs = []
+    outs = []
+    for r in range(n):
+        inp = xs[r].copy()
+        out = inp if inplace else np.zeros(count, st)
+        outs.append(out)
+        bufs.append([inp, out, np.zeros(max(scratch, 1), st)])
+    ret = O.replay(n, dtype, op, progs, bufs)
+    assert ret == 0, f"replay returned {ret}"
+    if inplace:
+        outs = [o[:count] for o in outs]
+    return used, xs, outs
+
+
+CASES = [
+    (AR, 1), (AR, 2), (AR, 3), (AR, 4),
+    (RS, 1), (RS, 3),
+    (RED, 1), (RED, 2),
+]
+
+
+@pytest.mark.parametrize("count", [1, 7, 1000, 65537])
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 8])
+@pytest.mark.parametrize("op_type,algo", CASES)
+def test_schedule_fp32_sum_matches_reference_order(op_type, algo, n, count):
+    dtype, op = O.FP32, O.SUM
+    used, xs, outs = run(op_type, algo, n, count, dtype, op, root=n - 1, piece_bytes=4096, seed=n)
+    want = R.expected(op_type, used, dtype, op, xs, count, root=n - 1)
+    for r in range(n):
+        if op_type == RED and r != n - 1:
+            assert not outs[r].any(), "Reduce must not write a non-root recvBuf"
+            continue
+        assert O.equal_bits(dtype, outs[r], want[r]), (op_type, used, n, count, r)
+
+
+@pytest.mark.parametrize("dtype", [O.INT8, O.INT32, O.INT64, O.UINT64, O.FP16, O.BFP16, O.FP64],
+                         ids=lambda v: O.DTYPE_NAMES[v])
+@pytest.mark.parametrize("op", O.OPS, ids=lambda v: O.OP_NAMES[v])
+@pytest.mark.parametrize("op_type,algo", CASES)
+def test_schedule_dtypes_ops(op_type, algo, dtype, op):
+    n, count = 4, 3001
+    used, xs, outs = run(op_type, algo, n, count, dtype, op, root=1, piece_bytes=1024, seed=7)
+    want = R.expected(op_type, used, dtype, op, xs, count, root=1)
+    for r in range(n):
+        if want[r] is None:
+            continue
+        assert O.equal_bits(dtype, outs[r], want[r]), (op_type, used, r)
+
+
+@pytest.mark.parametrize("algo", [1, 2, 3, 4])
+def test_allreduce_inplace(algo):
+    n, count = 4, 50000
+    used, xs, outs = run(AR, algo, n, count, O.FP32, O.SUM, piece_bytes=8192, inplace=True, seed=3)
+    want = R.expected(AR, used, O.FP32, O.SUM, xs, count)
+    for r in range(n):
+        assert O.equal_bits(O.FP32, outs[r], want[r])
+
+
+def test_auto_selection_follows_reference_thresholds():
+    """all_reduce_auto_selector.cc:545-550, reduce_scatter_auto_selector.cc:491, reduce_auto_selector.cc:319-324."""
+    mib = 1 << 20
+    assert programs(AR, 0, 8, 8 * mib // 4, O.FP32)[1] == R.ALGO_ONESHOT        # <= 8 MiB
+    assert programs(AR, 0, 8, 8 * mib // 4 + 1, O.FP32)[1] == R.ALGO_TWOSHOT    # > 8 MiB
+    assert programs(RS, 0, 8, 1024, O.FP32)[1] == R.ALGO_ONESHOT
+    assert programs(RED, 0, 8, 8 * mib // 4 - 1, O.FP32)[1] == R.ALGO_ONESHOT   # < 8 MiB
+    assert programs(RED, 0, 8, 8 * mib // 4, O.FP32)[1] == R.ALGO_TWOSHOT
+
+
+def test_rhd_non_power_of_two_falls_back_to_ring():
+    assert programs(AR, 4, 6, 1000, O.FP32)[1] == R.ALGO_RING
+
+
+def test_schedule_scratch_is_bounded():
+    """The staging a schedule addresses never exceeds the communicator's CCL buffer (256 MiB default)."""
+    for op_type, algo in CASES:
+        for n in (2, 8):
+            count = (4 << 30) // 4 // (n if op_type == RS else 1)
+            _, _, scratch = programs(op_type, algo, n, count, O.FP32)
+            assert scratch * 4 <= 256 << 20, (op_type, algo, n, scratch)
+
+
+def test_sends_and_recvs_pair_up():
+    """Every SEND has the matching RECV (same size, same posting order) on the peer."""
+    for op_type, algo in CASES:
+        n = 5
+        progs, _, _ = programs(op_type, algo, n, 4099, O.FP32, root=2, piece_bytes=2048)
+        for a in range(n):
+            for b in range(n):
+                if a == b:
+                    continue
+                sends = [o.count for o in progs[a][0][:progs[a][1]] if o.kind == 2 and o.peer == b]
+                recvs = [o.count for o in progs[b][0][:progs[b][1]] if o.kind == 3 and o.peer == a]
+                assert sends == recvs, (op_type, algo, a, b)
+
+
+def test_c1_sim_two_rank_1mib_allreduce():
+    """Config C1: 2-rank AllReduce SUM, 1 MiB fp32, schedule replayed on the host (reference analogue:
+    RunAllReduceCase, test/st/algorithm/testcase/all_reduce_testcase.cc:48-111, but with real data)."""
+    count = (1 << 20) // 4
+    t0 = time.perf_counter()
+    used, xs, outs = run(AR, 0, 2, count, O.FP32, O.SUM, seed=11)
+    dt = time.perf_counter() - t0
+    assert used == R.ALGO_ONESHOT
+    want = R.expected(AR, used, O.FP32, O.SUM, xs, count)
+    for r in range(2):
+        assert O.equal_bits(O.FP32, outs[r], want[r])
+    assert dt < 30
