@@ -77,6 +77,74 @@ def cpu_baseline_c2(budget_s: float = 12.0) -> dict:
     }
 
 
+def c1_sim_replay() -> dict:
+    """Config C1: 2-rank AllReduce SUM, 1 MiB fp32, the product's schedules replayed on the host by the oracle's
+    sim world (the reference's only multi-rank-without-hardware path is its host simulator)."""
+    from oracle import oracle as O
+
+    count = (1 << 20) // 4
+    progs, scratch = [], 0
+    for r in range(2):
+        arr, nops, algo, se = H.build_schedule(H.OpType.ALLREDUCE, H.Algo.AUTO, 2, r, count, H.HcclDataType.FP32)
+        progs.append((arr, nops))
+        scratch = max(scratch, se)
+    rng = np.random.default_rng(0x5EED0001)
+    xs = [rng.random(count, dtype=np.float32) for _ in range(2)]
+    times = []
+    for _ in range(7):
+        bufs = [[x.copy(), np.zeros(count, np.float32), np.zeros(max(scratch, 1), np.float32)] for x in xs]
+        t0 = time.perf_counter()
+        assert O.replay(2, O.FP32, O.SUM, progs, bufs) == 0
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return {"workload": "C1: 2-rank AllReduce SUM 1 MiB fp32, schedule replay on host (one-shot, order O1)",
+            "us": round(med * 1e6, 1), "GiBps_per_rank_input": round((1 << 20) / med / GIB, 3), "cores": 1}
+
+
+def end_to_end_host(steps: int = 5) -> dict:
+    """Gradient buckets that start and end in host memory: pinned H2D of both operands, the reduce, D2H of the
+    result, all on one stream (BASELINE.json). Rate = 3 GiB of algorithmic bytes per step over the wall time."""
+    dev = torch.device("cuda", 0)
+    h_src = torch.empty(C2_COUNT, dtype=torch.float32).pin_memory()
+    h_dst = torch.empty(C2_COUNT, dtype=torch.float32).pin_memory()
+    h_src.uniform_(-1, 1)
+    h_dst.uniform_(-1, 1)
+    d_src = torch.empty(C2_COUNT, device=dev)
+    d_dst = torch.empty(C2_COUNT, device=dev)
+    s = torch.cuda.current_stream()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+
+    def step(rec):
+        if rec:
+            evs[0].record(s)
+        d_src.copy_(h_src, non_blocking=True)
+        d_dst.copy_(h_dst, non_blocking=True)
+        if rec:
+            evs[1].record(s)
+        H.local_reduce(d_dst, d_src, H.HcclReduceOp.SUM, s)
+        if rec:
+            evs[2].record(s)
+        h_dst.copy_(d_dst, non_blocking=True)
+        if rec:
+            evs[3].record(s)
+
+    step(False)
+    torch.cuda.synchronize()
+    parts = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(True)
+        torch.cuda.synchronize()
+        parts.append([evs[i].elapsed_time(evs[i + 1]) for i in range(3)])
+    wall = (time.perf_counter() - t0) / steps
+    h2d, red, d2h = (float(np.median([p[i] for p in parts])) for i in range(3))
+    return {"GiBps": round(3 * C2_COUNT * 4 / wall / GIB, 2), "ms_per_step": round(wall * 1e3, 2),
+            "h2d_ms": round(h2d, 2), "reduce_ms": round(red, 3), "d2h_ms": round(d2h, 2),
+            "h2d_GBps": round(2 * C2_COUNT * 4 / (h2d / 1e3) / 1e9, 1),
+            "d2h_GBps": round(C2_COUNT * 4 / (d2h / 1e3) / 1e9, 1),
+            "note": "pinned host buffers, one stream, 2 GiB H2D + reduce + 1 GiB D2H per step (PCIe-bound)"}
+
+
 def load_pmc_traffic(name: str):
     """Per-launch HBM bytes from the committed rocprofv3 PMC summary (profiles/), if one exists for this kernel."""
     path = os.path.join(ROOT, "profiles", name)
@@ -145,9 +213,42 @@ def bench_local(args) -> dict:
             "kernel_avg_us": round(kavg * 1e6, 2),
         },
     }
+    if not args.no_e2e:
+        try:
+            res["end_to_end_host_buffers"] = end_to_end_host()
+        except Exception as e:  # noqa: BLE001  (reported, never fatal to the headline line)
+            res["end_to_end_host_buffers"] = {"error": f"{type(e).__name__}: {e}"}
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_c2(args.cpu_budget)
+        res["cpu_baseline"]["c1_sim"] = c1_sim_replay()
     return res
+
+
+def rccl_allreduce_reference(send, recv, world, args):
+    """RCCL's own ring/tree all_reduce on the same 4 GiB buffers (torch.distributed nccl backend = RCCL), for
+    context only: it is the vendor baseline the schedules here are compared against."""
+    import torch.distributed as dist
+
+    try:
+        g = dist.new_group(backend="nccl")
+        recv.copy_(send)
+        for _ in range(2):
+            dist.all_reduce(recv, group=g)
+        torch.cuda.synchronize()
+        dist.barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        n = max(3, args.steps // 2)
+        e0.record()
+        for _ in range(n):
+            dist.all_reduce(recv, group=g)
+        e1.record()
+        torch.cuda.synchronize()
+        t = torch.tensor([e0.elapsed_time(e1) / 1e3 / n], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        algbw = C3_BYTES / float(t[0]) / 1e9
+        return {"ms_per_step": round(float(t[0]) * 1e3, 3), "busbw_GBps": round(algbw * 2 * (world - 1) / world, 2)}
+    except Exception as e:  # noqa: BLE001
+        return {"error": f"{type(e).__name__}: {e}"}
 
 
 def bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
@@ -190,6 +291,9 @@ def bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     value = world * C3_BYTES * args.steps / elapsed / GIB
     algo = comm.last_algo
     comm.destroy()
+    rccl_ref = None
+    if not args.no_rccl_ref:
+        rccl_ref = rccl_allreduce_reference(send, recv, world, args)
     dist.destroy_process_group()
     res = {
         "metric": "device-resident reduce GiB/s (fp32 sum) vs HBM peak; ring all-reduce bus GB/s",
@@ -212,6 +316,7 @@ def bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
         },
         "busbw_GBps": round(busbw, 2),
         "algbw_GBps": round(algbw, 2),
+        "rccl_allreduce_reference": rccl_ref,
         "roofline": {
             "bound": "xgmi",
             "achieved": round(busbw, 2),
@@ -231,6 +336,8 @@ def main():
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
+    p.add_argument("--no-rccl-ref", action="store_true", help="N>1: skip timing RCCL's own all_reduce beside ours")
     p.add_argument("--cpu-budget", type=float, default=12.0)
     p.add_argument("--algo", default="", help="force an AllReduce schedule (mesh_oneshot/mesh_twoshot/ring/rhd)")
     args = p.parse_args()
