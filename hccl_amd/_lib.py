@@ -77,6 +77,7 @@ class Algo(enum.IntEnum):
     MESH_TWOSHOT = 2
     RING = 3
     RHD = 4
+    NHR = 5
 
 
 class OpType(enum.IntEnum):

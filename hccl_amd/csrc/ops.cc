@@ -215,7 +215,7 @@ HcclResult HcclAmdCommSetAlgo(HcclComm comm, int32_t algo)
 {
     Comm* c = AsComm(comm);
     if (c == nullptr) return HCCL_E_PTR;
-    if (algo < HCCL_AMD_ALGO_AUTO || algo > HCCL_AMD_ALGO_RHD) return HCCL_E_PARA;
+    if (algo < HCCL_AMD_ALGO_AUTO || algo > HCCL_AMD_ALGO_NHR) return HCCL_E_PARA;
     c->algoOverride = algo;
     return HCCL_SUCCESS;
 }

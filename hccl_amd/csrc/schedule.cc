@@ -8,6 +8,7 @@
 //       ins_temp_all_reduce_mesh_1D_two_shot.cc:312-338
 //   ring (build-side; the reference has no ring AllReduce template)   chunk c: acc = x_{c+1}, then x_{c+2} .. x_c
 //   RHD (docs/zh/user_guide/coll_algo_intro/RHD.md)  pairwise tree, partner = rank ^ d, d = n/2, n/4, .., 1
+//   NHR AllReduce                                    O5: ins_temp_all_reduce_nhr.cc:230-301, 390-482
 //
 // Data movement: a rank's data leaves it through SEND/RECV records grouped into one RCCL group per pipeline step;
 // every schedule is cut into pieces ("pipelining granule") so that the transfer of piece t+1 overlaps the reduce
@@ -330,6 +331,98 @@ void AllReduceRhd(const ScheduleParams& p, Builder& b)
     }
 }
 
+// NHR (ins_temp_all_reduce_nhr.cc:171-173, 230-369, 390-482): ceil(log2 n) reduce-scatter steps in which rank r
+// sends slices r-2^k, r-2^k-2^(k+1), ... to r-2^k and receives slices r, r-2^(k+1), ... from r+2^k, folding each as
+// receiver partial (dst) (op) sender partial (src); then the mirrored all-gather. Slices are floor(count/n) with the
+// tail on the last slice. The reference works in its CCL buffer (PreCopy / PostCopy); here recvBuf is the working
+// buffer, which gives the same per-element order.
+struct NhrStep {
+    uint32_t to, from;
+    std::vector<uint32_t> tx, rx;
+};
+
+std::vector<NhrStep> NhrSteps(uint32_t n, uint32_t me, bool gather)
+{
+    uint32_t nSteps = 0;
+    for (uint32_t t = n - 1; t != 0; t >>= 1) nSteps++;
+    std::vector<NhrStep> out(nSteps);
+    for (uint32_t step = 0; step < nSteps; ++step) {
+        NhrStep& st = out[step];
+        uint32_t nSlices, delta, tx, rx;
+        if (!gather) {
+            const uint32_t dr = 1u << step;
+            st.to = (me + n - dr) % n;
+            st.from = (me + dr) % n;
+            nSlices = (n - 1 + (1u << step)) / (1u << (step + 1));
+            delta = 1u << (step + 1);
+            tx = st.to;
+            rx = me;
+        } else {
+            const uint32_t dr = 1u << (nSteps - 1 - step);
+            st.to = (me + dr) % n;
+            st.from = (me + n - dr) % n;
+            nSlices = (n - 1 + dr) / (1u << (nSteps - step));
+            delta = 1u << (nSteps - step);
+            tx = me;
+            rx = (me + n - dr) % n;
+        }
+        for (uint32_t i = 0; i < nSlices; ++i) {
+            st.tx.push_back(tx);
+            st.rx.push_back(rx);
+            tx = (tx + n - delta % n) % n;
+            rx = (rx + n - delta % n) % n;
+        }
+    }
+    return out;
+}
+
+void AllReduceNhr(const ScheduleParams& p, Builder& b)
+{
+    const uint32_t n = p.nRanks, me = p.rank;
+    const uint64_t sliceElems = p.count / n;
+    auto slice = [&](uint32_t i) {
+        return i == n - 1 ? Span{uint64_t(i) * sliceElems, p.count - sliceElems * (n - 1)}
+                          : Span{uint64_t(i) * sliceElems, sliceElems};
+    };
+    const uint64_t kSlots = 2;
+    const uint64_t maxSlices = (n + 1) / 2;
+    const uint64_t tail = slice(n - 1).len;
+    const uint64_t pe = PieceElems(p, tail, kSlots * maxSlices);
+    const uint64_t np = std::max<uint64_t>(1, CeilDiv(tail, pe));
+    b.Copy(Out(0), In(0), p.count);  // PreCopy (ins_temp_all_reduce_nhr.cc PreCopy): the working buffer
+    uint64_t unit = 0;
+    for (const NhrStep& st : NhrSteps(n, me, false)) {
+        for (uint64_t t = 0; t < np; ++t, ++unit) {
+            for (size_t i = 0; i < st.tx.size(); ++i) {
+                Span s = Piece(slice(st.tx[i]), pe, t);
+                b.Send(st.to, Out(s.begin), s.len);
+            }
+            for (size_t i = 0; i < st.rx.size(); ++i) {
+                Span s = Piece(slice(st.rx[i]), pe, t);
+                b.Recv(st.from, Scr(((unit % kSlots) * maxSlices + i) * pe), s.len);
+            }
+            b.EndGroup();
+            for (size_t i = 0; i < st.rx.size(); ++i) {
+                Span s = Piece(slice(st.rx[i]), pe, t);
+                b.Reduce(Out(s.begin), {Out(s.begin), Scr(((unit % kSlots) * maxSlices + i) * pe)}, s.len);
+            }
+        }
+    }
+    for (const NhrStep& st : NhrSteps(n, me, true)) {
+        for (uint64_t t = 0; t < np; ++t) {
+            for (size_t i = 0; i < st.tx.size(); ++i) {
+                Span s = Piece(slice(st.tx[i]), pe, t);
+                b.Send(st.to, Out(s.begin), s.len);
+            }
+            for (size_t i = 0; i < st.rx.size(); ++i) {
+                Span s = Piece(slice(st.rx[i]), pe, t);
+                b.Recv(st.from, Out(s.begin), s.len);
+            }
+            b.EndGroup();
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------- ReduceScatter
 
 // Mesh (O1): every rank sends block q to rank q; rank me folds its own block first, then peers ascending
@@ -503,11 +596,14 @@ int BuildSchedule(const ScheduleParams& p, Schedule* out)
                 case HCCL_AMD_ALGO_MESH_TWOSHOT: AllReduceTwoShot(p, b); break;
                 case HCCL_AMD_ALGO_RING: AllReduceRing(p, b); break;
                 case HCCL_AMD_ALGO_RHD: AllReduceRhd(p, b); break;
+                case HCCL_AMD_ALGO_NHR: AllReduceNhr(p, b); break;
                 default: return HCCL_E_PARA;
             }
             break;
         case HCCL_AMD_OP_REDUCE_SCATTER:
-            if (algo == HCCL_AMD_ALGO_MESH_TWOSHOT || algo == HCCL_AMD_ALGO_RHD) algo = HCCL_AMD_ALGO_MESH_ONESHOT;
+            if (algo == HCCL_AMD_ALGO_MESH_TWOSHOT || algo == HCCL_AMD_ALGO_RHD || algo == HCCL_AMD_ALGO_NHR) {
+                algo = HCCL_AMD_ALGO_MESH_ONESHOT;
+            }
             switch (algo) {
                 case HCCL_AMD_ALGO_MESH_ONESHOT: ReduceScatterMesh(p, b); break;
                 case HCCL_AMD_ALGO_RING: ReduceScatterRing(p, b); break;
@@ -515,7 +611,9 @@ int BuildSchedule(const ScheduleParams& p, Schedule* out)
             }
             break;
         case HCCL_AMD_OP_REDUCE:
-            if (algo == HCCL_AMD_ALGO_RING || algo == HCCL_AMD_ALGO_RHD) algo = HCCL_AMD_ALGO_MESH_TWOSHOT;
+            if (algo == HCCL_AMD_ALGO_RING || algo == HCCL_AMD_ALGO_RHD || algo == HCCL_AMD_ALGO_NHR) {
+                algo = HCCL_AMD_ALGO_MESH_TWOSHOT;
+            }
             switch (algo) {
                 case HCCL_AMD_ALGO_MESH_ONESHOT: ReduceOneShot(p, b); break;
                 case HCCL_AMD_ALGO_MESH_TWOSHOT: ReduceTwoShot(p, b); break;

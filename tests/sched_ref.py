@@ -96,6 +96,63 @@ def allreduce_rhd(dtype, op, xs):
     return [out.copy() for _ in xs]
 
 
+def nhr_steps(n, me, gather):
+    """Step lists of ins_temp_all_reduce_nhr.cc:390-482 (GetReduceScatterStepInfoList / GetAllGatherStepInfoList),
+    restated from the reference text."""
+    n_steps = 0
+    t = n - 1
+    while t:
+        n_steps += 1
+        t >>= 1
+    steps = []
+    for step in range(n_steps):
+        if not gather:
+            dr = 1 << step
+            to, frm = (me + n - dr) % n, (me + dr) % n
+            n_sl = (n - 1 + (1 << step)) // (1 << (step + 1))
+            delta = 1 << (step + 1)
+            tx, rx = to, me
+        else:
+            dr = 1 << (n_steps - 1 - step)
+            to, frm = (me + dr) % n, (me + n - dr) % n
+            n_sl = (n - 1 + dr) // (1 << (n_steps - step))
+            delta = 1 << (n_steps - step)
+            tx, rx = me, (me - dr + n) % n
+        txs, rxs = [], []
+        for _ in range(n_sl):
+            txs.append(tx)
+            rxs.append(rx)
+            tx = (tx + n - delta % n) % n
+            rx = (rx + n - delta % n) % n
+        steps.append((to, frm, txs, rxs))
+    return steps
+
+
+def allreduce_nhr(dtype, op, xs):
+    """Simulates the NHR template with write-reduce semantics: the receiver's slice becomes
+    sender_partial (src) (op) receiver_partial (dst); slices are floor(count/n), tail on the last."""
+    n = len(xs)
+    count = xs[0].size
+    se = count // n
+    bounds = [(i * se, (i + 1) * se if i < n - 1 else count) for i in range(n)]
+    work = [x.copy() for x in xs]
+    for gather in (False, True):
+        per_rank = [nhr_steps(n, r, gather) for r in range(n)]
+        for step in range(len(per_rank[0])):
+            old = [w.copy() for w in work]
+            for r in range(n):
+                _, frm, _, rxs = per_rank[r][step]
+                for s_idx in rxs:
+                    b, e = bounds[s_idx]
+                    if e <= b:
+                        continue
+                    if gather:
+                        work[r][b:e] = old[frm][b:e]
+                    else:
+                        work[r][b:e] = apply(dtype, op, old[frm][b:e], old[r][b:e])
+    return work
+
+
 def reduce_scatter_o1(dtype, op, xs, rc):
     n = len(xs)
     blk = lambda r, q: xs[r][q * rc:(q + 1) * rc]  # noqa: E731
@@ -129,14 +186,14 @@ def reduce_twoshot(dtype, op, xs, root):
     return out
 
 
-ALGO_ONESHOT, ALGO_TWOSHOT, ALGO_RING, ALGO_RHD = 1, 2, 3, 4
+ALGO_ONESHOT, ALGO_TWOSHOT, ALGO_RING, ALGO_RHD, ALGO_NHR = 1, 2, 3, 4, 5
 
 
 def expected(op_type, algo, dtype, op, xs, count, root=0):
     """Per-rank expected outputs (Reduce: only the root's entry is meaningful; others are None)."""
     if op_type == 0:
         return {ALGO_ONESHOT: allreduce_o1, ALGO_TWOSHOT: allreduce_o2, ALGO_RING: allreduce_ring,
-                ALGO_RHD: allreduce_rhd}[algo](dtype, op, xs)
+                ALGO_RHD: allreduce_rhd, ALGO_NHR: allreduce_nhr}[algo](dtype, op, xs)
     if op_type == 1:
         return {ALGO_ONESHOT: reduce_scatter_o1, ALGO_RING: reduce_scatter_ring}[algo](dtype, op, xs, count)
     if op_type == 2:

@@ -98,7 +98,7 @@ def oracle_replay(op_type, algo, n, count, dtype, op, xs, root, piece_bytes):
     return [b[1] for b in bufs]
 
 
-CASES = [(AR, 1), (AR, 2), (AR, 3), (AR, 4), (RS, 1), (RS, 3), (RED, 1), (RED, 2)]
+CASES = [(AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5), (RS, 1), (RS, 3), (RED, 1), (RED, 2)]
 
 
 @pytest.mark.parametrize("count", [1, 1000, 262147])
@@ -142,7 +142,7 @@ def test_dtypes_ops(worlds, op_type, algo, dtype, op):
         assert O.equal_bits(dtype, outs[r], want[r]), r
 
 
-@pytest.mark.parametrize("algo", [1, 2, 3, 4])
+@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5])
 def test_allreduce_inplace(worlds, algo):
     n, count = 4, 300007
     comms = worlds(n)

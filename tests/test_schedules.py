@@ -50,7 +50,7 @@ def run(op_type, algo, n, count, dtype, op, root=0, piece_bytes=0, inplace=False
 
 
 CASES = [
-    (AR, 1), (AR, 2), (AR, 3), (AR, 4),
+    (AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5),
     (RS, 1), (RS, 3),
     (RED, 1), (RED, 2),
 ]
@@ -84,7 +84,23 @@ def test_schedule_dtypes_ops(op_type, algo, dtype, op):
         assert O.equal_bits(dtype, outs[r], want[r]), (op_type, used, r)
 
 
-@pytest.mark.parametrize("algo", [1, 2, 3, 4])
+def test_nhr_matches_survey_closed_form_o5():
+    """SURVEY.md Appendix A, O5 for n = 8: slice r = ((x_r+x_{r+1})+(x_{r+2}+x_{r+3}))+((x_{r+4}+x_{r+5})+(x_{r+6}
+    +x_{r+7})), every merge receiver partial (dst) (op) sender partial (src)."""
+    n, count = 8, 8 * 1001
+    used, xs, outs = run(AR, 5, n, count, O.FP32, O.SUM, piece_bytes=1024, seed=21)
+    assert used == R.ALGO_NHR
+    se = count // n
+    for r in range(n):
+        sl = slice(r * se, (r + 1) * se)
+        x = lambda k: xs[(r + k) % n][sl]  # noqa: E731
+        pair = lambda a, b: R.apply(O.FP32, O.SUM, b, a)  # noqa: E731  (a = dst, b = src)
+        want = pair(pair(pair(x(0), x(1)), pair(x(2), x(3))), pair(pair(x(4), x(5)), pair(x(6), x(7))))
+        for q in range(n):
+            assert O.equal_bits(O.FP32, outs[q][sl], want), (r, q)
+
+
+@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5])
 def test_allreduce_inplace(algo):
     n, count = 4, 50000
     used, xs, outs = run(AR, algo, n, count, O.FP32, O.SUM, piece_bytes=8192, inplace=True, seed=3)
