@@ -251,6 +251,62 @@ def rccl_allreduce_reference(send, recv, world, args):
         return {"error": f"{type(e).__name__}: {e}"}
 
 
+def _timed(fn, iters: int, warmup: int = 2) -> float:
+    """Per-iteration seconds of fn() on the current stream, max over ranks (barrier before and after)."""
+    import torch.distributed as dist
+
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    dist.barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = torch.tensor([e0.elapsed_time(e1) / 1e3 / iters], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0])
+
+
+def bench_c4(comm, send, recv, world) -> dict:
+    """C4: ZeRO-style gradient bucket, bf16, 2 GiB per rank: HcclReduceScatter (SUM) then HcclAllGather."""
+    nbytes = 2 << 30
+    x = send.view(torch.bfloat16)[: nbytes // 2]
+    full = recv.view(torch.bfloat16)[: nbytes // 2]
+    shard = torch.empty(x.numel() // world, dtype=torch.bfloat16, device=x.device)
+    s = torch.cuda.current_stream()
+    t_rs = _timed(lambda: comm.reduce_scatter(x, shard, H.HcclReduceOp.SUM, s), 5)
+    t_ag = _timed(lambda: comm.all_gather(shard, full, s), 5)
+    f = (world - 1) / world
+    return {"workload": "C4: ReduceScatter + AllGather bf16 SUM, 2 GiB per rank",
+            "rs_ms": round(t_rs * 1e3, 3), "ag_ms": round(t_ag * 1e3, 3),
+            "rs_busbw_GBps": round(nbytes / t_rs / 1e9 * f, 2), "ag_busbw_GBps": round(nbytes / t_ag / 1e9 * f, 2),
+            "rs_ag_busbw_GBps": round(2 * nbytes / (t_rs + t_ag) / 1e9 * f, 2)}
+
+
+def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
+    """C5: AllReduce fp16 SUM with the RHD schedule, 1 KiB .. 4 GiB: latency at small sizes, busbw at large."""
+    comm.set_algo(H.Algo.RHD)
+    s = torch.cuda.current_stream()
+    rows = []
+    nbytes = 1 << 10
+    try:
+        while nbytes <= max_bytes:
+            a = send.view(torch.float16)[: nbytes // 2]
+            b = recv.view(torch.float16)[: nbytes // 2]
+            iters = 20 if nbytes <= (64 << 20) else 3
+            t = _timed(lambda: comm.all_reduce(a, b, H.HcclReduceOp.SUM, s), iters)
+            rows.append({"bytes": nbytes, "us": round(t * 1e6, 1),
+                         "busbw_GBps": round(nbytes / t / 1e9 * 2 * (world - 1) / world, 2)})
+            nbytes *= 2
+    finally:
+        comm.set_algo(H.Algo.AUTO)
+    return {"workload": "C5: AllReduce fp16 SUM, RHD schedule, size sweep", "algo": "RHD", "points": rows}
+
+
 def bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     import torch.distributed as dist
 
@@ -290,6 +346,14 @@ def bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     busbw = algbw * 2 * (world - 1) / world
     value = world * C3_BYTES * args.steps / elapsed / GIB
     algo = comm.last_algo
+    extra = {}
+    if not args.no_extra_configs:
+        for name, fn in (("c4", lambda: bench_c4(comm, send, recv, world)),
+                         ("c5", lambda: bench_c5(comm, send, recv, world))):
+            try:
+                extra[name] = fn()
+            except Exception as e:  # noqa: BLE001  (a secondary config never hides the headline line)
+                extra[name] = {"error": f"{type(e).__name__}: {e}"}
     comm.destroy()
     rccl_ref = None
     if not args.no_rccl_ref:
@@ -317,6 +381,7 @@ def bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
         "busbw_GBps": round(busbw, 2),
         "algbw_GBps": round(algbw, 2),
         "rccl_allreduce_reference": rccl_ref,
+        "other_configs": extra,
         "roofline": {
             "bound": "xgmi",
             "achieved": round(busbw, 2),
@@ -331,6 +396,9 @@ def bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
 
 
 def main():
+    import faulthandler
+
+    faulthandler.dump_traceback_later(900, exit=False)  # diagnostics only: stacks to stderr if a run stalls
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
@@ -338,6 +406,7 @@ def main():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
     p.add_argument("--no-rccl-ref", action="store_true", help="N>1: skip timing RCCL's own all_reduce beside ours")
+    p.add_argument("--no-extra-configs", action="store_true", help="N>1: skip the C4 (RS+AG) and C5 (RHD sweep) lines")
     p.add_argument("--cpu-budget", type=float, default=12.0)
     p.add_argument("--algo", default="", help="force an AllReduce schedule (mesh_oneshot/mesh_twoshot/ring/rhd)")
     args = p.parse_args()

@@ -154,6 +154,10 @@ class Comm:
         check("HcclReduce", lib.HcclReduce(_ptr(send), _ptr(recv), send.numel(), hccl_dtype(send), int(op), root,
                                            self.handle, _stream(stream)))
 
+    def all_gather(self, send: torch.Tensor, recv: torch.Tensor, stream=None) -> None:
+        check("HcclAllGather", lib.HcclAllGather(_ptr(send), _ptr(recv), send.numel(), hccl_dtype(send),
+                                                 self.handle, _stream(stream)))
+
     def destroy(self) -> None:
         if self.handle:
             check("HcclCommDestroy", lib.HcclCommDestroy(self.handle))

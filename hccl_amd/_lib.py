@@ -84,6 +84,7 @@ class OpType(enum.IntEnum):
     ALLREDUCE = 0
     REDUCE_SCATTER = 1
     REDUCE = 2
+    ALLGATHER = 3
 
 
 class IrKind(enum.IntEnum):
@@ -128,6 +129,7 @@ SIGNATURES = {
     "HcclAllReduce": (_res, [_vp, _vp, _u64, _i32, _i32, _vp, _vp]),
     "HcclReduceScatter": (_res, [_vp, _vp, _u64, _i32, _i32, _vp, _vp]),
     "HcclReduce": (_res, [_vp, _vp, _u64, _i32, _i32, _u32, _vp, _vp]),
+    "HcclAllGather": (_res, [_vp, _vp, _u64, _i32, _vp, _vp]),
     "HcclGetRootInfo": (_res, [ctypes.POINTER(HcclRootInfo)]),
     "HcclCommInitRootInfo": (_res, [_u32, ctypes.POINTER(HcclRootInfo), _u32, ctypes.POINTER(_vp)]),
     "HcclCommDestroy": (_res, [_vp]),

@@ -137,6 +137,22 @@ HcclResult HcclReduce(void* sendBuf, void* recvBuf, uint64_t count, HcclDataType
                          static_cast<hipStream_t>(stream));
 }
 
+HcclResult HcclAllGather(void* sendBuf, void* recvBuf, uint64_t sendCount, HcclDataType dataType, HcclComm comm,
+                         aclrtStream stream)
+{
+    // all_gather_op.cc:22-50, AllGatherInitAndCheck :97-122
+    if (sendCount == 0) return HCCL_SUCCESS;
+    if (stream == nullptr || comm == nullptr || sendBuf == nullptr || recvBuf == nullptr) return HCCL_E_PTR;
+    Comm* c = AsComm(comm);
+    if (c == nullptr) return HCCL_E_PARA;
+    HCCL_CHK(CheckCount(sendCount));
+    // CheckDataType(dataType, needReduce = false): every valid type but INT128
+    if (DataTypeSize(dataType) == 0 || dataType == HCCL_DATA_TYPE_INT128) return HCCL_E_NOT_SUPPORT;
+    if (c->rank >= c->nRanks) return HCCL_E_PARA;
+    return RunCollective(*c, HCCL_AMD_OP_ALLGATHER, sendBuf, recvBuf, sendCount, dataType, HCCL_REDUCE_SUM, 0,
+                         static_cast<hipStream_t>(stream));
+}
+
 // ------------------------------------------------------------------------------------------------ communicators
 
 static const char kRootMagic[8] = {'H', 'C', 'C', 'L', 'A', 'M', 'D', '1'};

@@ -554,6 +554,48 @@ void ReduceTwoShot(const ScheduleParams& p, Builder& b)
     }
 }
 
+// ------------------------------------------------------------------------------------------- AllGather
+
+// Mesh: own block copied locally, every piece of the input sent to every peer in one group
+// (the all-gather half of ins_temp_all_reduce_mesh_1D_two_shot.cc:340-432 as an operator).
+void AllGatherMesh(const ScheduleParams& p, Builder& b)
+{
+    const uint32_t n = p.nRanks, me = p.rank;
+    const uint64_t sc = p.count;
+    const uint64_t pe = PieceElems(p, sc, 0);
+    const uint64_t np = std::max<uint64_t>(1, CeilDiv(sc, pe));
+    b.Copy(Out(uint64_t(me) * sc), In(0), sc);
+    for (uint64_t t = 0; t < np; ++t) {
+        Span s = Piece({0, sc}, pe, t);
+        for (uint32_t q : PeerOrder(n, me)) {
+            b.Send(q, In(s.begin), s.len);
+            b.Recv(q, Out(uint64_t(q) * sc + s.begin), s.len);
+        }
+        b.EndGroup();
+    }
+}
+
+// Ring: step s forwards block me-s to me+1 and receives block me-s-1 from me-1.
+void AllGatherRing(const ScheduleParams& p, Builder& b)
+{
+    const uint32_t n = p.nRanks, me = p.rank;
+    const uint64_t sc = p.count;
+    const uint64_t pe = PieceElems(p, sc, 0);
+    const uint64_t np = std::max<uint64_t>(1, CeilDiv(sc, pe));
+    const uint32_t next = (me + 1) % n, prev = (me + n - 1) % n;
+    b.Copy(Out(uint64_t(me) * sc), In(0), sc);
+    for (uint32_t s = 0; s + 1 < n; ++s) {
+        const uint32_t cs = (me + n - s) % n;
+        const uint32_t cr = (me + 2 * n - s - 1) % n;
+        for (uint64_t t = 0; t < np; ++t) {
+            Span piece = Piece({0, sc}, pe, t);
+            b.Send(next, s == 0 ? In(piece.begin) : Out(uint64_t(cs) * sc + piece.begin), piece.len);
+            b.Recv(prev, Out(uint64_t(cr) * sc + piece.begin), piece.len);
+            b.EndGroup();
+        }
+    }
+}
+
 bool IsPow2(uint32_t n) { return n != 0 && (n & (n - 1)) == 0; }
 
 }  // namespace
@@ -566,6 +608,7 @@ int32_t SelectAlgo(int32_t opType, uint32_t nRanks, uint64_t bytes)
         case HCCL_AMD_OP_REDUCE_SCATTER: return HCCL_AMD_ALGO_MESH_ONESHOT;
         case HCCL_AMD_OP_REDUCE:
             return bytes < kOneShotMaxBytes ? HCCL_AMD_ALGO_MESH_ONESHOT : HCCL_AMD_ALGO_MESH_TWOSHOT;
+        case HCCL_AMD_OP_ALLGATHER: return HCCL_AMD_ALGO_MESH_ONESHOT;
         default: return HCCL_AMD_ALGO_AUTO;
     }
 }
@@ -618,6 +661,14 @@ int BuildSchedule(const ScheduleParams& p, Schedule* out)
                 case HCCL_AMD_ALGO_MESH_ONESHOT: ReduceOneShot(p, b); break;
                 case HCCL_AMD_ALGO_MESH_TWOSHOT: ReduceTwoShot(p, b); break;
                 default: return HCCL_E_PARA;
+            }
+            break;
+        case HCCL_AMD_OP_ALLGATHER:
+            if (algo != HCCL_AMD_ALGO_RING) algo = HCCL_AMD_ALGO_MESH_ONESHOT;
+            if (algo == HCCL_AMD_ALGO_RING) {
+                AllGatherRing(p, b);
+            } else {
+                AllGatherMesh(p, b);
             }
             break;
         default: return HCCL_E_PARA;

@@ -40,6 +40,11 @@ extern HcclResult HcclReduceScatter(void* sendBuf, void* recvBuf, uint64_t recvC
 extern HcclResult HcclReduce(void* sendBuf, void* recvBuf, uint64_t count, HcclDataType dataType, HcclReduceOp op,
                              uint32_t root, HcclComm comm, aclrtStream stream);
 
+/* AllGather: recvBuf holds rankSize blocks of sendCount, block r = rank r's sendBuf (replaces
+ * /root/reference/include/hccl.h:120-121; the gather half of AllReduce and of config C4's RS + AG). */
+extern HcclResult HcclAllGather(void* sendBuf, void* recvBuf, uint64_t sendCount, HcclDataType dataType,
+                                HcclComm comm, aclrtStream stream);
+
 /* Communicator management (hcomm surface used by the reference's callers). */
 extern HcclResult HcclGetRootInfo(HcclRootInfo* rootInfo);
 extern HcclResult HcclCommInitRootInfo(uint32_t nRanks, const HcclRootInfo* rootInfo, uint32_t rank,

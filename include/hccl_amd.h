@@ -88,7 +88,8 @@ typedef struct {
 typedef enum {
     HCCL_AMD_OP_ALLREDUCE = 0,
     HCCL_AMD_OP_REDUCE_SCATTER = 1,
-    HCCL_AMD_OP_REDUCE = 2
+    HCCL_AMD_OP_REDUCE = 2,
+    HCCL_AMD_OP_ALLGATHER = 3 /* the second half of AllReduce as an operator (count = sendCount) */
 } HcclAmdOpType;
 
 typedef enum {

@@ -196,6 +196,9 @@ def expected(op_type, algo, dtype, op, xs, count, root=0):
                 ALGO_RHD: allreduce_rhd, ALGO_NHR: allreduce_nhr}[algo](dtype, op, xs)
     if op_type == 1:
         return {ALGO_ONESHOT: reduce_scatter_o1, ALGO_RING: reduce_scatter_ring}[algo](dtype, op, xs, count)
+    if op_type == 3:
+        full = np.concatenate([x[:count] for x in xs])
+        return [full.copy() for _ in xs]
     if op_type == 2:
         r = {ALGO_ONESHOT: reduce_oneshot, ALGO_TWOSHOT: reduce_twoshot}[algo](dtype, op, xs, root)
         return [r if q == root else None for q in range(len(xs))]

@@ -21,7 +21,7 @@ from tests._util import to_device, to_host
 
 pytestmark = pytest.mark.gpu
 
-AR, RS, RED = 0, 1, 2
+AR, RS, RED, AG = 0, 1, 2, 3
 
 
 @pytest.fixture(scope="module")
@@ -60,7 +60,7 @@ def run_ranks(n, fn):
 def collective(comms, op_type, algo, dtype, op, xs, count, root=0, piece_bytes=0, inplace=False):
     n = len(comms)
     sends = [to_device(dtype, x) for x in xs]
-    zeros = np.zeros(count, O.NP_STORAGE[dtype])
+    zeros = np.zeros(count * n if op_type == AG else count, O.NP_STORAGE[dtype])
     recvs = [s if inplace else to_device(dtype, zeros) for s in sends]
     streams = [torch.cuda.Stream() for _ in range(n)]
     for c in comms:
@@ -73,13 +73,15 @@ def collective(comms, op_type, algo, dtype, op, xs, count, root=0, piece_bytes=0
             comms[r].all_reduce(sends[r], recvs[r], op, streams[r])
         elif op_type == RS:
             comms[r].reduce_scatter(sends[r], recvs[r], op, streams[r])
+        elif op_type == AG:
+            comms[r].all_gather(sends[r], recvs[r], streams[r])
         else:
             comms[r].reduce(sends[r], recvs[r], root, op, streams[r])
 
     run_ranks(n, body)
     torch.cuda.synchronize()
     used = comms[0].last_algo
-    outs = [to_host(dtype, r)[:count] for r in recvs]
+    outs = [to_host(dtype, r)[:count * n if op_type == AG else count] for r in recvs]
     for c in comms:
         c.set_algo(0)
         c.set_piece_bytes(0)
@@ -93,12 +95,13 @@ def oracle_replay(op_type, algo, n, count, dtype, op, xs, root, piece_bytes):
         progs.append((arr, nops))
         scratch = max(scratch, se)
     st = O.NP_STORAGE[dtype]
-    bufs = [[x.copy(), np.zeros(count, st), np.zeros(max(scratch, 1), st)] for x in xs]
+    out_count = count * n if op_type == AG else count
+    bufs = [[x.copy(), np.zeros(out_count, st), np.zeros(max(scratch, 1), st)] for x in xs]
     assert O.replay(n, dtype, op, progs, bufs) == 0
     return [b[1] for b in bufs]
 
 
-CASES = [(AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5), (RS, 1), (RS, 3), (RED, 1), (RED, 2)]
+CASES = [(AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5), (RS, 1), (RS, 3), (RED, 1), (RED, 2), (AG, 1), (AG, 3)]
 
 
 @pytest.mark.parametrize("count", [1, 1000, 262147])

@@ -15,7 +15,7 @@ import hccl_amd as H
 from oracle import oracle as O
 from tests import sched_ref as R
 
-AR, RS, RED = 0, 1, 2
+AR, RS, RED, AG = 0, 1, 2, 3
 
 
 def programs(op_type, algo, n, count, dtype, root=0, piece_bytes=0):
@@ -39,7 +39,7 @@ def run(op_type, algo, n, count, dtype, op, root=0, piece_bytes=0, inplace=False
     outs = []
     for r in range(n):
         inp = xs[r].copy()
-        out = inp if inplace else np.zeros(count, st)
+        out = inp if inplace else np.zeros(count * n if op_type == AG else count, st)
         outs.append(out)
         bufs.append([inp, out, np.zeros(max(scratch, 1), st)])
     ret = O.replay(n, dtype, op, progs, bufs)
@@ -53,6 +53,7 @@ CASES = [
     (AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5),
     (RS, 1), (RS, 3),
     (RED, 1), (RED, 2),
+    (AG, 1), (AG, 3),
 ]
 
 
@@ -127,7 +128,7 @@ def test_schedule_scratch_is_bounded():
     """The staging a schedule addresses never exceeds the communicator's CCL buffer (256 MiB default)."""
     for op_type, algo in CASES:
         for n in (2, 8):
-            count = (4 << 30) // 4 // (n if op_type == RS else 1)
+            count = (4 << 30) // 4 // (n if op_type in (RS, AG) else 1)
             _, _, scratch = programs(op_type, algo, n, count, O.FP32)
             assert scratch * 4 <= 256 << 20, (op_type, algo, n, scratch)
 
