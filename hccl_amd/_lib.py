@@ -78,6 +78,7 @@ class Algo(enum.IntEnum):
     RING = 3
     RHD = 4
     NHR = 5
+    ORDER_PRESERVED = 6
 
 
 class OpType(enum.IntEnum):

@@ -6,6 +6,8 @@
 //   HcclReduce         reduce_op.cc:23-54, ReduceInitAndCheck, CheckReduceInputPara :106-127
 //   CheckCount / CheckDataType / CheckReduceOp / SingleRankProc   op_common.cc:2902-3098
 // then build this rank's schedule (schedule.cc) and run it (executor.cc).
+#include <strings.h>
+
 #include <cstring>
 
 #include "comm.h"
@@ -41,6 +43,18 @@ HcclResult CheckReduceOp(HcclDataType dt, HcclReduceOp op)
     return HCCL_SUCCESS;
 }
 
+// HCCL_DETERMINISTIC=strict (alg_env_config.cc:1036-1076) with fp16/fp32/bf16/fp64, SUM/PROD and more than two
+// ranks selects the order-preserved tree (IsNeedStrictModeForOrderPreserved, order_preserved_common.h:63-73).
+bool NeedStrictOrder(int32_t opType, HcclDataType dt, HcclReduceOp op, uint32_t nRanks)
+{
+    const char* e = std::getenv("HCCL_DETERMINISTIC");
+    if (e == nullptr || strcasecmp(e, "strict") != 0) return false;
+    if (opType != HCCL_AMD_OP_ALLREDUCE && opType != HCCL_AMD_OP_REDUCE_SCATTER) return false;
+    const bool fp = dt == HCCL_DATA_TYPE_FP16 || dt == HCCL_DATA_TYPE_FP32 || dt == HCCL_DATA_TYPE_BFP16 ||
+                    dt == HCCL_DATA_TYPE_FP64;
+    return fp && (op == HCCL_REDUCE_SUM || op == HCCL_REDUCE_PROD) && nRanks > 2;
+}
+
 HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, uint64_t count, HcclDataType dt,
                          HcclReduceOp op, uint32_t root, hipStream_t stream)
 {
@@ -58,6 +72,9 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     ScheduleParams p;
     p.opType = opType;
     p.algo = c.algoOverride;
+    if (p.algo == HCCL_AMD_ALGO_AUTO && NeedStrictOrder(opType, dt, op, c.nRanks)) {
+        p.algo = HCCL_AMD_ALGO_ORDER_PRESERVED;
+    }
     p.nRanks = c.nRanks;
     p.rank = c.rank;
     p.count = count;
@@ -231,7 +248,7 @@ HcclResult HcclAmdCommSetAlgo(HcclComm comm, int32_t algo)
 {
     Comm* c = AsComm(comm);
     if (c == nullptr) return HCCL_E_PTR;
-    if (algo < HCCL_AMD_ALGO_AUTO || algo > HCCL_AMD_ALGO_NHR) return HCCL_E_PARA;
+    if (algo < HCCL_AMD_ALGO_AUTO || algo > HCCL_AMD_ALGO_ORDER_PRESERVED) return HCCL_E_PARA;
     c->algoOverride = algo;
     return HCCL_SUCCESS;
 }

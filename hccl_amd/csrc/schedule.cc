@@ -423,6 +423,93 @@ void AllReduceNhr(const ScheduleParams& p, Builder& b)
     }
 }
 
+// ------------------------------------------------------------------------------------------- STRICT tree (O4)
+
+// Order-preserved tree fold (ins_temp_reduce_scatter_order_preserved_group.cc:305-399, RunLocalReduce): blocks are
+// indexed by source rank; while more than one remains, M = largest power of two below the count and block i >= M is
+// folded into block i % M as dst = src (op) dst. n = 8: ((x0+x4)+(x2+x6))+((x1+x5)+(x3+x7)). Rank-independent.
+// `blocks` must be writable (staging); the last fold writes `out`.
+void EmitTree(Builder& b, const std::vector<Ref>& blocks, Ref out, uint64_t count)
+{
+    uint32_t remaining = static_cast<uint32_t>(blocks.size());
+    if (remaining == 1) {
+        b.Copy(out, blocks[0], count);
+        return;
+    }
+    while (remaining > 1) {
+        uint32_t m = 1;
+        while (m * 2 < remaining) m *= 2;
+        for (uint32_t src = m; src < remaining; ++src) {
+            const uint32_t dst = src % m;
+            b.Reduce(m == 1 ? out : blocks[dst], {blocks[dst], blocks[src]}, count);
+        }
+        remaining = m;
+    }
+}
+
+// ReduceScatter in STRICT order: mesh exchange of blocks into per-source staging slots (own block copied in, as
+// PreLocalCopy does, :215-232), then the tree fold into recvBuf.
+void ReduceScatterTree(const ScheduleParams& p, Builder& b)
+{
+    const uint32_t n = p.nRanks, me = p.rank;
+    const uint64_t rc = p.count;
+    const uint64_t kSlots = 2;
+    const uint64_t pe = PieceElems(p, rc, kSlots * n);
+    const uint64_t np = std::max<uint64_t>(1, CeilDiv(rc, pe));
+    auto slot = [&](uint64_t t, uint32_t q) { return Scr(((t % kSlots) * n + q) * pe); };
+    for (uint64_t t = 0; t < np; ++t) {
+        Span s = Piece({0, rc}, pe, t);
+        for (uint32_t q : PeerOrder(n, me)) {
+            b.Send(q, In(uint64_t(q) * rc + s.begin), s.len);
+            b.Recv(q, slot(t, q), s.len);
+        }
+        b.EndGroup();
+        b.Copy(slot(t, me), In(uint64_t(me) * rc + s.begin), s.len);
+        std::vector<Ref> blocks;
+        for (uint32_t q = 0; q < n; ++q) blocks.push_back(slot(t, q));
+        EmitTree(b, blocks, Out(s.begin), s.len);
+    }
+}
+
+// AllReduce in STRICT order: the two-shot structure with the tree fold in place of the O2 chain.
+void AllReduceTree(const ScheduleParams& p, Builder& b)
+{
+    const uint32_t n = p.nRanks, me = p.rank;
+    const uint64_t alignElems = std::max<uint64_t>(1, kAlignBytes / p.elemSize);
+    const uint64_t kSlots = 2;
+    const Span mine = Chunk(p.count, n, me, alignElems);
+    const uint64_t maxChunk = Chunk(p.count, n, 0, alignElems).len;
+    const uint64_t pe = PieceElems(p, maxChunk, kSlots * n);
+    const uint64_t np = std::max<uint64_t>(1, CeilDiv(maxChunk, pe));
+    auto slot = [&](uint64_t t, uint32_t q) { return Scr(((t % kSlots) * n + q) * pe); };
+    for (uint64_t t = 0; t < np + 2; ++t) {
+        if (t < np) {
+            Span rs = Piece(mine, pe, t);
+            for (uint32_t q : PeerOrder(n, me)) {
+                Span out = Piece(Chunk(p.count, n, q, alignElems), pe, t);
+                b.Send(q, In(out.begin), out.len);
+                b.Recv(q, slot(t, q), rs.len);
+            }
+        }
+        if (t >= 2) {
+            Span mineP = Piece(mine, pe, t - 2);
+            for (uint32_t q : PeerOrder(n, me)) {
+                Span theirs = Piece(Chunk(p.count, n, q, alignElems), pe, t - 2);
+                b.Send(q, Out(mineP.begin), mineP.len);
+                b.Recv(q, Out(theirs.begin), theirs.len);
+            }
+        }
+        b.EndGroup();
+        if (t < np) {
+            Span rs = Piece(mine, pe, t);
+            b.Copy(slot(t, me), In(rs.begin), rs.len);
+            std::vector<Ref> blocks;
+            for (uint32_t q = 0; q < n; ++q) blocks.push_back(slot(t, q));
+            EmitTree(b, blocks, Out(rs.begin), rs.len);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------- ReduceScatter
 
 // Mesh (O1): every rank sends block q to rank q; rank me folds its own block first, then peers ascending
@@ -640,6 +727,7 @@ int BuildSchedule(const ScheduleParams& p, Schedule* out)
                 case HCCL_AMD_ALGO_RING: AllReduceRing(p, b); break;
                 case HCCL_AMD_ALGO_RHD: AllReduceRhd(p, b); break;
                 case HCCL_AMD_ALGO_NHR: AllReduceNhr(p, b); break;
+                case HCCL_AMD_ALGO_ORDER_PRESERVED: AllReduceTree(p, b); break;
                 default: return HCCL_E_PARA;
             }
             break;
@@ -650,11 +738,13 @@ int BuildSchedule(const ScheduleParams& p, Schedule* out)
             switch (algo) {
                 case HCCL_AMD_ALGO_MESH_ONESHOT: ReduceScatterMesh(p, b); break;
                 case HCCL_AMD_ALGO_RING: ReduceScatterRing(p, b); break;
+                case HCCL_AMD_ALGO_ORDER_PRESERVED: ReduceScatterTree(p, b); break;
                 default: return HCCL_E_PARA;
             }
             break;
         case HCCL_AMD_OP_REDUCE:
-            if (algo == HCCL_AMD_ALGO_RING || algo == HCCL_AMD_ALGO_RHD || algo == HCCL_AMD_ALGO_NHR) {
+            if (algo == HCCL_AMD_ALGO_RING || algo == HCCL_AMD_ALGO_RHD || algo == HCCL_AMD_ALGO_NHR ||
+                algo == HCCL_AMD_ALGO_ORDER_PRESERVED) {
                 algo = HCCL_AMD_ALGO_MESH_TWOSHOT;
             }
             switch (algo) {

@@ -98,7 +98,8 @@ typedef enum {
     HCCL_AMD_ALGO_MESH_TWOSHOT = 2, /* AllReduce: order O2 (ascending from rank 0); RS/Reduce: O1 */
     HCCL_AMD_ALGO_RING = 3,         /* ring reduce-scatter (+ ring all-gather) */
     HCCL_AMD_ALGO_RHD = 4,          /* recursive halving / doubling (power-of-two rank counts) */
-    HCCL_AMD_ALGO_NHR = 5           /* AllReduce: the reference's NHR template, order O5 (any rank count) */
+    HCCL_AMD_ALGO_NHR = 5,          /* AllReduce: the reference's NHR template, order O5 (any rank count) */
+    HCCL_AMD_ALGO_ORDER_PRESERVED = 6 /* AllReduce / ReduceScatter: HCCL_DETERMINISTIC=STRICT tree, order O4 */
 } HcclAmdAlgo;
 
 /* Build rank `rank`'s schedule. If ops == NULL only *numOps is written. scratchElems receives the number of

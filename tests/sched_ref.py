@@ -186,16 +186,47 @@ def reduce_twoshot(dtype, op, xs, root):
     return out
 
 
-ALGO_ONESHOT, ALGO_TWOSHOT, ALGO_RING, ALGO_RHD, ALGO_NHR = 1, 2, 3, 4, 5
+def tree_fold(dtype, op, blocks):
+    """O4 (ins_temp_reduce_scatter_order_preserved_group.cc:305-399): while more than one block remains, M = the
+    largest power of two below the count, block i >= M folds into block i % M as dst = src (op) dst."""
+    blocks = [np.ascontiguousarray(b).copy() for b in blocks]
+    remaining = len(blocks)
+    while remaining > 1:
+        m = 1
+        while m * 2 < remaining:
+            m *= 2
+        for src in range(m, remaining):
+            blocks[src % m] = apply(dtype, op, blocks[src], blocks[src % m])
+        remaining = m
+    return blocks[0]
+
+
+def allreduce_tree(dtype, op, xs):
+    n = len(xs)
+    es = xs[0].itemsize
+    out = np.empty_like(xs[0])
+    for b, e in chunk_bounds(xs[0].size, n, es):
+        if e > b:
+            out[b:e] = tree_fold(dtype, op, [x[b:e] for x in xs])
+    return [out.copy() for _ in xs]
+
+
+def reduce_scatter_tree(dtype, op, xs, rc):
+    n = len(xs)
+    return [tree_fold(dtype, op, [x[me * rc:(me + 1) * rc] for x in xs]) for me in range(n)]
+
+
+ALGO_ONESHOT, ALGO_TWOSHOT, ALGO_RING, ALGO_RHD, ALGO_NHR, ALGO_TREE = 1, 2, 3, 4, 5, 6
 
 
 def expected(op_type, algo, dtype, op, xs, count, root=0):
     """Per-rank expected outputs (Reduce: only the root's entry is meaningful; others are None)."""
     if op_type == 0:
         return {ALGO_ONESHOT: allreduce_o1, ALGO_TWOSHOT: allreduce_o2, ALGO_RING: allreduce_ring,
-                ALGO_RHD: allreduce_rhd, ALGO_NHR: allreduce_nhr}[algo](dtype, op, xs)
+                ALGO_RHD: allreduce_rhd, ALGO_NHR: allreduce_nhr, ALGO_TREE: allreduce_tree}[algo](dtype, op, xs)
     if op_type == 1:
-        return {ALGO_ONESHOT: reduce_scatter_o1, ALGO_RING: reduce_scatter_ring}[algo](dtype, op, xs, count)
+        return {ALGO_ONESHOT: reduce_scatter_o1, ALGO_RING: reduce_scatter_ring,
+                ALGO_TREE: reduce_scatter_tree}[algo](dtype, op, xs, count)
     if op_type == 3:
         full = np.concatenate([x[:count] for x in xs])
         return [full.copy() for _ in xs]

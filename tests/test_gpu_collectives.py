@@ -101,7 +101,25 @@ def oracle_replay(op_type, algo, n, count, dtype, op, xs, root, piece_bytes):
     return [b[1] for b in bufs]
 
 
-CASES = [(AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5), (RS, 1), (RS, 3), (RED, 1), (RED, 2), (AG, 1), (AG, 3)]
+CASES = [(AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5), (AR, 6), (RS, 1), (RS, 3), (RS, 6), (RED, 1), (RED, 2),
+         (AG, 1), (AG, 3)]
+
+
+def test_hccl_deterministic_strict_selects_tree(worlds, monkeypatch):
+    """HCCL_DETERMINISTIC=strict + fp32 SUM + more than 2 ranks selects the order-preserved tree (O4) for
+    AllReduce and ReduceScatter (order_preserved_common.h:63-73); int32 or 2 ranks keep the default."""
+    monkeypatch.setenv("HCCL_DETERMINISTIC", "strict")
+    n, count = 4, 70001
+    comms = worlds(n)
+    xs = [O.random_operands(O.FP32, count, seed=600 + r, edge=False) for r in range(n)]
+    used, outs = collective(comms, AR, 0, O.FP32, O.SUM, xs, count)
+    assert used == R.ALGO_TREE
+    want = R.expected(AR, used, O.FP32, O.SUM, xs, count)
+    for r in range(n):
+        assert O.equal_bits(O.FP32, outs[r], want[r]), r
+    xi = [O.random_operands(O.INT32, count, seed=700 + r, edge=False) for r in range(n)]
+    used, _ = collective(comms, AR, 0, O.INT32, O.SUM, xi, count)
+    assert used != R.ALGO_TREE
 
 
 @pytest.mark.parametrize("count", [1, 1000, 262147])
@@ -145,7 +163,7 @@ def test_dtypes_ops(worlds, op_type, algo, dtype, op):
         assert O.equal_bits(dtype, outs[r], want[r]), r
 
 
-@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5, 6])
 def test_allreduce_inplace(worlds, algo):
     n, count = 4, 300007
     comms = worlds(n)

@@ -50,8 +50,8 @@ def run(op_type, algo, n, count, dtype, op, root=0, piece_bytes=0, inplace=False
 
 
 CASES = [
-    (AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5),
-    (RS, 1), (RS, 3),
+    (AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5), (AR, 6),
+    (RS, 1), (RS, 3), (RS, 6),
     (RED, 1), (RED, 2),
     (AG, 1), (AG, 3),
 ]
@@ -101,7 +101,19 @@ def test_nhr_matches_survey_closed_form_o5():
             assert O.equal_bits(O.FP32, outs[q][sl], want), (r, q)
 
 
-@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5])
+def test_order_preserved_tree_matches_o4():
+    """SURVEY.md Appendix A, O4 for n = 8: ((x0+x4)+(x2+x6))+((x1+x5)+(x3+x7)), the same bits on every rank."""
+    n, rc = 8, 3001
+    used, xs, outs = run(RS, 6, n, rc, O.FP32, O.SUM, piece_bytes=2048, seed=41)
+    assert used == R.ALGO_TREE
+    for me in range(n):
+        x = [xs[q][me * rc:(me + 1) * rc] for q in range(n)]
+        pair = lambda a, b: R.apply(O.FP32, O.SUM, b, a)  # noqa: E731  (a = dst, b = src)
+        want = pair(pair(pair(x[0], x[4]), pair(x[2], x[6])), pair(pair(x[1], x[5]), pair(x[3], x[7])))
+        assert O.equal_bits(O.FP32, outs[me], want), me
+
+
+@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5, 6])
 def test_allreduce_inplace(algo):
     n, count = 4, 50000
     used, xs, outs = run(AR, algo, n, count, O.FP32, O.SUM, piece_bytes=8192, inplace=True, seed=3)
@@ -145,6 +157,35 @@ def test_sends_and_recvs_pair_up():
                 sends = [o.count for o in progs[a][0][:progs[a][1]] if o.kind == 2 and o.peer == b]
                 recvs = [o.count for o in progs[b][0][:progs[b][1]] if o.kind == 3 and o.peer == a]
                 assert sends == recvs, (op_type, algo, a, b)
+
+
+@pytest.mark.parametrize("inplace", [False, True])
+def test_groups_are_race_free(inplace):
+    """The reference ST's memory-conflict check (test/st/algorithm/utils/src/hccl_verifier/mem_conflict_check/)
+    applied to the IR: the SEND/RECV records of one group run concurrently inside one RCCL group, so no two of
+    them may touch overlapping bytes when either writes. (Ordering between groups and the reduce stream is derived
+    by the executor from the same byte ranges, so it cannot race.) In-place aliases INPUT onto OUTPUT."""
+    for op_type, algo in CASES:
+        if inplace and op_type != AR:
+            continue
+        for n in (2, 3, 5, 8):
+            count = 10007
+            progs, _, _ = programs(op_type, algo, n, count, O.FP32, root=n - 1, piece_bytes=4096)
+            for arr, nops in progs:
+                groups = {}
+                for o in arr[:nops]:
+                    if o.kind in (2, 3):
+                        buf = o.srcBuf[0] if o.kind == 2 else o.dstBuf
+                        off = o.srcOff[0] if o.kind == 2 else o.dstOff
+                        if inplace and buf == 0:
+                            buf = 1
+                        groups.setdefault(o.group, []).append((buf, off, off + o.count, o.kind == 3))
+                for g, acc in groups.items():
+                    for i in range(len(acc)):
+                        for j in range(i + 1, len(acc)):
+                            a, b = acc[i], acc[j]
+                            if a[0] == b[0] and (a[3] or b[3]) and a[1] < b[2] and b[1] < a[2]:
+                                raise AssertionError((op_type, algo, n, g, a, b))
 
 
 def test_c1_sim_two_rank_1mib_allreduce():
