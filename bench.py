@@ -307,6 +307,21 @@ def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
     return {"workload": "C5: AllReduce fp16 SUM, RHD schedule, size sweep", "algo": "RHD", "points": rows}
 
 
+def bench_c3_algos(comm, send, recv, world) -> dict:
+    """C3 shape (fp32 SUM, 4 GiB per rank) under every AllReduce schedule, 3 timed iterations each."""
+    s = torch.cuda.current_stream()
+    out = {}
+    try:
+        for algo in (H.Algo.MESH_TWOSHOT, H.Algo.RING, H.Algo.RHD, H.Algo.NHR, H.Algo.MESH_ONESHOT):
+            comm.set_algo(algo)
+            t = _timed(lambda: comm.all_reduce(send, recv, H.HcclReduceOp.SUM, s), 3, warmup=1)
+            out[algo.name] = {"ms": round(t * 1e3, 3),
+                              "busbw_GBps": round(C3_BYTES / t / 1e9 * 2 * (world - 1) / world, 2)}
+    finally:
+        comm.set_algo(H.Algo.AUTO)
+    return out
+
+
 def bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     import torch.distributed as dist
 
@@ -348,7 +363,8 @@ def bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     algo = comm.last_algo
     extra = {}
     if not args.no_extra_configs:
-        for name, fn in (("c4", lambda: bench_c4(comm, send, recv, world)),
+        for name, fn in (("c3_schedules", lambda: bench_c3_algos(comm, send, recv, world)),
+                         ("c4", lambda: bench_c4(comm, send, recv, world)),
                          ("c5", lambda: bench_c5(comm, send, recv, world))):
             try:
                 extra[name] = fn()

@@ -30,6 +30,17 @@ uint64_t ScratchBytesDefault()
     return mb << 20;
 }
 
+uint64_t SingleStreamBytes()
+{
+    const char* e = std::getenv("HCCL_AMD_SINGLE_STREAM_BYTES");  // read per call: tests switch it
+    if (e != nullptr && e[0] != '\0') {
+        char* end = nullptr;
+        unsigned long long x = std::strtoull(e, &end, 10);
+        if (end != e) return static_cast<uint64_t>(x);
+    }
+    return static_cast<uint64_t>(1) << 20;
+}
+
 HcclResult Comm::Init(int dev)
 {
     device = dev;

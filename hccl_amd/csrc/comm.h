@@ -71,8 +71,12 @@ Comm* AsComm(HcclComm c);
 uint64_t ScratchBytesDefault();
 
 // Runs one rank's schedule. bufs = {sendBuf, recvBuf, scratch}. Stream-ordered after `user`; `user` waits for the
-// whole schedule before anything enqueued later on it runs.
+// whole schedule before anything enqueued later on it runs. singleStream puts every unit on `user` in program order.
 HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const bufs[3], HcclDataType dt,
-                   HcclReduceOp op, hipStream_t user);
+                   HcclReduceOp op, hipStream_t user, bool singleStream = false);
+
+// Collectives whose per-rank payload is at most this many bytes run single-stream (HCCL_AMD_SINGLE_STREAM_BYTES,
+// default 1 MiB).
+uint64_t SingleStreamBytes();
 
 }  // namespace hccl_amd

@@ -42,9 +42,53 @@ bool Conflicts(const std::vector<Range>& a, const std::vector<Range>& b)
 
 }  // namespace
 
-HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const bufs[3], HcclDataType dt,
-                   HcclReduceOp op, hipStream_t user)
+// Small collectives have one pipeline piece, so the two-stream split cannot overlap anything: every unit goes on
+// the caller's stream in program order and no event is recorded or waited on (the latency floor of C5).
+static HcclResult ExecuteSingleStream(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const bufs[3],
+                                      HcclDataType dt, HcclReduceOp op, hipStream_t user)
 {
+    const uint64_t es = DataTypeSize(dt);
+    auto addr = [&](int32_t buf, uint64_t off) -> uintptr_t {
+        return reinterpret_cast<uintptr_t>(bufs[buf]) + off * es;
+    };
+    std::vector<P2pOp> p2p;
+    size_t i = 0;
+    while (i < ops.size()) {
+        const HcclAmdIrOp& o = ops[i];
+        if (o.kind == HCCL_AMD_IR_SEND || o.kind == HCCL_AMD_IR_RECV) {
+            p2p.clear();
+            const int32_t g = o.group;
+            while (i < ops.size() && (ops[i].kind == HCCL_AMD_IR_SEND || ops[i].kind == HCCL_AMD_IR_RECV) &&
+                   ops[i].group == g) {
+                const HcclAmdIrOp& q = ops[i];
+                const bool send = q.kind == HCCL_AMD_IR_SEND;
+                uintptr_t a = send ? addr(q.srcBuf[0], q.srcOff[0]) : addr(q.dstBuf, q.dstOff);
+                p2p.push_back({send, static_cast<uint32_t>(q.peer), reinterpret_cast<void*>(a), q.count * es});
+                ++i;
+            }
+            HCCL_CHK(c.transport->Group(p2p, user));
+            continue;
+        }
+        void* dst = reinterpret_cast<void*>(addr(o.dstBuf, o.dstOff));
+        if (o.kind == HCCL_AMD_IR_COPY) {
+            const void* src = reinterpret_cast<const void*>(addr(o.srcBuf[0], o.srcOff[0]));
+            if (src != dst) HIP_CHK(hipMemcpyAsync(dst, src, o.count * es, hipMemcpyDeviceToDevice, user));
+        } else if (o.kind == HCCL_AMD_IR_REDUCE) {
+            const void* srcs[HCCL_AMD_IR_MAX_SRC];
+            for (int j = 0; j < o.nsrc; ++j) srcs[j] = reinterpret_cast<const void*>(addr(o.srcBuf[j], o.srcOff[j]));
+            HCCL_CHK(LaunchReduceN(dst, srcs, static_cast<uint32_t>(o.nsrc), o.count, dt, op, user));
+        } else {
+            return HCCL_E_INTERNAL;
+        }
+        ++i;
+    }
+    return HCCL_SUCCESS;
+}
+
+HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const bufs[3], HcclDataType dt,
+                   HcclReduceOp op, hipStream_t user, bool singleStream)
+{
+    if (singleStream) return ExecuteSingleStream(c, ops, bufs, dt, op, user);
     const uint64_t es = DataTypeSize(dt);
     hipStream_t streams[2] = {c.commStream, c.reduceStream};
     c.nextEvent = 0;

@@ -94,7 +94,8 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     HCCL_AMD_LOG("rank %u op %d algo %d count %llu ops %zu", c.rank, opType, s.algo, (unsigned long long)count,
                  s.ops.size());
     void* bufs[3] = {sendBuf, recvBuf, c.scratch};
-    return Execute(c, s.ops, bufs, dt, op, stream);
+    const uint64_t payload = count * es * (opType == HCCL_AMD_OP_REDUCE_SCATTER ? c.nRanks : 1);
+    return Execute(c, s.ops, bufs, dt, op, stream, payload <= SingleStreamBytes());
 }
 
 }  // namespace

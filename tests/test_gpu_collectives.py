@@ -122,10 +122,15 @@ def test_hccl_deterministic_strict_selects_tree(worlds, monkeypatch):
     assert used != R.ALGO_TREE
 
 
+@pytest.mark.parametrize("streams", ["auto", "two"])
 @pytest.mark.parametrize("count", [1, 1000, 262147])
 @pytest.mark.parametrize("n", [2, 3, 4, 8])
 @pytest.mark.parametrize("op_type,algo", CASES)
-def test_fp32_sum(worlds, op_type, algo, n, count):
+def test_fp32_sum(worlds, op_type, algo, n, count, streams, monkeypatch):
+    """streams: 'auto' runs payloads <= 1 MiB on the caller's stream only; 'two' forces the link/reduce stream
+    split with event-derived dependencies at every size."""
+    if streams == "two":
+        monkeypatch.setenv("HCCL_AMD_SINGLE_STREAM_BYTES", "0")
     comms = worlds(n)
     root = n - 1
     in_count = count * n if op_type == RS else count
