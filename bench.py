@@ -309,14 +309,33 @@ def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
 
 def bench_c3_algos(comm, send, recv, world) -> dict:
     """C3 shape (fp32 SUM, 4 GiB per rank) under every AllReduce schedule, 3 timed iterations each."""
+    import ctypes
+
+    import torch.distributed as dist
+
     s = torch.cuda.current_stream()
     out = {}
+    ref = None
     try:
-        for algo in (H.Algo.MESH_TWOSHOT, H.Algo.RING, H.Algo.RHD, H.Algo.NHR, H.Algo.MESH_ONESHOT):
+        for algo in (H.Algo.MESH_TWOSHOT, H.Algo.IPC_TWOSHOT, H.Algo.RING, H.Algo.RHD, H.Algo.NHR,
+                     H.Algo.MESH_ONESHOT):
             comm.set_algo(algo)
             t = _timed(lambda: comm.all_reduce(send, recv, H.HcclReduceOp.SUM, s), 3, warmup=1)
-            out[algo.name] = {"ms": round(t * 1e3, 3),
-                              "busbw_GBps": round(C3_BYTES / t / 1e9 * 2 * (world - 1) / world, 2)}
+            row = {"ms": round(t * 1e3, 3), "busbw_GBps": round(C3_BYTES / t / 1e9 * 2 * (world - 1) / world, 2)}
+            if algo in (H.Algo.MESH_TWOSHOT, H.Algo.IPC_TWOSHOT):
+                # both compute order O2: the outputs must be identical bit for bit
+                digest = recv.view(torch.int32)[:: 1 << 12].clone()
+                if ref is None:
+                    ref = digest
+                else:
+                    same = torch.tensor([1 if torch.equal(ref, digest) else 0], dtype=torch.int32)
+                    dist.all_reduce(same, op=dist.ReduceOp.MIN)
+                    row["matches_rccl_two_shot"] = bool(same.item())
+                st = ctypes.c_uint32(0)
+                H.lib.HcclAmdCommIpcStatus(comm.handle, ctypes.byref(st))
+                if algo == H.Algo.IPC_TWOSHOT:
+                    row["barrier_timeouts"] = int(st.value)
+            out[algo.name] = row
     finally:
         comm.set_algo(H.Algo.AUTO)
     return out

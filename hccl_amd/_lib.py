@@ -79,6 +79,7 @@ class Algo(enum.IntEnum):
     RHD = 4
     NHR = 5
     ORDER_PRESERVED = 6
+    IPC_TWOSHOT = 7
 
 
 class OpType(enum.IntEnum):
@@ -152,6 +153,7 @@ SIGNATURES = {
     "HcclAmdCommSetAlgo": (_res, [_vp, _i32]),
     "HcclAmdCommSetPieceBytes": (_res, [_vp, _u64]),
     "HcclAmdCommLastAlgo": (_i32, [_vp]),
+    "HcclAmdCommIpcStatus": (_res, [_vp, ctypes.POINTER(_u32)]),
 }
 
 

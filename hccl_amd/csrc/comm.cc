@@ -76,6 +76,7 @@ Comm::~Comm()
     }
     if (commStream != nullptr) (void)hipStreamSynchronize(commStream);
     if (reduceStream != nullptr) (void)hipStreamSynchronize(reduceStream);
+    IpcRelease(*this);
     transport.reset();
     for (hipEvent_t e : events) (void)hipEventDestroy(e);
     if (scratch != nullptr) (void)hipFree(scratch);
@@ -122,6 +123,26 @@ public:
         return FromNccl(ncclGroupEnd(), "ncclGroupEnd");
     }
     const char* Name() const override { return "rccl"; }
+    HcclResult AllGatherHost(const void* mine, size_t bytes, void* all) override
+    {
+        int n = 0;
+        HcclResult r = FromNccl(ncclCommCount(comm, &n), "ncclCommCount");
+        if (r != HCCL_SUCCESS) return r;
+        void* d = nullptr;
+        hipStream_t s = nullptr;
+        HIP_CHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        HIP_CHK(hipMalloc(&d, bytes * (size_t(n) + 1)));
+        char* dAll = static_cast<char*>(d) + bytes;
+        HIP_CHK(hipMemcpyAsync(d, mine, bytes, hipMemcpyHostToDevice, s));
+        r = FromNccl(ncclAllGather(d, dAll, bytes, ncclUint8, comm, s), "ncclAllGather");
+        if (r == HCCL_SUCCESS) {
+            HIP_CHK(hipMemcpyAsync(all, dAll, bytes * size_t(n), hipMemcpyDeviceToHost, s));
+            HIP_CHK(hipStreamSynchronize(s));
+        }
+        (void)hipFree(d);
+        (void)hipStreamDestroy(s);
+        return r;
+    }
 };
 
 }  // namespace
@@ -166,11 +187,38 @@ public:
         bool consumed = false;
         bool failed = false;
     };
-    explicit LoopbackWorld(uint32_t n) : n_(n), boxes_(size_t(n) * n) {}
+    explicit LoopbackWorld(uint32_t n) : n_(n), boxes_(size_t(n) * n), slots_(n) {}
     uint32_t n_;
     std::mutex mu_;
     std::condition_variable cv_;
     std::vector<std::deque<std::shared_ptr<Entry>>> boxes_;
+
+    // host all-gather among the rank threads (generation-counted so that back-to-back exchanges cannot mix)
+    std::vector<std::vector<char>> slots_;
+    std::vector<char> result_;
+    uint32_t arrived_ = 0;
+    uint64_t generation_ = 0;
+
+    HcclResult Exchange(uint32_t rank, const void* mine, size_t bytes, void* all)
+    {
+        std::unique_lock<std::mutex> lk(mu_);
+        const uint64_t gen = generation_;
+        slots_[rank].assign(static_cast<const char*>(mine), static_cast<const char*>(mine) + bytes);
+        if (++arrived_ == n_) {
+            result_.clear();
+            for (auto& s : slots_) {
+                if (s.size() != bytes) return HCCL_E_INTERNAL;
+                result_.insert(result_.end(), s.begin(), s.end());
+            }
+            arrived_ = 0;
+            generation_++;
+            cv_.notify_all();
+        } else if (!cv_.wait_for(lk, std::chrono::seconds(600), [&] { return generation_ != gen; })) {
+            return HCCL_E_TIMEOUT;
+        }
+        std::memcpy(all, result_.data(), bytes * n_);
+        return HCCL_SUCCESS;
+    }
 };
 
 namespace {
@@ -181,6 +229,11 @@ class LoopbackTransport : public Transport {
 public:
     LoopbackTransport(std::shared_ptr<LoopbackWorld> w, uint32_t rank) : w_(std::move(w)), me_(rank) {}
     const char* Name() const override { return "loopback"; }
+    bool SharedDevice() const override { return true; }
+    HcclResult AllGatherHost(const void* mine, size_t bytes, void* all) override
+    {
+        return w_->Exchange(me_, mine, bytes, all);
+    }
 
     HcclResult Group(const std::vector<P2pOp>& ops, hipStream_t stream) override
     {

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "internal.h"
+#include "ipc.h"
 #include "schedule.h"
 
 namespace hccl_amd {
@@ -31,6 +32,10 @@ public:
     virtual ~Transport() = default;
     virtual HcclResult Group(const std::vector<P2pOp>& ops, hipStream_t stream) = 0;
     virtual const char* Name() const = 0;
+    // Blocking all-gather of `bytes` host bytes per rank into all[nRanks * bytes] (setup and rendezvous only).
+    virtual HcclResult AllGatherHost(const void* mine, size_t bytes, void* all) = 0;
+    // True when every rank lives in this process on this device (loopback world).
+    virtual bool SharedDevice() const { return false; }
 };
 
 std::unique_ptr<Transport> MakeRcclTransport(void* uniqueId, uint32_t nRanks, uint32_t rank, HcclResult* err);
@@ -59,10 +64,18 @@ struct Comm {
     std::vector<hipEvent_t> events;
     size_t nextEvent = 0;
 
+    IpcState ipc;  // one-sided AllReduce path, set up on first use (collectively)
+
     HcclResult Init(int dev);
     HcclResult NextEvent(hipEvent_t* e);
     ~Comm();
 };
+
+// One-sided AllReduce (HCCL_AMD_ALGO_IPC_TWOSHOT). Returns HCCL_E_NOT_SUPPORT when the buffers are not 16-B aligned
+// (the caller then runs the RCCL two-shot, which has the same order O2).
+HcclResult RunIpcAllReduce(Comm& c, const void* sendBuf, void* recvBuf, uint64_t count, HcclDataType dt,
+                           HcclReduceOp op, hipStream_t stream);
+void IpcRelease(Comm& c);
 
 Comm* AsComm(HcclComm c);
 

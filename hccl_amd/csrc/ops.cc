@@ -75,6 +75,16 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     if (p.algo == HCCL_AMD_ALGO_AUTO && NeedStrictOrder(opType, dt, op, c.nRanks)) {
         p.algo = HCCL_AMD_ALGO_ORDER_PRESERVED;
     }
+    if (p.algo == HCCL_AMD_ALGO_IPC_TWOSHOT) {
+        if (opType == HCCL_AMD_OP_ALLREDUCE) {
+            HcclResult r = RunIpcAllReduce(c, sendBuf, recvBuf, count, dt, op, stream);
+            if (r != HCCL_E_NOT_SUPPORT) {
+                c.lastAlgo = HCCL_AMD_ALGO_IPC_TWOSHOT;
+                return r;
+            }
+        }
+        p.algo = HCCL_AMD_ALGO_MESH_TWOSHOT;  // same order (O2) through the RCCL executor
+    }
     p.nRanks = c.nRanks;
     p.rank = c.rank;
     p.count = count;
@@ -249,7 +259,7 @@ HcclResult HcclAmdCommSetAlgo(HcclComm comm, int32_t algo)
 {
     Comm* c = AsComm(comm);
     if (c == nullptr) return HCCL_E_PTR;
-    if (algo < HCCL_AMD_ALGO_AUTO || algo > HCCL_AMD_ALGO_ORDER_PRESERVED) return HCCL_E_PARA;
+    if (algo < HCCL_AMD_ALGO_AUTO || algo > HCCL_AMD_ALGO_IPC_TWOSHOT) return HCCL_E_PARA;
     c->algoOverride = algo;
     return HCCL_SUCCESS;
 }

@@ -710,6 +710,9 @@ int BuildSchedule(const ScheduleParams& p, Schedule* out)
     int32_t algo = p.algo;
     uint64_t bytes = p.count * p.elemSize;
     if (algo == HCCL_AMD_ALGO_AUTO) algo = SelectAlgo(p.opType, p.nRanks, bytes);
+    // The one-sided IPC AllReduce runs as one kernel, not as IR; its IR twin (same order O2, same bits) is the
+    // two-shot, which is also what runs when the IPC path cannot (unaligned buffers).
+    if (algo == HCCL_AMD_ALGO_IPC_TWOSHOT) algo = HCCL_AMD_ALGO_MESH_TWOSHOT;
     if (p.nRanks == 1) {
         // SingleRankProc (op_common.cc:3042-3098): a copy when the buffers differ.
         b.Copy(Out(0), In(0), p.count);

@@ -99,7 +99,8 @@ typedef enum {
     HCCL_AMD_ALGO_RING = 3,         /* ring reduce-scatter (+ ring all-gather) */
     HCCL_AMD_ALGO_RHD = 4,          /* recursive halving / doubling (power-of-two rank counts) */
     HCCL_AMD_ALGO_NHR = 5,          /* AllReduce: the reference's NHR template, order O5 (any rank count) */
-    HCCL_AMD_ALGO_ORDER_PRESERVED = 6 /* AllReduce / ReduceScatter: HCCL_DETERMINISTIC=STRICT tree, order O4 */
+    HCCL_AMD_ALGO_ORDER_PRESERVED = 6, /* AllReduce / ReduceScatter: HCCL_DETERMINISTIC=STRICT tree, order O4 */
+    HCCL_AMD_ALGO_IPC_TWOSHOT = 7      /* AllReduce: one kernel over peer-mapped staging (AIV GM_IN model), O2 */
 } HcclAmdAlgo;
 
 /* Build rank `rank`'s schedule. If ops == NULL only *numOps is written. scratchElems receives the number of
@@ -123,6 +124,9 @@ extern HcclResult HcclAmdCommSetPieceBytes(HcclComm comm, uint64_t pieceBytes);
 
 /* Algorithm the last collective on comm executed (HcclAmdAlgo), or -1. */
 extern int32_t HcclAmdCommLastAlgo(HcclComm comm);
+
+/* Status word of the IPC path (synchronous read): bit 0 = a cross-rank barrier timed out (results invalid). */
+extern HcclResult HcclAmdCommIpcStatus(HcclComm comm, uint32_t* status);
 
 #ifdef __cplusplus
 }

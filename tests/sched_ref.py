@@ -216,14 +216,15 @@ def reduce_scatter_tree(dtype, op, xs, rc):
     return [tree_fold(dtype, op, [x[me * rc:(me + 1) * rc] for x in xs]) for me in range(n)]
 
 
-ALGO_ONESHOT, ALGO_TWOSHOT, ALGO_RING, ALGO_RHD, ALGO_NHR, ALGO_TREE = 1, 2, 3, 4, 5, 6
+ALGO_ONESHOT, ALGO_TWOSHOT, ALGO_RING, ALGO_RHD, ALGO_NHR, ALGO_TREE, ALGO_IPC = 1, 2, 3, 4, 5, 6, 7
 
 
 def expected(op_type, algo, dtype, op, xs, count, root=0):
     """Per-rank expected outputs (Reduce: only the root's entry is meaningful; others are None)."""
     if op_type == 0:
         return {ALGO_ONESHOT: allreduce_o1, ALGO_TWOSHOT: allreduce_o2, ALGO_RING: allreduce_ring,
-                ALGO_RHD: allreduce_rhd, ALGO_NHR: allreduce_nhr, ALGO_TREE: allreduce_tree}[algo](dtype, op, xs)
+                ALGO_RHD: allreduce_rhd, ALGO_NHR: allreduce_nhr, ALGO_TREE: allreduce_tree,
+                ALGO_IPC: allreduce_o2}[algo](dtype, op, xs)
     if op_type == 1:
         return {ALGO_ONESHOT: reduce_scatter_o1, ALGO_RING: reduce_scatter_ring,
                 ALGO_TREE: reduce_scatter_tree}[algo](dtype, op, xs, count)

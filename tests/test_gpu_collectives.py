@@ -101,8 +101,51 @@ def oracle_replay(op_type, algo, n, count, dtype, op, xs, root, piece_bytes):
     return [b[1] for b in bufs]
 
 
-CASES = [(AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5), (AR, 6), (RS, 1), (RS, 3), (RS, 6), (RED, 1), (RED, 2),
-         (AG, 1), (AG, 3)]
+CASES = [(AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5), (AR, 6), (AR, 7), (RS, 1), (RS, 3), (RS, 6), (RED, 1),
+         (RED, 2), (AG, 1), (AG, 3)]
+
+
+def ipc_status(comm):
+    import ctypes
+    v = ctypes.c_uint32(0)
+    H.check("HcclAmdCommIpcStatus", H.lib.HcclAmdCommIpcStatus(comm.handle, ctypes.byref(v)))
+    return v.value
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+@pytest.mark.parametrize("count", [5, 4096, 1000003, 36 * (1 << 20) + 11])
+def test_ipc_allreduce_o2_and_status(worlds, n, count):
+    """The one-sided IPC AllReduce (one kernel, every rank's blocks in one launch on this GPU): bit-exact with the
+    two-shot order O2, across several staging rounds (36 Mi fp32 > one 32 Mi-element round), barrier status clean."""
+    comms = worlds(n)
+    xs = [O.random_operands(O.FP32, count, seed=800 + r, edge=False) for r in range(n)]
+    used, outs = collective(comms, AR, 7, O.FP32, O.SUM, xs, count)
+    assert used == 7
+    assert ipc_status(comms[0]) == 0
+    want = R.expected(AR, R.ALGO_TWOSHOT, O.FP32, O.SUM, xs, count)
+    for r in range(n):
+        assert O.equal_bits(O.FP32, outs[r], want[r]), r
+
+
+def test_ipc_unaligned_falls_back_to_twoshot(worlds):
+    """Buffers not 16-B aligned run the RCCL-path two-shot (same order O2)."""
+    n, count = 4, 10001
+    comms = worlds(n)
+    xs = [O.random_operands(O.FP32, count + 1, seed=900 + r, edge=False) for r in range(n)]
+    sends = [to_device(O.FP32, x)[1:] for x in xs]
+    recvs = [torch.zeros(count + 1, device="cuda")[1:] for _ in range(n)]
+    streams = [torch.cuda.Stream() for _ in range(n)]
+    for c in comms:
+        c.set_algo(7)
+    torch.cuda.synchronize()
+    run_ranks(n, lambda r: comms[r].all_reduce(sends[r], recvs[r], O.SUM, streams[r]))
+    torch.cuda.synchronize()
+    assert comms[0].last_algo == R.ALGO_TWOSHOT
+    for c in comms:
+        c.set_algo(0)
+    want = R.expected(AR, R.ALGO_TWOSHOT, O.FP32, O.SUM, [x[1:].copy() for x in xs], count)
+    for r in range(n):
+        assert O.equal_bits(O.FP32, to_host(O.FP32, recvs[r]), want[r]), r
 
 
 def test_hccl_deterministic_strict_selects_tree(worlds, monkeypatch):
@@ -149,7 +192,7 @@ def test_fp32_sum(worlds, op_type, algo, n, count, streams, monkeypatch):
 @pytest.mark.parametrize("dtype", [O.INT8, O.INT16, O.INT32, O.INT64, O.UINT64, O.FP16, O.BFP16, O.FP64],
                          ids=lambda v: O.DTYPE_NAMES[v])
 @pytest.mark.parametrize("op", O.OPS, ids=lambda v: O.OP_NAMES[v])
-@pytest.mark.parametrize("op_type,algo", [(AR, 1), (AR, 2), (AR, 3), (RS, 1), (RED, 2)])
+@pytest.mark.parametrize("op_type,algo", [(AR, 1), (AR, 2), (AR, 3), (AR, 7), (RS, 1), (RED, 2)])
 def test_dtypes_ops(worlds, op_type, algo, dtype, op):
     n, count, root = 4, 40961, 2
     comms = worlds(n)
