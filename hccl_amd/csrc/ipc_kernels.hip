@@ -41,7 +41,11 @@ __device__ __forceinline__ void Barrier(const IpcArgs& a, uint32_t me, uint32_t 
         uint32_t* mine = a.flags[me] + blockIdx.x * a.n + t;
         uint32_t polls = 0;
         while (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
-            if (++polls > a.maxPolls) {
+            ++polls;
+            // a timeout anywhere is sticky: later barriers of this launch stop waiting at once
+            if (polls > a.maxPolls ||
+                ((polls & 1023u) == 0 &&
+                 (__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 1u) != 0)) {
                 __hip_atomic_fetch_or(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 break;
             }
