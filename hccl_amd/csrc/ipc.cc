@@ -123,6 +123,7 @@ HcclResult RunIpcAllReduce(Comm& c, const void* sendBuf, void* recvBuf, uint64_t
         a.me = static_cast<int32_t>(c.rank);
         a.in[c.rank] = sendBuf;
         a.out[c.rank] = recvBuf;
+        HIP_CHK(hipMemsetAsync(s.status, 0, sizeof(uint32_t), stream));  // the status describes the last call
         return LaunchIpcAllReduce(a, s.blocks, 0, dt, op, stream);
     }
 
@@ -147,6 +148,7 @@ HcclResult RunIpcAllReduce(Comm& c, const void* sendBuf, void* recvBuf, uint64_t
             a.out[r] = all[r].out;
             HIP_CHK(hipStreamWaitEvent(stream, all[r].ready, 0));
         }
+        HIP_CHK(hipMemsetAsync(s.status, 0, sizeof(uint32_t), stream));
         HCCL_CHK(LaunchIpcAllReduce(a, s.blocks, n, dt, op, stream));
         HCCL_CHK(c.NextEvent(&done));
         HIP_CHK(hipEventRecord(done, stream));
