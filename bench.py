@@ -309,8 +309,6 @@ def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
 
 def bench_c3_algos(comm, send, recv, world) -> dict:
     """C3 shape (fp32 SUM, 4 GiB per rank) under every AllReduce schedule, 3 timed iterations each."""
-    import ctypes
-
     import torch.distributed as dist
 
     s = torch.cuda.current_stream()
@@ -331,10 +329,11 @@ def bench_c3_algos(comm, send, recv, world) -> dict:
                     same = torch.tensor([1 if torch.equal(ref, digest) else 0], dtype=torch.int32)
                     dist.all_reduce(same, op=dist.ReduceOp.MIN)
                     row["matches_rccl_two_shot"] = bool(same.item())
-                st = ctypes.c_uint32(0)
-                H.lib.HcclAmdCommIpcStatus(comm.handle, ctypes.byref(st))
                 if algo == H.Algo.IPC_TWOSHOT:
-                    row["barrier_timeouts"] = int(st.value)
+                    st = comm.ipc_status()
+                    row["barrier_timeouts"] = st & 1
+                    row["longest_wait_polls_log2"] = (st >> 8) & 0xFF
+                    row["ran"] = H.Algo(comm.last_algo).name  # MESH_TWOSHOT if the IPC set-up fell back
             out[algo.name] = row
     finally:
         comm.set_algo(H.Algo.AUTO)

@@ -140,6 +140,12 @@ class Comm:
     def last_algo(self) -> int:
         return lib.HcclAmdCommLastAlgo(self.handle)
 
+    def ipc_status(self) -> int:
+        """Status word of the IPC path (bit 0: a cross-rank barrier timed out on the last IPC AllReduce)."""
+        v = ctypes.c_uint32(0)
+        check("HcclAmdCommIpcStatus", lib.HcclAmdCommIpcStatus(self.handle, ctypes.byref(v)))
+        return v.value
+
     def all_reduce(self, send: torch.Tensor, recv: torch.Tensor, op: int = HcclReduceOp.SUM, stream=None) -> None:
         check("HcclAllReduce", lib.HcclAllReduce(_ptr(send), _ptr(recv), send.numel(), hccl_dtype(send), int(op),
                                                  self.handle, _stream(stream)))
@@ -182,3 +188,31 @@ def loopback_world(n_ranks: int) -> List[Comm]:
     arr = (ctypes.c_void_p * n_ranks)()
     check("HcclAmdCommInitLoopback", lib.HcclAmdCommInitLoopback(n_ranks, arr))
     return [Comm(arr[i]) for i in range(n_ranks)]
+
+
+# HcclAmdHostAllGatherFn (include/hccl_amd.h)
+HOST_ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                     ctypes.c_void_p)
+
+
+def comm_init_host_exchange(n_ranks: int, rank: int, all_gather) -> Comm:
+    """IPC-only communicator bootstrapped by `all_gather(bytes) -> list of n_ranks bytes objects` (e.g. over a
+    torch.distributed gloo group). Its AllReduce is the one-sided IPC path."""
+
+    def _cb(_ctx, mine, nbytes, out):
+        try:
+            parts = all_gather(ctypes.string_at(mine, nbytes))
+            if len(parts) != n_ranks or any(len(b) != nbytes for b in parts):
+                return 1
+            ctypes.memmove(out, b"".join(parts), nbytes * n_ranks)
+            return 0
+        except Exception:  # noqa: BLE001  (an exception cannot cross the C boundary; the library reports failure)
+            return 1
+
+    fn = HOST_ALLGATHER_FN(_cb)
+    h = ctypes.c_void_p(0)
+    check("HcclAmdCommInitHostExchange",
+          lib.HcclAmdCommInitHostExchange(n_ranks, rank, ctypes.cast(fn, ctypes.c_void_p), None, ctypes.byref(h)))
+    c = Comm(h.value)
+    c._keepalive = fn  # the library calls it for the communicator's lifetime
+    return c

@@ -154,6 +154,7 @@ SIGNATURES = {
     "HcclAmdCommSetPieceBytes": (_res, [_vp, _u64]),
     "HcclAmdCommLastAlgo": (_i32, [_vp]),
     "HcclAmdCommIpcStatus": (_res, [_vp, ctypes.POINTER(_u32)]),
+    "HcclAmdCommInitHostExchange": (_res, [_u32, _u32, _vp, _vp, ctypes.POINTER(_vp)]),
 }
 
 

@@ -76,6 +76,7 @@ Comm::~Comm()
     }
     if (commStream != nullptr) (void)hipStreamSynchronize(commStream);
     if (reduceStream != nullptr) (void)hipStreamSynchronize(reduceStream);
+    IpcQuiesce(*this);
     IpcRelease(*this);
     transport.reset();
     for (hipEvent_t e : events) (void)hipEventDestroy(e);
@@ -318,6 +319,36 @@ std::shared_ptr<LoopbackWorld> MakeLoopbackWorld(uint32_t nRanks) { return std::
 std::unique_ptr<Transport> MakeLoopbackTransport(std::shared_ptr<LoopbackWorld> world, uint32_t rank)
 {
     return std::make_unique<LoopbackTransport>(std::move(world), rank);
+}
+
+namespace {
+
+// Bootstrap-only transport of HcclAmdCommInitHostExchange: the host exchange is the caller's all-gather; there is
+// no send/recv data path (the IPC AllReduce moves the data itself).
+class HostExchangeTransport : public Transport {
+public:
+    HostExchangeTransport(HcclAmdHostAllGatherFn fn, void* ctx) : fn_(fn), ctx_(ctx) {}
+    const char* Name() const override { return "host-exchange"; }
+    HcclResult Group(const std::vector<P2pOp>&, hipStream_t) override
+    {
+        HCCL_AMD_ERR("host-exchange communicator has no send/recv path (only the IPC AllReduce)");
+        return HCCL_E_NOT_SUPPORT;
+    }
+    HcclResult AllGatherHost(const void* mine, size_t bytes, void* all) override
+    {
+        return fn_(ctx_, mine, bytes, all) == 0 ? HCCL_SUCCESS : HCCL_E_INTERNAL;
+    }
+
+private:
+    HcclAmdHostAllGatherFn fn_;
+    void* ctx_;
+};
+
+}  // namespace
+
+std::unique_ptr<Transport> MakeHostExchangeTransport(HcclAmdHostAllGatherFn fn, void* ctx)
+{
+    return std::make_unique<HostExchangeTransport>(fn, ctx);
 }
 
 }  // namespace hccl_amd

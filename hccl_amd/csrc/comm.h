@@ -44,6 +44,7 @@ HcclResult RcclGetUniqueId(void* id128);
 class LoopbackWorld;
 std::unique_ptr<Transport> MakeLoopbackTransport(std::shared_ptr<LoopbackWorld> world, uint32_t rank);
 std::shared_ptr<LoopbackWorld> MakeLoopbackWorld(uint32_t nRanks);
+std::unique_ptr<Transport> MakeHostExchangeTransport(HcclAmdHostAllGatherFn fn, void* ctx);
 
 struct Comm {
     uint32_t magic = 0x48434C41;  // "HCLA"
@@ -71,10 +72,12 @@ struct Comm {
     ~Comm();
 };
 
-// One-sided AllReduce (HCCL_AMD_ALGO_IPC_TWOSHOT). Returns HCCL_E_NOT_SUPPORT when the buffers are not 16-B aligned
-// (the caller then runs the RCCL two-shot, which has the same order O2).
+// One-sided AllReduce (HCCL_AMD_ALGO_IPC_TWOSHOT), any buffer alignment. Returns HCCL_E_NOT_SUPPORT, on every rank
+// alike, when the peer mappings cannot be set up (the caller then runs the RCCL two-shot, which has the same order O2).
 HcclResult RunIpcAllReduce(Comm& c, const void* sendBuf, void* recvBuf, uint64_t count, HcclDataType dt,
                            HcclReduceOp op, hipStream_t stream);
+// Collective: every rank's IPC kernels have finished before any rank unmaps or frees (called by ~Comm).
+void IpcQuiesce(Comm& c);
 void IpcRelease(Comm& c);
 
 Comm* AsComm(HcclComm c);

@@ -7,6 +7,7 @@
 // In a loopback world the ranks share a device and the raw pointers are exchanged instead, and the whole world runs
 // as one launch (all ranks' blocks must be resident together, which separate per-rank launches on 4 hardware queues
 // would not guarantee).
+#include <cstdlib>
 #include <cstring>
 
 #include "comm.h"
@@ -29,18 +30,21 @@ HcclResult IpcSetup(Comm& c)
 {
     IpcState& s = c.ipc;
     if (s.ready) return HCCL_SUCCESS;
+    if (s.unavailable) return HCCL_E_NOT_SUPPORT;
     const uint32_t n = c.nRanks, me = c.rank;
     s.blocks = kIpcBlocks;
     s.stgInBytes = kIpcStagingBytes;
-    s.stgResBytes = kIpcStagingBytes / n + 4096;
+    s.stgResBytes = kIpcStagingBytes;  // results of a whole round, in round coordinates
     const size_t flagBytes = size_t(s.blocks) * kIpcMaxRanks * sizeof(uint32_t);
-    HIP_CHK(hipExtMallocWithFlags(&s.stg, s.stgInBytes + s.stgResBytes, hipDeviceMallocUncached));
-    HIP_CHK(hipExtMallocWithFlags(reinterpret_cast<void**>(&s.flags), flagBytes, hipDeviceMallocUncached));
-    HIP_CHK(hipMalloc(reinterpret_cast<void**>(&s.status), sizeof(uint32_t)));
-    HIP_CHK(hipMemset(s.flags, 0, flagBytes));
-    HIP_CHK(hipMemset(s.status, 0, sizeof(uint32_t)));
-    HIP_CHK(hipDeviceSynchronize());
+    bool ok = hipExtMallocWithFlags(&s.stg, s.stgInBytes + s.stgResBytes, hipDeviceMallocUncached) == hipSuccess &&
+              hipExtMallocWithFlags(reinterpret_cast<void**>(&s.flags), flagBytes, hipDeviceMallocUncached) ==
+                  hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&s.status), kIpcStatusBytes) == hipSuccess &&
+              hipMemset(s.flags, 0, flagBytes) == hipSuccess && hipMemset(s.status, 0, kIpcStatusBytes) == hipSuccess &&
+              hipDeviceSynchronize() == hipSuccess;
+    if (!ok) HCCL_AMD_ERR("rank %u: IPC staging allocation failed", me);
     if (c.transport->SharedDevice()) {
+        if (!ok) return HCCL_E_MEMORY;
         RawPtrs mine{s.stg, s.flags};
         std::vector<RawPtrs> all(n);
         HCCL_CHK(c.transport->AllGatherHost(&mine, sizeof mine, all.data()));
@@ -49,22 +53,42 @@ HcclResult IpcSetup(Comm& c)
             s.peerFlags[r] = all[r].flags;
         }
     } else {
+        // Every rank takes part in both exchanges whatever happens locally, and the outcome is agreed: either all
+        // ranks have every peer mapped or all release and report NOT_SUPPORT (the caller then runs the RCCL
+        // two-shot on every rank alike, never a mix of paths that would leave peers waiting).
         Exported mine{};
-        HIP_CHK(hipIpcGetMemHandle(&mine.stg, s.stg));
-        HIP_CHK(hipIpcGetMemHandle(&mine.flags, s.flags));
+        ok = ok && hipIpcGetMemHandle(&mine.stg, s.stg) == hipSuccess &&
+             hipIpcGetMemHandle(&mine.flags, s.flags) == hipSuccess;
         std::vector<Exported> all(n);
         HCCL_CHK(c.transport->AllGatherHost(&mine, sizeof mine, all.data()));
-        for (uint32_t r = 0; r < n; ++r) {
+        for (uint32_t r = 0; r < n && ok; ++r) {
             if (r == me) {
                 s.peerStg[r] = s.stg;
                 s.peerFlags[r] = s.flags;
                 continue;
             }
-            HIP_CHK(hipIpcOpenMemHandle(&s.peerStg[r], all[r].stg, hipIpcMemLazyEnablePeerAccess));
             void* f = nullptr;
-            HIP_CHK(hipIpcOpenMemHandle(&f, all[r].flags, hipIpcMemLazyEnablePeerAccess));
+            hipError_t e = hipIpcOpenMemHandle(&s.peerStg[r], all[r].stg, hipIpcMemLazyEnablePeerAccess);
+            if (e == hipSuccess) {
+                e = hipIpcOpenMemHandle(&f, all[r].flags, hipIpcMemLazyEnablePeerAccess);
+                if (e != hipSuccess) (void)hipIpcCloseMemHandle(s.peerStg[r]);
+            }
+            if (e != hipSuccess) {
+                HCCL_AMD_ERR("rank %u: hipIpcOpenMemHandle of rank %u failed: %s", me, r, hipGetErrorString(e));
+                ok = false;
+                break;
+            }
             s.peerFlags[r] = static_cast<uint32_t*>(f);
             s.opened[r] = true;
+        }
+        const uint8_t mineOk = ok ? 1 : 0;
+        std::vector<uint8_t> allOk(n);
+        HCCL_CHK(c.transport->AllGatherHost(&mineOk, 1, allOk.data()));
+        for (uint32_t r = 0; r < n; ++r) ok = ok && allOk[r] != 0;
+        if (!ok) {
+            IpcRelease(c);
+            s.unavailable = true;
+            return HCCL_E_NOT_SUPPORT;
         }
     }
     s.epoch = 0;
@@ -72,7 +96,40 @@ HcclResult IpcSetup(Comm& c)
     return HCCL_SUCCESS;
 }
 
+bool Aligned16(const void* p, const void* q)
+{
+    return ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(q)) & 15u) == 0;
+}
+
+// Wall-time bound of one barrier wait: HCCL_AMD_IPC_TIMEOUT_MS (default 60 s), in 100 MHz s_memrealtime ticks.
+uint64_t IpcTimeoutTicks()
+{
+    uint64_t ms = 60000;
+    const char* e = std::getenv("HCCL_AMD_IPC_TIMEOUT_MS");
+    if (e != nullptr && *e != '\0') {
+        const unsigned long long v = std::strtoull(e, nullptr, 0);
+        if (v >= 1 && v <= 3600000ull) ms = v;
+    }
+    return ms * 100000ull;
+}
+
 }  // namespace
+
+void IpcQuiesce(Comm& c)
+{
+    if (!c.ipc.ready) return;
+    // Peers store into this rank's staging and flags: unmapping or freeing them while any peer's kernel may still
+    // run would fault that peer. Wait for this device, then for every rank to get here (each has waited for its own).
+    (void)hipDeviceSynchronize();
+    if (!c.transport->SharedDevice()) {
+        uint8_t mine = 1;
+        std::vector<uint8_t> all(c.nRanks);
+        if (c.transport->AllGatherHost(&mine, 1, all.data()) != HCCL_SUCCESS) {
+            HCCL_AMD_ERR("rank %u: IPC teardown rendezvous failed; peer mappings are left in place", c.rank);
+            c.ipc = IpcState{};  // leak rather than free memory a peer may still write
+        }
+    }
+}
 
 void IpcRelease(Comm& c)
 {
@@ -93,9 +150,6 @@ void IpcRelease(Comm& c)
 HcclResult RunIpcAllReduce(Comm& c, const void* sendBuf, void* recvBuf, uint64_t count, HcclDataType dt,
                            HcclReduceOp op, hipStream_t stream)
 {
-    if ((reinterpret_cast<uintptr_t>(sendBuf) | reinterpret_cast<uintptr_t>(recvBuf)) & 15u) {
-        return HCCL_E_NOT_SUPPORT;
-    }
     const uint64_t es = DataTypeSize(dt);
     if (es == 0 || c.nRanks > kIpcMaxRanks) return HCCL_E_NOT_SUPPORT;
     HCCL_CHK(IpcSetup(c));
@@ -103,8 +157,6 @@ HcclResult RunIpcAllReduce(Comm& c, const void* sendBuf, void* recvBuf, uint64_t
     const uint32_t n = c.nRanks;
     const uint64_t unit = uint64_t(n) * (16 / es);
     const uint64_t roundElems = (s.stgInBytes / es) / unit * unit;
-    const uint64_t rounds = (count + roundElems - 1) / roundElems;
-
     IpcArgs a{};
     for (uint32_t r = 0; r < n; ++r) {
         a.stgIn[r] = s.peerStg[r];
@@ -112,22 +164,39 @@ HcclResult RunIpcAllReduce(Comm& c, const void* sendBuf, void* recvBuf, uint64_t
         a.flags[r] = s.peerFlags[r];
     }
     a.n = n;
-    a.count = count;
     a.roundElems = roundElems;
-    a.epochBase = s.epoch;
-    a.maxPolls = 1u << 22;  // ~ seconds of polling: a lost peer ends the kernel with status bit 0, never a hang
+    a.timeoutTicks = IpcTimeoutTicks();  // a lost peer ends the kernel with status bit 0, never a hang
     a.status = s.status;
-    s.epoch += static_cast<uint32_t>(3 * rounds);
+
+    // The per-block barrier is sound only while every round of a launch has the same geometry (block b touches the
+    // same slot and result addresses each round); a shorter last round moves every block's range, so it runs as a
+    // launch of its own (a kernel ends only after all its blocks passed their last barrier on every rank).
+    const uint64_t fullElems = count / roundElems * roundElems;
+    struct Span {
+        uint64_t off, count;
+    };
+    Span spans[2];
+    int nspans = 0;
+    if (fullElems != 0) spans[nspans++] = {0, fullElems};
+    if (count != fullElems) spans[nspans++] = {fullElems, count - fullElems};
+    auto at = [es](const void* p, uint64_t off) { return static_cast<const char*>(p) + off * es; };
 
     if (!c.transport->SharedDevice()) {
         a.me = static_cast<int32_t>(c.rank);
-        a.in[c.rank] = sendBuf;
-        a.out[c.rank] = recvBuf;
-        HIP_CHK(hipMemsetAsync(s.status, 0, sizeof(uint32_t), stream));  // the status describes the last call
-        return LaunchIpcAllReduce(a, s.blocks, 0, dt, op, stream);
+        a.aligned = Aligned16(sendBuf, recvBuf);
+        HIP_CHK(hipMemsetAsync(s.status + 1, 0, sizeof(uint32_t), stream));  // wait diagnostic of this call
+        for (int i = 0; i < nspans; ++i) {
+            a.in[c.rank] = at(sendBuf, spans[i].off);
+            a.out[c.rank] = const_cast<char*>(at(recvBuf, spans[i].off));
+            a.count = spans[i].count;
+            a.epochBase = s.epoch;
+            s.epoch += static_cast<uint32_t>(2 * ((spans[i].count + roundElems - 1) / roundElems));
+            HCCL_CHK(LaunchIpcAllReduce(a, s.blocks, 0, dt, op, stream));
+        }
+        return HCCL_SUCCESS;
     }
 
-    // loopback world: one launch for every rank, issued by rank 0 behind every rank's stream
+    // loopback world: one launch per span for every rank, issued by rank 0 behind every rank's stream
     struct Part {
         const void* in;
         void* out;
@@ -143,13 +212,22 @@ HcclResult RunIpcAllReduce(Comm& c, const void* sendBuf, void* recvBuf, uint64_t
     hipEvent_t done = nullptr;
     if (c.rank == 0) {
         a.me = -1;
+        a.aligned = true;
         for (uint32_t r = 0; r < n; ++r) {
-            a.in[r] = all[r].in;
-            a.out[r] = all[r].out;
+            a.aligned = a.aligned && Aligned16(all[r].in, all[r].out);
             HIP_CHK(hipStreamWaitEvent(stream, all[r].ready, 0));
         }
-        HIP_CHK(hipMemsetAsync(s.status, 0, sizeof(uint32_t), stream));
-        HCCL_CHK(LaunchIpcAllReduce(a, s.blocks, n, dt, op, stream));
+        HIP_CHK(hipMemsetAsync(s.status + 1, 0, sizeof(uint32_t), stream));
+        for (int i = 0; i < nspans; ++i) {
+            for (uint32_t r = 0; r < n; ++r) {
+                a.in[r] = at(all[r].in, spans[i].off);
+                a.out[r] = const_cast<char*>(at(all[r].out, spans[i].off));
+            }
+            a.count = spans[i].count;
+            a.epochBase = s.epoch;
+            s.epoch += static_cast<uint32_t>(2 * ((spans[i].count + roundElems - 1) / roundElems));
+            HCCL_CHK(LaunchIpcAllReduce(a, s.blocks, n, dt, op, stream));
+        }
         HCCL_CHK(c.NextEvent(&done));
         HIP_CHK(hipEventRecord(done, stream));
     }
@@ -170,6 +248,10 @@ extern "C" HcclResult HcclAmdCommIpcStatus(HcclComm comm, uint32_t* status)
     *status = 0;
     if (!c->ipc.ready) return HCCL_SUCCESS;
     HIP_CHK(hipSetDevice(c->device));
-    HIP_CHK(hipMemcpy(status, c->ipc.status, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    uint32_t w[2] = {0, 0};
+    HIP_CHK(hipMemcpy(w, c->ipc.status, sizeof w, hipMemcpyDeviceToHost));
+    uint32_t lg = 0;
+    while (lg < 32 && (uint64_t(1) << lg) <= w[1]) ++lg;  // bit length of the longest wait
+    *status = (w[0] & 0xFFu) | (lg << 8);
     return HCCL_SUCCESS;
 }

@@ -25,8 +25,9 @@ struct IpcArgs {
     uint64_t count;
     uint64_t roundElems;
     uint32_t epochBase;
-    uint32_t maxPolls;
-    uint32_t* status;  // bit 0: a barrier timed out
+    uint64_t timeoutTicks;  // per barrier wait, in s_memrealtime ticks (100 MHz)
+    uint32_t* status;  // [0] bit 0: a barrier timed out (sticky per communicator); [1]: longest wait, in polls
+    bool aligned;      // every in[] / out[] the launch touches is 16-B aligned (else element-wise accesses to them)
 };
 
 HcclResult LaunchIpcAllReduce(const IpcArgs& a, uint32_t blocks, uint32_t worldRanks, HcclDataType dt,
@@ -35,9 +36,10 @@ HcclResult LaunchIpcAllReduce(const IpcArgs& a, uint32_t blocks, uint32_t worldR
 // Per-communicator state of the IPC path.
 struct IpcState {
     bool ready = false;
+    bool unavailable = false;      // set-up failed on some rank: every later call reports NOT_SUPPORT
     void* stg = nullptr;           // own staging: [in area: stgInBytes][result area: stgResBytes], uncached
     uint32_t* flags = nullptr;     // own flags, uncached, zeroed
-    uint32_t* status = nullptr;    // device word
+    uint32_t* status = nullptr;    // device words: [0] bit 0 = barrier timeout, [1] = longest barrier wait (polls)
     void* peerStg[kIpcMaxRanks] = {};
     uint32_t* peerFlags[kIpcMaxRanks] = {};
     bool opened[kIpcMaxRanks] = {};
@@ -48,6 +50,7 @@ struct IpcState {
 };
 
 constexpr uint32_t kIpcBlocks = 128;
-constexpr uint64_t kIpcStagingBytes = 128ull << 20;  // input area per rank; the result area is 1/n of it
+constexpr size_t kIpcStatusBytes = 16;  // status words, reset as one 16-B block per call
+constexpr uint64_t kIpcStagingBytes = 128ull << 20;  // slot area per rank; the result area is as large
 
 }  // namespace hccl_amd

@@ -3,20 +3,31 @@
 // The reference's AIV engine runs AllReduce as ONE kernel whose blocks write into every peer's CCL buffer
 // (GM_IN[r]) and synchronise with per-block flags (aiv_all_reduce_mesh_1d_twoshot.h:20-217,
 // aiv_communication_base_v2.h:296-357). This is the MI355X form of that model, two-shot with the reference's
-// deterministic order O2 (acc = x_0, then x_1 .. x_{n-1}; ins_temp_all_reduce_mesh_1D_two_shot.cc:327-335):
-//   per round of `roundElems` elements (bounded staging):
-//     phase 0  every rank copies its input slice into its own staging (local HBM)
-//     barrier  block b tells block b of every rank "my staging is written", waits for theirs
-//     phase 1  rank c folds chunk c reading all n stagings (n-1 of them over xGMI), writes recvBuf and a result area
+// deterministic order O2 (acc = x_0, then x_1 .. x_{n-1}; ins_temp_all_reduce_mesh_1D_two_shot.cc:327-335).
+// PUSH only: every access to a peer's memory is a store; every load reads this rank's own uncached staging or its own
+// user buffers. (A load through an imported mapping may be served by this XCD's L2, which no in-kernel acquire
+// evicts, so a pull design re-reading a peer's staging in a later round can see stale lines.)
+//   per round of `roundElems` elements (bounded staging), chunk c of the round is owned by rank c:
+//     phase 0  rank r stores its values of chunk c into owner c's staging slot r (c != r; the owner reads its own
+//              slot straight from its input)
+//     barrier  block b tells block b of every rank "my stores are out", waits for theirs
+//     phase 1  owner c folds slots 0..n-1 in rank order (O2), writes recvBuf and stores the result into every
+//              peer's result area
 //     barrier
-//     phase 2  every rank copies the other chunks' results from their owners' result areas (xGMI reads)
-//     barrier  (the staging may be overwritten by the next round / call)
-// Block b of every rank always handles the same element ranges, so a block only waits for block b of its peers;
-// nothing in a GPU waits for another block of the same GPU. Staging and flags are uncached device memory (fine
-// grained), stores are drained and released at system scope before a flag store, flags are polled with system-scope
-// relaxed loads followed by an acquire. Every poll loop is bounded: on timeout the kernel sets status bit 0 and
-// finishes (wrong data, never a hang). World mode (me < 0) runs all n ranks of a loopback world as blockIdx.y of one
-// launch on one GPU, which is how the protocol is tested without a second GPU.
+//     phase 2  every rank copies the other chunks from its own result area
+// Two barriers per round suffice: a peer's next-round phase-0 stores into my staging come after it passed barrier 2
+// (so after my phase-1 reads), and its next phase-1 stores into my result area come after barrier 1 of the next
+// round (so after my phase-2 reads); the same holds across calls (kernels of a stream run in order).
+// Every round of one launch has the same geometry (the host launches a shorter last round separately), so block b
+// of every rank touches the same slot and result addresses in every round and only waits for block b of its peers;
+// nothing in a GPU waits for another block of the same GPU. Every storing wave drains (s_waitcnt vmcnt(0)) before the
+// workgroup barrier, one wave then releases at system scope (L2 write-back) and stores the flags with system-scope
+// release stores; flags are polled with system-scope relaxed loads and followed by an acquire. Every wait is bounded
+// in wall time (s_memrealtime, HCCL_AMD_IPC_TIMEOUT_MS): on timeout the kernel sets status bit 0 and finishes (wrong
+// data, never a hang); the bit is sticky for the communicator, so later launches return at once. World mode (me < 0) runs all
+// n ranks of a loopback world as blockIdx.y of one launch on one GPU, which is how the protocol is tested without a
+// second GPU; the rank-mode path (one launch per process, peers opened from IPC handles) is tested with n processes
+// sharing the GPU.
 #include <hip/hip_runtime.h>
 
 #include "internal.h"
@@ -30,8 +41,11 @@ namespace {
 constexpr int kIpcBlock = 256;
 constexpr int kIpcU = 4;
 
-__device__ __forceinline__ void Barrier(const IpcArgs& a, uint32_t me, uint32_t epoch)
+// Returns false when a barrier of this launch timed out (status bit 0): the caller then stops at once, so a rank
+// never stores into a peer it has lost track of.
+__device__ __forceinline__ bool Barrier(const IpcArgs& a, uint32_t me, uint32_t epoch)
 {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its stores have left the CU
     __syncthreads();
     const uint32_t t = threadIdx.x;
     if (t < a.n) {
@@ -40,50 +54,58 @@ __device__ __forceinline__ void Barrier(const IpcArgs& a, uint32_t me, uint32_t 
         __hip_atomic_store(remote, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         uint32_t* mine = a.flags[me] + blockIdx.x * a.n + t;
         uint32_t polls = 0;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz constant clock
         while (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
             ++polls;
-            // a timeout anywhere is sticky: later barriers of this launch stop waiting at once
-            if (polls > a.maxPolls ||
-                ((polls & 1023u) == 0 &&
-                 (__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 1u) != 0)) {
-                __hip_atomic_fetch_or(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                break;
+            if ((polls & 63u) == 0) {
+                // a timeout anywhere (this or another block of this rank) ends the wait at once
+                if ((__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 1u) != 0) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeoutTicks) {
+                    __hip_atomic_fetch_or(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
             }
             __builtin_amdgcn_s_sleep(2);
         }
+        if (polls != 0) __hip_atomic_fetch_max(a.status + 1, polls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate has completed before the barrier opens
     }
+    __shared__ uint32_t failed;
+    if (t == 0) failed = __hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 1u;
     __syncthreads();
+    return failed == 0;
+}
+
+// Chunk size of a round of `len` elements: ceil(len / n) rounded up to whole 16-B vectors.
+__device__ __forceinline__ uint64_t ChunkElems(uint64_t len, uint32_t n, uint64_t vecElems)
+{
+    uint64_t cs = (len + n - 1) / n;
+    return (cs + vecElems - 1) / vecElems * vecElems;
 }
 
 struct Range {
     uint64_t lo, hi;  // elements, relative to the round base
 };
 
-// Chunk c of a round of `len` elements, rounded to whole 16-B vectors; the block's share of it likewise.
-__device__ __forceinline__ Range BlockRange(uint64_t len, uint32_t n, uint32_t c, uint64_t vecElems)
+// Block blockIdx.x's share of chunk c, in whole 16-B vectors (the last chunk may end mid-vector).
+__device__ __forceinline__ Range BlockRange(uint64_t len, uint32_t c, uint64_t cs, uint64_t vecElems)
 {
-    uint64_t cs = (len + n - 1) / n;
-    cs = (cs + vecElems - 1) / vecElems * vecElems;
-    uint64_t clo = min(len, uint64_t(c) * cs), chi = min(len, clo + cs);
+    const uint64_t clo = min(len, uint64_t(c) * cs), chi = min(len, clo + cs);
     uint64_t bs = (chi - clo + gridDim.x - 1) / gridDim.x;
     bs = (bs + vecElems - 1) / vecElems * vecElems;
-    uint64_t lo = min(chi, clo + uint64_t(blockIdx.x) * bs);
+    const uint64_t lo = min(chi, clo + uint64_t(blockIdx.x) * bs);
     return {lo, min(chi, lo + bs)};
 }
 
-__device__ __forceinline__ uint64_t ChunkLo(uint64_t len, uint32_t n, uint32_t c, uint64_t vecElems)
-{
-    uint64_t cs = (len + n - 1) / n;
-    cs = (cs + vecElems - 1) / vecElems * vecElems;
-    return min(len, uint64_t(c) * cs);
-}
-
+// dst[e] = src[e] for e in r (both pointers pre-offset to round coordinates). vec = both pointers are 16-B aligned;
+// otherwise every element goes through the scalar loop.
 template <typename S>
-__device__ __forceinline__ void CopyRange(S* dst, const S* src, Range r)
+__device__ __forceinline__ void CopyRange(S* dst, const S* src, Range r, bool vec)
 {
     constexpr uint64_t V = 16 / sizeof(S);
-    const uint64_t vlo = r.lo / V, vhi = r.hi / V;  // r.lo is vector aligned; r.hi may not be (last chunk)
+    // r.lo is vector aligned unless the range is empty at the end of the round (lo = hi = len); r.hi may be anything
+    const uint64_t vlo = r.lo / V, vhi = vec ? max(vlo, r.hi / V) : vlo;
     const u32x4* s = reinterpret_cast<const u32x4*>(src);
     u32x4* d = reinterpret_cast<u32x4*>(dst);
     uint64_t v = vlo + threadIdx.x;
@@ -95,7 +117,7 @@ __device__ __forceinline__ void CopyRange(S* dst, const S* src, Range r)
         for (int u = 0; u < kIpcU; ++u) d[v + u * kIpcBlock] = x[u];
     }
     for (; v < vhi; v += kIpcBlock) d[v] = s[v];
-    for (uint64_t e = vhi * V + threadIdx.x; e < r.hi; e += kIpcBlock) dst[e] = src[e];
+    for (uint64_t e = max(vhi * V, r.lo) + threadIdx.x; e < r.hi; e += kIpcBlock) dst[e] = src[e];
 }
 
 template <class E, int OP>
@@ -107,66 +129,72 @@ __global__ __launch_bounds__(kIpcBlock) void k_allreduce_ipc(IpcArgs a)
     const uint32_t me = a.me >= 0 ? static_cast<uint32_t>(a.me) : blockIdx.y;
     const S* in = static_cast<const S*>(a.in[me]);
     S* out = static_cast<S*>(a.out[me]);
+    // a communicator whose IPC barrier ever timed out stays failed (sticky bit): never wait on its peers again
+    if ((__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 1u) != 0) return;
     uint32_t epoch = a.epochBase;
     for (uint64_t base = 0; base < a.count; base += a.roundElems) {
         const uint64_t len = min(a.roundElems, a.count - base);
-        // phase 0: own input -> own staging, every chunk's block-b range
-        S* stg = static_cast<S*>(a.stgIn[me]);
+        const uint64_t cs = ChunkElems(len, n, V);
+        // phase 0: my values of chunk c -> owner c's slot `me` (pointer offset so that index e is round coordinate)
         for (uint32_t c = 0; c < n; ++c) {
-            Range r = BlockRange(len, n, c, V);
-            CopyRange<S>(stg, in + base, r);
+            if (c == me) continue;
+            const uint64_t clo = min(len, uint64_t(c) * cs);
+            S* slot = static_cast<S*>(a.stgIn[c]) + uint64_t(me) * cs - clo;
+            CopyRange<S>(slot, in + base, BlockRange(len, c, cs, V), a.aligned);
         }
-        Barrier(a, me, ++epoch);
-        // phase 1: fold chunk `me` over all stagings in rank order (O2)
+        if (!Barrier(a, me, ++epoch)) return;
+        // phase 1: fold chunk `me` over the slots in rank order (O2); slot `me` is my own input
         {
-            Range r = BlockRange(len, n, me, V);
-            const uint64_t clo = ChunkLo(len, n, me, V);
-            S* res = static_cast<S*>(a.stgRes[me]);
-            const uint64_t vlo = r.lo / V, vhi = r.hi / V;
+            const Range r = BlockRange(len, me, cs, V);
+            const uint64_t clo = min(len, uint64_t(me) * cs);
+            const S* inb = in + base;
+            const S* slots = static_cast<const S*>(a.stgIn[me]) - clo;
+            auto src = [&](uint32_t q) { return q == me ? inb : slots + uint64_t(q) * cs; };
+            const uint64_t vlo = r.lo / V, vhi = a.aligned ? max(vlo, r.hi / V) : vlo;
             uint64_t v = vlo + threadIdx.x;
             for (; v + (kIpcU - 1) * kIpcBlock < vhi; v += kIpcU * kIpcBlock) {
                 u32x4 acc[kIpcU];
-                const u32x4* s0 = reinterpret_cast<const u32x4*>(a.stgIn[0]);
 #pragma unroll
-                for (int u = 0; u < kIpcU; ++u) acc[u] = s0[v + u * kIpcBlock];
+                for (int u = 0; u < kIpcU; ++u) acc[u] = reinterpret_cast<const u32x4*>(src(0))[v + u * kIpcBlock];
                 for (uint32_t q = 1; q < n; ++q) {
-                    const u32x4* sq = reinterpret_cast<const u32x4*>(a.stgIn[q]);
                     u32x4 x[kIpcU];
 #pragma unroll
-                    for (int u = 0; u < kIpcU; ++u) x[u] = sq[v + u * kIpcBlock];
+                    for (int u = 0; u < kIpcU; ++u) x[u] = reinterpret_cast<const u32x4*>(src(q))[v + u * kIpcBlock];
 #pragma unroll
                     for (int u = 0; u < kIpcU; ++u) acc[u] = combine<E, OP>(x[u], acc[u]);
                 }
 #pragma unroll
-                for (int u = 0; u < kIpcU; ++u) {
-                    reinterpret_cast<u32x4*>(out + base)[v + u * kIpcBlock] = acc[u];
-                    reinterpret_cast<u32x4*>(res - clo)[v + u * kIpcBlock] = acc[u];
+                for (int u = 0; u < kIpcU; ++u) reinterpret_cast<u32x4*>(out + base)[v + u * kIpcBlock] = acc[u];
+                for (uint32_t p = 0; p < n; ++p) {
+                    if (p == me) continue;
+                    u32x4* res = reinterpret_cast<u32x4*>(a.stgRes[p]);
+#pragma unroll
+                    for (int u = 0; u < kIpcU; ++u) res[v + u * kIpcBlock] = acc[u];
                 }
             }
             for (; v < vhi; v += kIpcBlock) {
-                u32x4 acc = reinterpret_cast<const u32x4*>(a.stgIn[0])[v];
-                for (uint32_t q = 1; q < n; ++q) {
-                    acc = combine<E, OP>(reinterpret_cast<const u32x4*>(a.stgIn[q])[v], acc);
-                }
+                u32x4 acc = reinterpret_cast<const u32x4*>(src(0))[v];
+                for (uint32_t q = 1; q < n; ++q) acc = combine<E, OP>(reinterpret_cast<const u32x4*>(src(q))[v], acc);
                 reinterpret_cast<u32x4*>(out + base)[v] = acc;
-                reinterpret_cast<u32x4*>(res - clo)[v] = acc;
+                for (uint32_t p = 0; p < n; ++p) {
+                    if (p != me) reinterpret_cast<u32x4*>(a.stgRes[p])[v] = acc;
+                }
             }
-            for (uint64_t e = vhi * V + threadIdx.x; e < r.hi; e += kIpcBlock) {
-                S acc = static_cast<const S*>(a.stgIn[0])[e];
-                for (uint32_t q = 1; q < n; ++q) acc = E::template ap<OP>(static_cast<const S*>(a.stgIn[q])[e], acc);
+            for (uint64_t e = max(vhi * V, r.lo) + threadIdx.x; e < r.hi; e += kIpcBlock) {
+                S acc = src(0)[e];
+                for (uint32_t q = 1; q < n; ++q) acc = E::template ap<OP>(src(q)[e], acc);
                 out[base + e] = acc;
-                res[e - clo] = acc;
+                for (uint32_t p = 0; p < n; ++p) {
+                    if (p != me) static_cast<S*>(a.stgRes[p])[e] = acc;
+                }
             }
         }
-        Barrier(a, me, ++epoch);
-        // phase 2: the other chunks from their owners' result areas
+        if (!Barrier(a, me, ++epoch)) return;
+        // phase 2: the other chunks from my own result area
         for (uint32_t c = 0; c < n; ++c) {
             if (c == me) continue;
-            Range r = BlockRange(len, n, c, V);
-            const uint64_t clo = ChunkLo(len, n, c, V);
-            CopyRange<S>(out + base, static_cast<const S*>(a.stgRes[c]) - clo, r);
+            CopyRange<S>(out + base, static_cast<const S*>(a.stgRes[me]), BlockRange(len, c, cs, V), a.aligned);
         }
-        Barrier(a, me, ++epoch);
     }
 }
 

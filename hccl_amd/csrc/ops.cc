@@ -255,6 +255,23 @@ HcclResult HcclAmdCommInitLoopback(uint32_t nRanks, HcclComm* comms)
     return HCCL_SUCCESS;
 }
 
+HcclResult HcclAmdCommInitHostExchange(uint32_t nRanks, uint32_t rank, HcclAmdHostAllGatherFn fn, void* ctx,
+                                       HcclComm* comm)
+{
+    if (fn == nullptr || comm == nullptr) return HCCL_E_PTR;
+    if (nRanks == 0 || rank >= nRanks || nRanks > kIpcMaxRanks) return HCCL_E_PARA;
+    int dev = 0;
+    HIP_CHK(hipGetDevice(&dev));
+    auto c = std::make_unique<Comm>();
+    c->rank = rank;
+    c->nRanks = nRanks;
+    HCCL_CHK(c->Init(dev));
+    c->transport = MakeHostExchangeTransport(fn, ctx);
+    c->algoOverride = HCCL_AMD_ALGO_IPC_TWOSHOT;
+    *comm = c.release();
+    return HCCL_SUCCESS;
+}
+
 HcclResult HcclAmdCommSetAlgo(HcclComm comm, int32_t algo)
 {
     Comm* c = AsComm(comm);

@@ -125,8 +125,23 @@ extern HcclResult HcclAmdCommSetPieceBytes(HcclComm comm, uint64_t pieceBytes);
 /* Algorithm the last collective on comm executed (HcclAmdAlgo), or -1. */
 extern int32_t HcclAmdCommLastAlgo(HcclComm comm);
 
-/* Status word of the IPC path (synchronous read): bit 0 = a cross-rank barrier timed out (results invalid). */
+/* Status of the IPC path of comm (synchronous read). Bit 0: a cross-rank barrier wait exceeded HCCL_AMD_IPC_TIMEOUT_MS
+ * (default 60000) — the results of that and every later IPC AllReduce on comm are invalid (sticky: the communicator is
+ * failed, as after an asynchronous error). Bits 8-15: bit length of the longest barrier wait of the last IPC
+ * AllReduce, in polls (diagnostic; 0 = no block ever waited). */
 extern HcclResult HcclAmdCommIpcStatus(HcclComm comm, uint32_t* status);
+
+/* Blocking host all-gather supplied by the caller's bootstrap (a TCP store, MPI, torch.distributed gloo ...):
+ * gathers `bytes` bytes from every rank into all[nRanks * bytes] in rank order; returns 0 on success. */
+typedef int32_t (*HcclAmdHostAllGatherFn)(void* ctx, const void* mine, uint64_t bytes, void* all);
+
+/* Rank `rank` of an IPC-only communicator on the current HIP device, bootstrapped through `fn` instead of RCCL.
+ * Its data path is the one-sided AllReduce (HCCL_AMD_ALGO_IPC_TWOSHOT, the default on such a communicator) over
+ * peer-mapped memory opened with hipIpcOpenMemHandle; collectives that need send/recv return HCCL_E_NOT_SUPPORT.
+ * Ranks may share a device (separate processes), which is how the rank-mode IPC path is tested on one GPU.
+ * `fn` and `ctx` must stay valid for the communicator's lifetime. */
+extern HcclResult HcclAmdCommInitHostExchange(uint32_t nRanks, uint32_t rank, HcclAmdHostAllGatherFn fn, void* ctx,
+                                              HcclComm* comm);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,194 @@
+"""The one-sided IPC AllReduce in RANK mode: n separate processes, each one rank with its own launch, peers' staging
+and flags opened from hipIpcMemHandles — the path the 8-GPU node runs (here all ranks share the one GPU, which the
+bootstrap-only communicator of HcclAmdCommInitHostExchange allows; RCCL refuses two ranks on one device).
+Expected results: order O2 (acc = x_0, then x_1 .. x_{n-1}; ins_temp_all_reduce_mesh_1D_two_shot.cc:327-335), from
+the oracle's fold, bit-exact."""
+import datetime
+import multiprocessing as mp
+import os
+import socket
+import time
+import traceback
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+# (dtype, op, count): ragged counts, every reduce dtype family, and a count that needs two staging rounds
+CASES = [
+    (O.FP32, O.SUM, 1), (O.FP32, O.SUM, 4099), (O.FP32, O.MAX, 100003), (O.FP32, O.SUM, (36 << 20) + 11),
+    (O.FP16, O.SUM, 65537), (O.BFP16, O.SUM, 70001), (O.BFP16, O.MIN, 4097), (O.INT32, O.PROD, 9999),
+    (O.INT8, O.SUM, 33333), (O.INT64, O.MAX, 5000), (O.FP64, O.SUM, 12345), (O.FP32, O.PROD, 777),
+    (O.FP32, O.SUM, 250001),
+]
+UNALIGNED_CASE = len(CASES) - 1
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _inputs(dtype, count, n, seed):
+    return [O.random_operands(dtype, count, seed * 1000 + r) for r in range(n)]
+
+
+def _rank_main(rank, n, port, q):
+    os.environ["HCCL_AMD_IPC_TIMEOUT_MS"] = "20000"  # a lost peer shows as a status bit, never a hang
+    os.makedirs("gpurun_out", exist_ok=True)
+    progress = open(f"gpurun_out/ipc_ranks_n{n}_r{rank}.log", "w", buffering=1)
+    try:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n,
+                                timeout=datetime.timedelta(seconds=120))
+        torch.cuda.set_device(0)
+        import hccl_amd as H
+        from _util import to_device, to_host
+
+        def all_gather(b):
+            out = [None] * n
+            dist.all_gather_object(out, b)
+            return out
+
+        comm = H.comm_init_host_exchange(n, rank, all_gather)
+        stream = torch.cuda.Stream()
+        results = []
+        for i, (dtype, op, count) in enumerate(CASES):
+            progress.write(f"case {i} {CASES[i]} start\n")
+            send = to_device(dtype, _inputs(dtype, count, n, i)[rank])
+            recv = torch.empty_like(send)
+            if i == UNALIGNED_CASE and rank == n - 1:  # one rank with unaligned buffers: still the IPC path
+                send = torch.cat([send[:1], send])[1:]
+                recv = torch.empty(count + 1, dtype=send.dtype, device=send.device)[1:]
+            torch.cuda.synchronize()
+            comm.all_reduce(send, recv, op, stream=stream)
+            stream.synchronize()
+            status = comm.ipc_status()
+            progress.write(f"case {i} done status {status} algo {comm.last_algo}\n")
+            results.append((i, status, comm.last_algo, to_host(dtype, recv).tobytes()))
+            if max(all_gather(status & 1)) != 0:  # every rank stops together after a barrier timeout anywhere
+                break
+        dist.barrier()
+        comm.destroy()  # collective: no rank unmaps while a peer's kernel may still store into it
+        progress.write("destroyed\n")
+        dist.destroy_process_group()
+        q.put((rank, "ok", results if rank == 0 else [(i, s, a, None) for i, s, a, _ in results]))
+    except Exception:  # noqa: BLE001
+        progress.write(traceback.format_exc())
+        q.put((rank, traceback.format_exc(), None))
+        time.sleep(10)  # peers' kernels are bounded: let them drain before this process's memory goes away
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_ipc_allreduce_rank_mode(n):
+    import sched_ref as R
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, n, port, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    try:
+        got = {}
+        for _ in procs:
+            rank, msg, res = q.get(timeout=300)
+            got[rank] = (msg, res)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(n):
+        assert got[r][0] == "ok", f"rank {r}:\n{got[r][0]}"
+    for r in range(n):
+        assert len(got[r][1]) == len(CASES), f"rank {r} stopped after case {len(got[r][1]) - 1}"
+        for i, status, algo, _ in got[r][1]:
+            assert status & 1 == 0, f"rank {r} case {CASES[i]}: barrier timeout (status {status:#x})"
+            assert algo == R.ALGO_IPC
+    for i, status, algo, raw in got[0][1]:
+        dtype, op, count = CASES[i]
+        want = R.allreduce_o2(dtype, op, _inputs(dtype, count, n, i))[0]
+        assert O.equal_bits(dtype, np.frombuffer(raw, dtype=want.dtype), want), f"case {CASES[i]} differs from O2"
+
+
+def _lost_peer_main(rank, port, q):
+    os.environ["HCCL_AMD_IPC_TIMEOUT_MS"] = "1500"
+    os.makedirs("gpurun_out", exist_ok=True)
+    progress = open(f"gpurun_out/ipc_lost_peer_r{rank}.log", "w", buffering=1)
+    try:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2,
+                                timeout=datetime.timedelta(seconds=120))
+        torch.cuda.set_device(0)
+        import hccl_amd as H
+
+        def all_gather(b):
+            out = [None] * 2
+            dist.all_gather_object(out, b)
+            return out
+
+        comm = H.comm_init_host_exchange(2, rank, all_gather)
+        stream = torch.cuda.Stream()
+        x = torch.full((1 << 20,), float(rank + 1), device="cuda")
+        y = torch.empty_like(x)
+        torch.cuda.synchronize()
+        comm.all_reduce(x, y, H.HcclReduceOp.SUM, stream=stream)  # both ranks: set-up + a good call
+        stream.synchronize()
+        res = {"first_status": comm.ipc_status(), "first_ok": bool(torch.all(y == 3.0).item())}
+        progress.write(f"first {res}\n")
+        dist.barrier()
+        if rank == 0:  # rank 1 never joins this call
+            t0 = time.time()
+            comm.all_reduce(x, y, H.HcclReduceOp.SUM, stream=stream)
+            stream.synchronize()
+            res["lost_s"] = time.time() - t0
+            res["lost_status"] = comm.ipc_status()
+            t0 = time.time()
+            comm.all_reduce(x, y, H.HcclReduceOp.SUM, stream=stream)  # sticky: returns without waiting
+            stream.synchronize()
+            res["after_s"] = time.time() - t0
+            res["after_status"] = comm.ipc_status()
+            progress.write(f"lost {res}\n")
+        dist.barrier()
+        comm.destroy()
+        dist.destroy_process_group()
+        q.put((rank, "ok", res))
+    except Exception:  # noqa: BLE001
+        progress.write(traceback.format_exc())
+        q.put((rank, traceback.format_exc(), None))
+        time.sleep(10)
+
+
+def test_ipc_lost_peer_times_out_and_sticks():
+    """A peer that never joins: the barrier gives up after HCCL_AMD_IPC_TIMEOUT_MS with status bit 0 (no hang), the
+    communicator stays failed (the next call returns at once with the bit still set), teardown still completes."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_lost_peer_main, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        got = {}
+        for _ in procs:
+            rank, msg, res = q.get(timeout=300)
+            got[rank] = (msg, res)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(2):
+        assert got[r][0] == "ok", f"rank {r}:\n{got[r][0]}"
+        assert got[r][1]["first_ok"] and got[r][1]["first_status"] & 1 == 0
+    r0 = got[0][1]
+    assert r0["lost_status"] & 1 == 1
+    assert 1.0 < r0["lost_s"] < 15.0, r0
+    assert r0["after_status"] & 1 == 1
+    assert r0["after_s"] < 1.0, r0
