@@ -72,10 +72,11 @@ struct Comm {
     ~Comm();
 };
 
-// One-sided AllReduce (HCCL_AMD_ALGO_IPC_TWOSHOT), any buffer alignment. Returns HCCL_E_NOT_SUPPORT, on every rank
-// alike, when the peer mappings cannot be set up (the caller then runs the RCCL two-shot, which has the same order O2).
-HcclResult RunIpcAllReduce(Comm& c, const void* sendBuf, void* recvBuf, uint64_t count, HcclDataType dt,
-                           HcclReduceOp op, hipStream_t stream);
+// One-sided AllReduce / ReduceScatter / Reduce (HCCL_AMD_ALGO_IPC_TWOSHOT), any buffer alignment, in the
+// reference's orders (O2 / O1 / two-shot O1). Returns HCCL_E_NOT_SUPPORT, on every rank alike, when the peer mappings
+// cannot be set up (the caller then runs the RCCL schedule of the same order).
+HcclResult RunIpcCollective(Comm& c, int32_t opType, const void* sendBuf, void* recvBuf, uint64_t count,
+                            HcclDataType dt, HcclReduceOp op, uint32_t root, hipStream_t stream);
 // Collective: every rank's IPC kernels have finished before any rank unmaps or frees (called by ~Comm).
 void IpcQuiesce(Comm& c);
 void IpcRelease(Comm& c);

@@ -7,6 +7,7 @@
 // In a loopback world the ranks share a device and the raw pointers are exchanged instead, and the whole world runs
 // as one launch (all ranks' blocks must be resident together, which separate per-rank launches on 4 hardware queues
 // would not guarantee).
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -147,16 +148,23 @@ void IpcRelease(Comm& c)
     s = IpcState{};
 }
 
-HcclResult RunIpcAllReduce(Comm& c, const void* sendBuf, void* recvBuf, uint64_t count, HcclDataType dt,
-                           HcclReduceOp op, hipStream_t stream)
+HcclResult RunIpcCollective(Comm& c, int32_t opType, const void* sendBuf, void* recvBuf, uint64_t count,
+                            HcclDataType dt, HcclReduceOp op, uint32_t root, hipStream_t stream)
 {
     const uint64_t es = DataTypeSize(dt);
     if (es == 0 || c.nRanks > kIpcMaxRanks) return HCCL_E_NOT_SUPPORT;
+    IpcKind kind;
+    switch (opType) {
+        case HCCL_AMD_OP_ALLREDUCE: kind = kIpcAllReduce; break;
+        case HCCL_AMD_OP_REDUCE_SCATTER: kind = kIpcReduceScatter; break;
+        case HCCL_AMD_OP_REDUCE: kind = kIpcReduce; break;
+        default: return HCCL_E_NOT_SUPPORT;
+    }
     HCCL_CHK(IpcSetup(c));
     IpcState& s = c.ipc;
     const uint32_t n = c.nRanks;
-    const uint64_t unit = uint64_t(n) * (16 / es);
-    const uint64_t roundElems = (s.stgInBytes / es) / unit * unit;
+    const uint64_t V = 16 / es;
+
     IpcArgs a{};
     for (uint32_t r = 0; r < n; ++r) {
         a.stgIn[r] = s.peerStg[r];
@@ -164,46 +172,46 @@ HcclResult RunIpcAllReduce(Comm& c, const void* sendBuf, void* recvBuf, uint64_t
         a.flags[r] = s.peerFlags[r];
     }
     a.n = n;
-    a.roundElems = roundElems;
+    a.kind = kind;
+    a.root = root;
+    if (kind == kIpcReduceScatter) {
+        // block c of the input (recvCount elements) is chunk c (reduce_scatter_op.cc:158-159)
+        a.total = uint64_t(n) * count;
+        a.chunkStride = a.chunkLen = count;
+    } else {
+        // ceil(count / n) rounded up to HCCL_MIN_SLICE_ALIGN = 128 B (alg_template_base.h:34), as the RCCL path and
+        // the reference's two-shot templates slice: the Reduce order (chunk owner first) depends on these bounds
+        const uint64_t align = 128 / es;
+        const uint64_t cs = ((count + n - 1) / n + align - 1) / align * align;
+        a.total = count;
+        a.chunkStride = a.chunkLen = cs;
+    }
+    const uint64_t slotCap = (s.stgInBytes / es / n) / V * V;
+    a.piece = std::min(slotCap, (a.chunkLen + V - 1) / V * V);
+    a.blockElems = ((a.piece + s.blocks - 1) / s.blocks + V - 1) / V * V;
+    a.rounds = static_cast<uint32_t>((a.chunkLen + a.piece - 1) / a.piece);
     a.timeoutTicks = IpcTimeoutTicks();  // a lost peer ends the kernel with status bit 0, never a hang
     a.status = s.status;
-
-    // The per-block barrier is sound only while every round of a launch has the same geometry (block b touches the
-    // same slot and result addresses each round); a shorter last round moves every block's range, so it runs as a
-    // launch of its own (a kernel ends only after all its blocks passed their last barrier on every rank).
-    const uint64_t fullElems = count / roundElems * roundElems;
-    struct Span {
-        uint64_t off, count;
-    };
-    Span spans[2];
-    int nspans = 0;
-    if (fullElems != 0) spans[nspans++] = {0, fullElems};
-    if (count != fullElems) spans[nspans++] = {fullElems, count - fullElems};
-    auto at = [es](const void* p, uint64_t off) { return static_cast<const char*>(p) + off * es; };
+    a.epochBase = s.epoch;
+    s.epoch += 2 * a.rounds;
+    const bool strideAligned = (a.chunkStride * es) % 16 == 0;
 
     if (!c.transport->SharedDevice()) {
         a.me = static_cast<int32_t>(c.rank);
-        a.aligned = Aligned16(sendBuf, recvBuf);
+        a.in[c.rank] = sendBuf;
+        a.out[c.rank] = recvBuf;
+        a.aligned = strideAligned && Aligned16(sendBuf, recvBuf);
         HIP_CHK(hipMemsetAsync(s.status + 1, 0, sizeof(uint32_t), stream));  // wait diagnostic of this call
-        for (int i = 0; i < nspans; ++i) {
-            a.in[c.rank] = at(sendBuf, spans[i].off);
-            a.out[c.rank] = const_cast<char*>(at(recvBuf, spans[i].off));
-            a.count = spans[i].count;
-            a.epochBase = s.epoch;
-            s.epoch += static_cast<uint32_t>(2 * ((spans[i].count + roundElems - 1) / roundElems));
-            HCCL_CHK(LaunchIpcAllReduce(a, s.blocks, 0, dt, op, stream));
-        }
-        return HCCL_SUCCESS;
+        return LaunchIpcCollective(a, s.blocks, 0, dt, op, stream);
     }
 
-    // loopback world: one launch per span for every rank, issued by rank 0 behind every rank's stream
+    // loopback world: one launch for every rank, issued by rank 0 behind every rank's stream
     struct Part {
         const void* in;
         void* out;
         hipEvent_t ready;
-        uint32_t* status;
     };
-    Part mine{sendBuf, recvBuf, nullptr, s.status};
+    Part mine{sendBuf, recvBuf, nullptr};
     c.nextEvent = 0;
     HCCL_CHK(c.NextEvent(&mine.ready));
     HIP_CHK(hipEventRecord(mine.ready, stream));
@@ -212,22 +220,15 @@ HcclResult RunIpcAllReduce(Comm& c, const void* sendBuf, void* recvBuf, uint64_t
     hipEvent_t done = nullptr;
     if (c.rank == 0) {
         a.me = -1;
-        a.aligned = true;
+        a.aligned = strideAligned;
         for (uint32_t r = 0; r < n; ++r) {
+            a.in[r] = all[r].in;
+            a.out[r] = all[r].out;
             a.aligned = a.aligned && Aligned16(all[r].in, all[r].out);
             HIP_CHK(hipStreamWaitEvent(stream, all[r].ready, 0));
         }
         HIP_CHK(hipMemsetAsync(s.status + 1, 0, sizeof(uint32_t), stream));
-        for (int i = 0; i < nspans; ++i) {
-            for (uint32_t r = 0; r < n; ++r) {
-                a.in[r] = at(all[r].in, spans[i].off);
-                a.out[r] = const_cast<char*>(at(all[r].out, spans[i].off));
-            }
-            a.count = spans[i].count;
-            a.epochBase = s.epoch;
-            s.epoch += static_cast<uint32_t>(2 * ((spans[i].count + roundElems - 1) / roundElems));
-            HCCL_CHK(LaunchIpcAllReduce(a, s.blocks, n, dt, op, stream));
-        }
+        HCCL_CHK(LaunchIpcCollective(a, s.blocks, n, dt, op, stream));
         HCCL_CHK(c.NextEvent(&done));
         HIP_CHK(hipEventRecord(done, stream));
     }

@@ -77,34 +77,31 @@ __device__ __forceinline__ bool Barrier(const IpcArgs& a, uint32_t me, uint32_t 
     return failed == 0;
 }
 
-// Chunk size of a round of `len` elements: ceil(len / n) rounded up to whole 16-B vectors.
-__device__ __forceinline__ uint64_t ChunkElems(uint64_t len, uint32_t n, uint64_t vecElems)
-{
-    uint64_t cs = (len + n - 1) / n;
-    return (cs + vecElems - 1) / vecElems * vecElems;
-}
-
 struct Range {
-    uint64_t lo, hi;  // elements, relative to the round base
+    uint64_t lo, hi;  // piece coordinates
 };
 
-// Block blockIdx.x's share of chunk c, in whole 16-B vectors (the last chunk may end mid-vector).
-__device__ __forceinline__ Range BlockRange(uint64_t len, uint32_t c, uint64_t cs, uint64_t vecElems)
+// Elements of chunk c in round k (piece coordinates [0, len)), and the block's fixed window clipped to it.
+__device__ __forceinline__ uint64_t PieceLen(const IpcArgs& a, uint32_t c, uint64_t kP)
 {
-    const uint64_t clo = min(len, uint64_t(c) * cs), chi = min(len, clo + cs);
-    uint64_t bs = (chi - clo + gridDim.x - 1) / gridDim.x;
-    bs = (bs + vecElems - 1) / vecElems * vecElems;
-    const uint64_t lo = min(chi, clo + uint64_t(blockIdx.x) * bs);
-    return {lo, min(chi, lo + bs)};
+    const uint64_t start = uint64_t(c) * a.chunkStride;
+    const uint64_t clen = start >= a.total ? 0 : min(a.chunkLen, a.total - start);
+    return kP >= clen ? 0 : min(a.piece, clen - kP);
 }
 
-// dst[e] = src[e] for e in r (both pointers pre-offset to round coordinates). vec = both pointers are 16-B aligned;
-// otherwise every element goes through the scalar loop.
+__device__ __forceinline__ Range BlockWindow(const IpcArgs& a, uint64_t len)
+{
+    const uint64_t lo = min(len, uint64_t(blockIdx.x) * a.blockElems);
+    return {lo, min(len, lo + a.blockElems)};
+}
+
+// dst[e] = src[e] for e in r. vec = both pointers are 16-B aligned; otherwise every element goes through the scalar
+// loop.
 template <typename S>
 __device__ __forceinline__ void CopyRange(S* dst, const S* src, Range r, bool vec)
 {
     constexpr uint64_t V = 16 / sizeof(S);
-    // r.lo is vector aligned unless the range is empty at the end of the round (lo = hi = len); r.hi may be anything
+    // r.lo is vector aligned unless the window is empty at the end of a piece (lo = hi = len); r.hi may be anything
     const uint64_t vlo = r.lo / V, vhi = vec ? max(vlo, r.hi / V) : vlo;
     const u32x4* s = reinterpret_cast<const u32x4*>(src);
     u32x4* d = reinterpret_cast<u32x4*>(dst);
@@ -120,11 +117,55 @@ __device__ __forceinline__ void CopyRange(S* dst, const S* src, Range r, bool ve
     for (uint64_t e = max(vhi * V, r.lo) + threadIdx.x; e < r.hi; e += kIpcBlock) dst[e] = src[e];
 }
 
-template <class E, int OP>
-__global__ __launch_bounds__(kIpcBlock) void k_allreduce_ipc(IpcArgs a)
+// Fold of chunk `me` over the n operands in the kind's order, written to up to kIpcMaxRanks destinations.
+//   all-reduce (O2):            operand i = rank i
+//   reduce-scatter / reduce (O1): operand 0 = rank me (the owner), then the others ascending
+template <class E, int OP, class Dst>
+__device__ __forceinline__ void FoldRange(const IpcArgs& a, uint32_t me, const typename E::S* own,
+                                          const typename E::S* slots, Dst dsts, uint32_t ndst, Range r)
 {
     using S = typename E::S;
     constexpr uint64_t V = 16 / sizeof(S);
+    const uint32_t n = a.n;
+    const bool o2 = a.kind == kIpcAllReduce;
+    auto src = [&](uint32_t i) {
+        const uint32_t q = o2 ? i : (i == 0 ? me : (i <= me ? i - 1 : i));
+        return q == me ? own : slots + uint64_t(q) * a.piece;
+    };
+    const uint64_t vlo = r.lo / V, vhi = a.aligned ? max(vlo, r.hi / V) : vlo;
+    uint64_t v = vlo + threadIdx.x;
+    for (; v + (kIpcU - 1) * kIpcBlock < vhi; v += kIpcU * kIpcBlock) {
+        u32x4 acc[kIpcU];
+#pragma unroll
+        for (int u = 0; u < kIpcU; ++u) acc[u] = reinterpret_cast<const u32x4*>(src(0))[v + u * kIpcBlock];
+        for (uint32_t i = 1; i < n; ++i) {
+            u32x4 x[kIpcU];
+#pragma unroll
+            for (int u = 0; u < kIpcU; ++u) x[u] = reinterpret_cast<const u32x4*>(src(i))[v + u * kIpcBlock];
+#pragma unroll
+            for (int u = 0; u < kIpcU; ++u) acc[u] = combine<E, OP>(x[u], acc[u]);
+        }
+        for (uint32_t d = 0; d < ndst; ++d) {
+#pragma unroll
+            for (int u = 0; u < kIpcU; ++u) reinterpret_cast<u32x4*>(dsts(d))[v + u * kIpcBlock] = acc[u];
+        }
+    }
+    for (; v < vhi; v += kIpcBlock) {
+        u32x4 acc = reinterpret_cast<const u32x4*>(src(0))[v];
+        for (uint32_t i = 1; i < n; ++i) acc = combine<E, OP>(reinterpret_cast<const u32x4*>(src(i))[v], acc);
+        for (uint32_t d = 0; d < ndst; ++d) reinterpret_cast<u32x4*>(dsts(d))[v] = acc;
+    }
+    for (uint64_t e = max(vhi * V, r.lo) + threadIdx.x; e < r.hi; e += kIpcBlock) {
+        S acc = src(0)[e];
+        for (uint32_t i = 1; i < n; ++i) acc = E::template ap<OP>(src(i)[e], acc);
+        for (uint32_t d = 0; d < ndst; ++d) dsts(d)[e] = acc;
+    }
+}
+
+template <class E, int OP>
+__global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
+{
+    using S = typename E::S;
     const uint32_t n = a.n;
     const uint32_t me = a.me >= 0 ? static_cast<uint32_t>(a.me) : blockIdx.y;
     const S* in = static_cast<const S*>(a.in[me]);
@@ -132,68 +173,43 @@ __global__ __launch_bounds__(kIpcBlock) void k_allreduce_ipc(IpcArgs a)
     // a communicator whose IPC barrier ever timed out stays failed (sticky bit): never wait on its peers again
     if ((__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 1u) != 0) return;
     uint32_t epoch = a.epochBase;
-    for (uint64_t base = 0; base < a.count; base += a.roundElems) {
-        const uint64_t len = min(a.roundElems, a.count - base);
-        const uint64_t cs = ChunkElems(len, n, V);
-        // phase 0: my values of chunk c -> owner c's slot `me` (pointer offset so that index e is round coordinate)
+    for (uint32_t k = 0; k < a.rounds; ++k) {
+        const uint64_t kP = uint64_t(k) * a.piece;
+        // phase 0: my piece of chunk c -> owner c's slot `me`
         for (uint32_t c = 0; c < n; ++c) {
             if (c == me) continue;
-            const uint64_t clo = min(len, uint64_t(c) * cs);
-            S* slot = static_cast<S*>(a.stgIn[c]) + uint64_t(me) * cs - clo;
-            CopyRange<S>(slot, in + base, BlockRange(len, c, cs, V), a.aligned);
+            const Range r = BlockWindow(a, PieceLen(a, c, kP));
+            S* slot = static_cast<S*>(a.stgIn[c]) + uint64_t(me) * a.piece;
+            CopyRange<S>(slot, in + uint64_t(c) * a.chunkStride + kP, r, a.aligned);
         }
         if (!Barrier(a, me, ++epoch)) return;
-        // phase 1: fold chunk `me` over the slots in rank order (O2); slot `me` is my own input
+        // phase 1: fold my chunk's piece over the slots (my own operand straight from my input)
         {
-            const Range r = BlockRange(len, me, cs, V);
-            const uint64_t clo = min(len, uint64_t(me) * cs);
-            const S* inb = in + base;
-            const S* slots = static_cast<const S*>(a.stgIn[me]) - clo;
-            auto src = [&](uint32_t q) { return q == me ? inb : slots + uint64_t(q) * cs; };
-            const uint64_t vlo = r.lo / V, vhi = a.aligned ? max(vlo, r.hi / V) : vlo;
-            uint64_t v = vlo + threadIdx.x;
-            for (; v + (kIpcU - 1) * kIpcBlock < vhi; v += kIpcU * kIpcBlock) {
-                u32x4 acc[kIpcU];
-#pragma unroll
-                for (int u = 0; u < kIpcU; ++u) acc[u] = reinterpret_cast<const u32x4*>(src(0))[v + u * kIpcBlock];
-                for (uint32_t q = 1; q < n; ++q) {
-                    u32x4 x[kIpcU];
-#pragma unroll
-                    for (int u = 0; u < kIpcU; ++u) x[u] = reinterpret_cast<const u32x4*>(src(q))[v + u * kIpcBlock];
-#pragma unroll
-                    for (int u = 0; u < kIpcU; ++u) acc[u] = combine<E, OP>(x[u], acc[u]);
-                }
-#pragma unroll
-                for (int u = 0; u < kIpcU; ++u) reinterpret_cast<u32x4*>(out + base)[v + u * kIpcBlock] = acc[u];
-                for (uint32_t p = 0; p < n; ++p) {
-                    if (p == me) continue;
-                    u32x4* res = reinterpret_cast<u32x4*>(a.stgRes[p]);
-#pragma unroll
-                    for (int u = 0; u < kIpcU; ++u) res[v + u * kIpcBlock] = acc[u];
-                }
-            }
-            for (; v < vhi; v += kIpcBlock) {
-                u32x4 acc = reinterpret_cast<const u32x4*>(src(0))[v];
-                for (uint32_t q = 1; q < n; ++q) acc = combine<E, OP>(reinterpret_cast<const u32x4*>(src(q))[v], acc);
-                reinterpret_cast<u32x4*>(out + base)[v] = acc;
-                for (uint32_t p = 0; p < n; ++p) {
-                    if (p != me) reinterpret_cast<u32x4*>(a.stgRes[p])[v] = acc;
-                }
-            }
-            for (uint64_t e = max(vhi * V, r.lo) + threadIdx.x; e < r.hi; e += kIpcBlock) {
-                S acc = src(0)[e];
-                for (uint32_t q = 1; q < n; ++q) acc = E::template ap<OP>(src(q)[e], acc);
-                out[base + e] = acc;
-                for (uint32_t p = 0; p < n; ++p) {
-                    if (p != me) static_cast<S*>(a.stgRes[p])[e] = acc;
-                }
-            }
+            const Range r = BlockWindow(a, PieceLen(a, me, kP));
+            const S* own = in + uint64_t(me) * a.chunkStride + kP;
+            const S* slots = static_cast<const S*>(a.stgIn[me]);
+            // destination 0: my output (or, for a non-root Reduce rank, the root's result area); all-reduce also
+            // pushes to every peer's result area (destinations 1 .. n-1 = the peers in ascending order)
+            S* first = a.kind == kIpcReduceScatter ? out + kP
+                     : (a.kind == kIpcReduce && me != a.root)
+                         ? static_cast<S*>(a.stgRes[a.root]) + uint64_t(me) * a.piece
+                         : out + uint64_t(me) * a.chunkStride + kP;
+            auto dst = [&](uint32_t d) {
+                if (d == 0) return first;
+                const uint32_t p = d - 1 < me ? d - 1 : d;
+                return static_cast<S*>(a.stgRes[p]) + uint64_t(me) * a.piece;
+            };
+            FoldRange<E, OP>(a, me, own, slots, dst, a.kind == kIpcAllReduce ? n : 1u, r);
         }
         if (!Barrier(a, me, ++epoch)) return;
-        // phase 2: the other chunks from my own result area
-        for (uint32_t c = 0; c < n; ++c) {
-            if (c == me) continue;
-            CopyRange<S>(out + base, static_cast<const S*>(a.stgRes[me]), BlockRange(len, c, cs, V), a.aligned);
+        // phase 2: the other chunks' results from my own result area (all-reduce: every rank; reduce: the root)
+        if (a.kind == kIpcAllReduce || (a.kind == kIpcReduce && me == a.root)) {
+            for (uint32_t c = 0; c < n; ++c) {
+                if (c == me) continue;
+                const Range r = BlockWindow(a, PieceLen(a, c, kP));
+                CopyRange<S>(out + uint64_t(c) * a.chunkStride + kP,
+                             static_cast<const S*>(a.stgRes[me]) + uint64_t(c) * a.piece, r, a.aligned);
+            }
         }
     }
 }
@@ -202,17 +218,17 @@ template <class E>
 hipError_t LaunchIpcT(int op, const IpcArgs& a, dim3 grid, hipStream_t s)
 {
     switch (op) {
-        case R_SUM: hipLaunchKernelGGL((k_allreduce_ipc<E, R_SUM>), grid, dim3(kIpcBlock), 0, s, a); break;
-        case R_PROD: hipLaunchKernelGGL((k_allreduce_ipc<E, R_PROD>), grid, dim3(kIpcBlock), 0, s, a); break;
-        case R_MAX: hipLaunchKernelGGL((k_allreduce_ipc<E, R_MAX>), grid, dim3(kIpcBlock), 0, s, a); break;
-        default: hipLaunchKernelGGL((k_allreduce_ipc<E, R_MIN>), grid, dim3(kIpcBlock), 0, s, a); break;
+        case R_SUM: hipLaunchKernelGGL((k_ipc_collective<E, R_SUM>), grid, dim3(kIpcBlock), 0, s, a); break;
+        case R_PROD: hipLaunchKernelGGL((k_ipc_collective<E, R_PROD>), grid, dim3(kIpcBlock), 0, s, a); break;
+        case R_MAX: hipLaunchKernelGGL((k_ipc_collective<E, R_MAX>), grid, dim3(kIpcBlock), 0, s, a); break;
+        default: hipLaunchKernelGGL((k_ipc_collective<E, R_MIN>), grid, dim3(kIpcBlock), 0, s, a); break;
     }
     return hipGetLastError();
 }
 
 }  // namespace
 
-HcclResult LaunchIpcAllReduce(const IpcArgs& a, uint32_t blocks, uint32_t worldRanks, HcclDataType dt,
+HcclResult LaunchIpcCollective(const IpcArgs& a, uint32_t blocks, uint32_t worldRanks, HcclDataType dt,
                               HcclReduceOp op, hipStream_t stream)
 {
     dim3 grid(blocks, worldRanks == 0 ? 1 : worldRanks);
@@ -230,7 +246,7 @@ HcclResult LaunchIpcAllReduce(const IpcArgs& a, uint32_t blocks, uint32_t worldR
         default: return HCCL_E_NOT_SUPPORT;
     }
     if (e != hipSuccess) {
-        HCCL_AMD_ERR("ipc allreduce launch failed: %s", hipGetErrorString(e));
+        HCCL_AMD_ERR("ipc collective launch failed: %s", hipGetErrorString(e));
         return HCCL_E_RUNTIME;
     }
     return HCCL_SUCCESS;

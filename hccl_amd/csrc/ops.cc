@@ -76,14 +76,17 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
         p.algo = HCCL_AMD_ALGO_ORDER_PRESERVED;
     }
     if (p.algo == HCCL_AMD_ALGO_IPC_TWOSHOT) {
-        if (opType == HCCL_AMD_OP_ALLREDUCE) {
-            HcclResult r = RunIpcAllReduce(c, sendBuf, recvBuf, count, dt, op, stream);
+        if (opType != HCCL_AMD_OP_ALLGATHER) {
+            HcclResult r = RunIpcCollective(c, opType, sendBuf, recvBuf, count, dt, op, root, stream);
             if (r != HCCL_E_NOT_SUPPORT) {
                 c.lastAlgo = HCCL_AMD_ALGO_IPC_TWOSHOT;
                 return r;
             }
         }
-        p.algo = HCCL_AMD_ALGO_MESH_TWOSHOT;  // same order (O2) through the RCCL executor
+        // the RCCL schedule with the same order: AllReduce / Reduce two-shot (O2 / owner-first O1), ReduceScatter
+        // mesh (O1); AllGather has no IPC form
+        p.algo = opType == HCCL_AMD_OP_REDUCE_SCATTER || opType == HCCL_AMD_OP_ALLGATHER ? HCCL_AMD_ALGO_MESH_ONESHOT
+                                                                                          : HCCL_AMD_ALGO_MESH_TWOSHOT;
     }
     p.nRanks = c.nRanks;
     p.rank = c.rank;

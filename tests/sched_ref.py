@@ -227,11 +227,12 @@ def expected(op_type, algo, dtype, op, xs, count, root=0):
                 ALGO_IPC: allreduce_o2}[algo](dtype, op, xs)
     if op_type == 1:
         return {ALGO_ONESHOT: reduce_scatter_o1, ALGO_RING: reduce_scatter_ring,
-                ALGO_TREE: reduce_scatter_tree}[algo](dtype, op, xs, count)
+                ALGO_TREE: reduce_scatter_tree, ALGO_IPC: reduce_scatter_o1}[algo](dtype, op, xs, count)
     if op_type == 3:
         full = np.concatenate([x[:count] for x in xs])
         return [full.copy() for _ in xs]
     if op_type == 2:
-        r = {ALGO_ONESHOT: reduce_oneshot, ALGO_TWOSHOT: reduce_twoshot}[algo](dtype, op, xs, root)
+        r = {ALGO_ONESHOT: reduce_oneshot, ALGO_TWOSHOT: reduce_twoshot, ALGO_IPC: reduce_twoshot}[algo](
+            dtype, op, xs, root)
         return [r if q == root else None for q in range(len(xs))]
     raise ValueError(op_type)

@@ -101,8 +101,8 @@ def oracle_replay(op_type, algo, n, count, dtype, op, xs, root, piece_bytes):
     return [b[1] for b in bufs]
 
 
-CASES = [(AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5), (AR, 6), (AR, 7), (RS, 1), (RS, 3), (RS, 6), (RED, 1),
-         (RED, 2), (AG, 1), (AG, 3)]
+CASES = [(AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5), (AR, 6), (AR, 7), (RS, 1), (RS, 3), (RS, 6), (RS, 7),
+         (RED, 1), (RED, 2), (RED, 7), (AG, 1), (AG, 3)]
 
 
 def ipc_status(comm):
@@ -124,6 +124,26 @@ def test_ipc_allreduce_o2_and_status(worlds, n, count):
     assert ipc_status(comms[0]) & 1 == 0
     want = R.expected(AR, R.ALGO_TWOSHOT, O.FP32, O.SUM, xs, count)
     for r in range(n):
+        assert O.equal_bits(O.FP32, outs[r], want[r]), r
+
+
+@pytest.mark.parametrize("op_type,n,count", [(RS, 2, (17 << 20) + 5), (RS, 4, 3), (RED, 4, (36 << 20) + 7),
+                                              (RED, 3, 5)])
+def test_ipc_reduce_scatter_and_reduce(worlds, op_type, n, count):
+    """IPC ReduceScatter (order O1 per block owner) and Reduce (two-shot O1, chunk owner first, root gathers), with
+    several pieces per chunk and with chunks smaller than one vector."""
+    comms = worlds(n)
+    root = n // 2
+    in_count = count * n if op_type == RS else count
+    xs = [O.random_operands(O.FP32, in_count, seed=600 + r, edge=False) for r in range(n)]
+    used, outs = collective(comms, op_type, 7, O.FP32, O.SUM, xs, count, root=root)
+    assert used == 7
+    assert ipc_status(comms[0]) & 1 == 0
+    want = R.expected(op_type, R.ALGO_IPC, O.FP32, O.SUM, xs, count, root=root)
+    for r in range(n):
+        if op_type == RED and r != root:
+            assert not outs[r].any(), "non-root recvBuf written"
+            continue
         assert O.equal_bits(O.FP32, outs[r], want[r]), r
 
 
@@ -196,7 +216,7 @@ def test_fp32_sum(worlds, op_type, algo, n, count, streams, monkeypatch):
 @pytest.mark.parametrize("dtype", [O.INT8, O.INT16, O.INT32, O.INT64, O.UINT64, O.FP16, O.BFP16, O.FP64],
                          ids=lambda v: O.DTYPE_NAMES[v])
 @pytest.mark.parametrize("op", O.OPS, ids=lambda v: O.OP_NAMES[v])
-@pytest.mark.parametrize("op_type,algo", [(AR, 1), (AR, 2), (AR, 3), (AR, 7), (RS, 1), (RED, 2)])
+@pytest.mark.parametrize("op_type,algo", [(AR, 1), (AR, 2), (AR, 3), (AR, 7), (RS, 1), (RS, 7), (RED, 2), (RED, 7)])
 def test_dtypes_ops(worlds, op_type, algo, dtype, op):
     n, count, root = 4, 40961, 2
     comms = worlds(n)
@@ -215,7 +235,7 @@ def test_dtypes_ops(worlds, op_type, algo, dtype, op):
         assert O.equal_bits(dtype, outs[r], want[r]), r
 
 
-@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5, 6, 7])
 def test_allreduce_inplace(worlds, algo):
     n, count = 4, 300007
     comms = worlds(n)

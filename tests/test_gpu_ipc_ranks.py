@@ -17,14 +17,22 @@ from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
-# (dtype, op, count): ragged counts, every reduce dtype family, and a count that needs two staging rounds
+AR, RS, RED = 0, 1, 2
+# (collective, dtype, op, count): ragged counts, every reduce dtype family, counts that need several pieces per chunk
 CASES = [
-    (O.FP32, O.SUM, 1), (O.FP32, O.SUM, 4099), (O.FP32, O.MAX, 100003), (O.FP32, O.SUM, (36 << 20) + 11),
-    (O.FP16, O.SUM, 65537), (O.BFP16, O.SUM, 70001), (O.BFP16, O.MIN, 4097), (O.INT32, O.PROD, 9999),
-    (O.INT8, O.SUM, 33333), (O.INT64, O.MAX, 5000), (O.FP64, O.SUM, 12345), (O.FP32, O.PROD, 777),
-    (O.FP32, O.SUM, 250001),
+    (AR, O.FP32, O.SUM, 1), (AR, O.FP32, O.SUM, 4099), (AR, O.FP32, O.MAX, 100003), (AR, O.FP32, O.SUM, (36 << 20) + 11),
+    (AR, O.FP16, O.SUM, 65537), (AR, O.BFP16, O.SUM, 70001), (AR, O.BFP16, O.MIN, 4097), (AR, O.INT32, O.PROD, 9999),
+    (AR, O.INT8, O.SUM, 33333), (AR, O.INT64, O.MAX, 5000), (AR, O.FP64, O.SUM, 12345), (AR, O.FP32, O.PROD, 777),
+    (RS, O.FP32, O.SUM, 3), (RS, O.FP32, O.SUM, 50001), (RS, O.BFP16, O.MAX, 20003), (RS, O.FP32, O.SUM, (17 << 20) + 5),
+    (RED, O.FP32, O.SUM, 5), (RED, O.FP16, O.SUM, 60001), (RED, O.FP32, O.MIN, (36 << 20) + 7),
+    (AR, O.FP32, O.SUM, 250001),
 ]
 UNALIGNED_CASE = len(CASES) - 1
+ROOT = 1
+
+
+def _in_count(kind, count, n):
+    return count * n if kind == RS else count
 
 
 def _free_port():
@@ -48,6 +56,7 @@ def _rank_main(rank, n, port, q):
                                 timeout=datetime.timedelta(seconds=120))
         torch.cuda.set_device(0)
         import hccl_amd as H
+        import sched_ref as R
         from _util import to_device, to_host
 
         def all_gather(b):
@@ -58,26 +67,37 @@ def _rank_main(rank, n, port, q):
         comm = H.comm_init_host_exchange(n, rank, all_gather)
         stream = torch.cuda.Stream()
         results = []
-        for i, (dtype, op, count) in enumerate(CASES):
+        for i, (kind, dtype, op, count) in enumerate(CASES):
             progress.write(f"case {i} {CASES[i]} start\n")
-            send = to_device(dtype, _inputs(dtype, count, n, i)[rank])
-            recv = torch.empty_like(send)
+            send = to_device(dtype, _inputs(dtype, _in_count(kind, count, n), n, i)[rank])
+            recv = torch.zeros(count, dtype=send.dtype, device=send.device)
             if i == UNALIGNED_CASE and rank == n - 1:  # one rank with unaligned buffers: still the IPC path
                 send = torch.cat([send[:1], send])[1:]
                 recv = torch.empty(count + 1, dtype=send.dtype, device=send.device)[1:]
             torch.cuda.synchronize()
-            comm.all_reduce(send, recv, op, stream=stream)
+            if kind == AR:
+                comm.all_reduce(send, recv, op, stream=stream)
+            elif kind == RS:
+                comm.reduce_scatter(send, recv, op, stream=stream)
+            else:
+                comm.reduce(send, recv, ROOT % n, op, stream=stream)
             stream.synchronize()
             status = comm.ipc_status()
-            progress.write(f"case {i} done status {status} algo {comm.last_algo}\n")
-            results.append((i, status, comm.last_algo, to_host(dtype, recv).tobytes()))
+            got = to_host(dtype, recv)
+            ok = True
+            if not (kind == RED and rank != ROOT % n):
+                xs = _inputs(dtype, _in_count(kind, count, n), n, i)
+                want = R.expected(kind, R.ALGO_IPC, dtype, op, xs, count, root=ROOT % n)[rank]
+                ok = O.equal_bits(dtype, got, want)
+            progress.write(f"case {i} done status {status} algo {comm.last_algo} ok {ok}\n")
+            results.append((i, status, comm.last_algo, ok))
             if max(all_gather(status & 1)) != 0:  # every rank stops together after a barrier timeout anywhere
                 break
         dist.barrier()
         comm.destroy()  # collective: no rank unmaps while a peer's kernel may still store into it
         progress.write("destroyed\n")
         dist.destroy_process_group()
-        q.put((rank, "ok", results if rank == 0 else [(i, s, a, None) for i, s, a, _ in results]))
+        q.put((rank, "ok", results))
     except Exception:  # noqa: BLE001
         progress.write(traceback.format_exc())
         q.put((rank, traceback.format_exc(), None))
@@ -85,7 +105,7 @@ def _rank_main(rank, n, port, q):
 
 
 @pytest.mark.parametrize("n", [2, 4])
-def test_ipc_allreduce_rank_mode(n):
+def test_ipc_collectives_rank_mode(n):
     import sched_ref as R
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -107,13 +127,12 @@ def test_ipc_allreduce_rank_mode(n):
         assert got[r][0] == "ok", f"rank {r}:\n{got[r][0]}"
     for r in range(n):
         assert len(got[r][1]) == len(CASES), f"rank {r} stopped after case {len(got[r][1]) - 1}"
-        for i, status, algo, _ in got[r][1]:
+        for i, status, algo, _ok in got[r][1]:
             assert status & 1 == 0, f"rank {r} case {CASES[i]}: barrier timeout (status {status:#x})"
             assert algo == R.ALGO_IPC
-    for i, status, algo, raw in got[0][1]:
-        dtype, op, count = CASES[i]
-        want = R.allreduce_o2(dtype, op, _inputs(dtype, count, n, i))[0]
-        assert O.equal_bits(dtype, np.frombuffer(raw, dtype=want.dtype), want), f"case {CASES[i]} differs from O2"
+    for r in range(n):
+        for i, status, algo, ok in got[r][1]:
+            assert ok, f"rank {r} case {CASES[i]} differs from the reference order"
 
 
 def _lost_peer_main(rank, port, q):

@@ -1,94 +1,122 @@
-"""Index model of the one-sided IPC AllReduce kernel (hccl_amd/csrc/ipc_kernels.hip), run on the CPU before any
-launch: every phase's accesses, with the kernel's exact loop bounds (vector loop over [vlo, vhi), element loop from
-max(vhi*V, lo) to hi), must stay inside their buffer and cover each element of the round exactly once.
+"""Index model of the one-sided IPC collectives (hccl_amd/csrc/ipc_kernels.hip, geometry from ipc.cc
+RunIpcCollective), run on the CPU before any launch. With the kernel's exact loop bounds (vector loop over
+[vlo, vhi), element loop from max(vhi*V, lo) to hi), every phase must
+  * stay inside each buffer it touches (input, output, a slot of the owner's staging, a result area), and
+  * cover each element of each chunk exactly once per phase,
+and block b must touch the same piece coordinates in every round of a launch (the per-block barrier relies on it).
 
-An element loop that started at vhi*V wrote one element before a peer's staging for an empty range at the end of a
-round (count 5, 4 ranks: chunks 2 and 3 are [5, 5)); this model pins the corrected bounds."""
+An element loop that started at vhi*V wrote one element before a peer's staging for an empty window at the end of a
+piece (count 5 on 4 ranks); this model pins the corrected bounds."""
 import numpy as np
 import pytest
 
 STG_BYTES = 128 << 20  # kIpcStagingBytes (slot area and result area each)
 BLOCKS = 128           # kIpcBlocks
+AR, RS, RED = 0, 1, 2
 
 
-def chunk_elems(length, n, v):
-    cs = -(-length // n)
-    return -(-cs // v) * v
+def geometry(kind, n, count, es):
+    """RunIpcCollective: (total, chunk stride = chunk length, piece, block elems, rounds)."""
+    v = 16 // es
+    if kind == RS:
+        total, clen = n * count, count
+    else:
+        align = 128 // es
+        clen = -(-(-(-count // n)) // align) * align
+        total = count
+    slot_cap = (STG_BYTES // es // n) // v * v
+    piece = min(slot_cap, -(-clen // v) * v)
+    block = -(-(-(-piece // BLOCKS)) // v) * v
+    rounds = -(-clen // piece)
+    return total, clen, piece, block, rounds
 
 
-def block_range(length, c, cs, v, b):
-    clo = min(length, c * cs)
-    chi = min(length, clo + cs)
-    bs = -(-(chi - clo) // BLOCKS)
-    bs = -(-bs // v) * v
-    lo = min(chi, clo + b * bs)
-    return lo, min(chi, lo + bs)
+def piece_len(total, clen, c, kp, piece):
+    start = c * clen
+    cl = 0 if start >= total else min(clen, total - start)
+    return 0 if kp >= cl else min(piece, cl - kp)
 
 
 def touched(lo, hi, v, vec=True):
-    """Element indices CopyRange / the phase-1 loops touch for range [lo, hi) (kernel lines: vlo, vhi, tail)."""
     vlo = lo // v
     vhi = max(vlo, hi // v) if vec else vlo
-    tail_start = max(vhi * v, lo)
-    return [(vlo * v, vhi * v), (tail_start, max(tail_start, hi))]
+    t0 = max(vhi * v, lo)
+    return [(vlo * v, vhi * v), (t0, max(t0, hi))]
 
 
-def check_round(n, length, es, stg_elems, vec):
+def check(kind, n, count, es, vec, root=0):
     v = 16 // es
-    cs = chunk_elems(length, n, v)
-    assert n * cs <= stg_elems
+    total, clen, piece, block, rounds = geometry(kind, n, count, es)
+    in_len = total
+    out_len = count
+    assert n * piece <= STG_BYTES // es
     for me in range(n):
-        p0 = np.zeros(length, np.int32)   # phase 0: elements of chunk c != me written into owner c's slot me
-        p1 = np.zeros(length, np.int32)   # phase 1: elements of chunk me folded
-        p2 = np.zeros(length, np.int32)   # phase 2: elements of chunks c != me copied out
-        for b in range(BLOCKS):
-            for c in range(n):
-                lo, hi = block_range(length, c, cs, v, b)
-                clo = min(length, c * cs)
-                for a0, a1 in touched(lo, hi, v, vec):
-                    if a1 <= a0:
-                        continue
-                    assert lo <= a0 and a1 <= hi, (me, c, b, lo, hi, a0, a1)
-                    if c != me:
-                        slot0, slot1 = me * cs - clo + a0, me * cs - clo + a1  # stgIn[c] + me*cs - clo + e
-                        assert 0 <= slot0 and slot1 <= stg_elems
-                        assert a1 <= stg_elems                                 # stgRes[me][e]
-                        p0[a0:a1] += 1
-                        p2[a0:a1] += 1
-                    else:
-                        for q in range(n):
-                            if q != me:
-                                s0, s1 = q * cs - clo + a0, q * cs - clo + a1  # stgIn[me] + q*cs - clo + e
-                                assert 0 <= s0 and s1 <= stg_elems
-                        p1[a0:a1] += 1
+        cover = {ph: np.zeros(total, np.int32) for ph in (0, 1, 2)}
+        for k in range(rounds):
+            kp = k * piece
+            for b in range(BLOCKS):
+                for c in range(n):
+                    plen = piece_len(total, clen, c, kp, piece)
+                    lo = min(plen, b * block)
+                    hi = min(plen, lo + block)
+                    assert b * block <= lo or lo == hi          # block b's fixed window, whatever the round
+                    for a0, a1 in touched(lo, hi, v, vec):
+                        if a1 <= a0:
+                            continue
+                        assert lo <= a0 and a1 <= hi
+                        g0, g1 = c * clen + kp + a0, c * clen + kp + a1   # input coordinates
+                        assert 0 <= g0 and g1 <= in_len
+                        if c != me:
+                            assert me * piece + a1 <= n * piece          # owner c's slot me
+                            cover[0][g0:g1] += 1
+                            if kind == AR or (kind == RED and me == root):
+                                assert c * piece + a1 <= n * piece       # my result area, chunk c
+                                assert g1 <= out_len
+                                cover[2][g0:g1] += 1
+                        else:
+                            for q in range(n):
+                                assert q * piece + a1 <= n * piece       # my slots
+                            if kind == RS:
+                                assert kp + a1 <= out_len
+                            elif kind == RED and me != root:
+                                assert me * piece + a1 <= n * piece      # root's result area
+                            else:
+                                assert g1 <= out_len
+                            cover[1][g0:g1] += 1
         for c in range(n):
-            clo, chi = min(length, c * cs), min(length, c * cs + cs)
-            want = 1
-            got = (p1 if c == me else p0)[clo:chi]
-            assert np.all(got == want), (me, c)
-            if c != me:
-                assert np.all(p2[clo:chi] == 1)
+            start = c * clen
+            cl = 0 if start >= total else min(clen, total - start)
+            seg = slice(start, start + cl)
+            if c == me:
+                assert np.all(cover[1][seg] == 1), (me, c)
+            else:
+                assert np.all(cover[0][seg] == 1), (me, c)
+                if kind == AR or (kind == RED and me == root):
+                    assert np.all(cover[2][seg] == 1), (me, c)
 
 
-@pytest.mark.parametrize("n", [2, 3, 4, 5, 8, 16])
+@pytest.mark.parametrize("kind", [AR, RS, RED])
+@pytest.mark.parametrize("n", [2, 3, 4, 8, 16])
 @pytest.mark.parametrize("es", [1, 2, 4, 8])
-@pytest.mark.parametrize("count", [1, 5, 7, 33, 4096, 4099, 100003, 1 << 20])
-@pytest.mark.parametrize("vec", [True, False])
-def test_ipc_rounds_in_bounds_and_exact_cover(n, es, count, vec):
-    v = 16 // es
-    unit = n * v
-    round_elems = (STG_BYTES // es) // unit * unit
-    base = 0
-    while base < count:
-        check_round(n, min(round_elems, count - base), es, STG_BYTES // es, vec)
-        base += round_elems
+@pytest.mark.parametrize("count", [1, 5, 7, 33, 4099, 100003])
+def test_ipc_in_bounds_and_exact_cover(kind, n, es, count):
+    check(kind, n, count, es, vec=True, root=n - 1)
+    check(kind, n, count, es, vec=False, root=0)
 
 
-@pytest.mark.parametrize("n", [2, 4, 8])
-def test_ipc_full_round_fills_staging(n):
-    """A full round uses exactly the slot area: n chunks of roundElems / n."""
-    es = 4
-    v = 16 // es
-    unit = n * v
-    round_elems = (STG_BYTES // es) // unit * unit
-    assert n * chunk_elems(round_elems, n, v) == round_elems <= STG_BYTES // es
+@pytest.mark.parametrize("kind,n,count", [(AR, 2, (36 << 20) + 11), (RS, 4, (9 << 20) + 3), (RED, 4, (36 << 20) + 7)])
+def test_ipc_multi_round_geometry(kind, n, count):
+    """Counts that need several pieces per chunk (fp32): still in bounds, exact cover, fixed block windows."""
+    total, clen, piece, block, rounds = geometry(kind, n, count, 4)
+    assert rounds >= 2
+    check(kind, n, count, 4, vec=True, root=1)
+
+
+def test_old_element_loop_start_is_caught():
+    """The pre-fix element loop (from vhi*V) touches an element outside an empty window: the model rejects it."""
+    lo = hi = 5
+    v = 4
+    vhi = hi // v
+    bad = (vhi * v, hi)
+    assert bad[0] < lo  # would write element 4 for the empty window [5, 5)
+    assert touched(lo, hi, v)[1][0] >= lo
