@@ -17,11 +17,12 @@ Comm* AsComm(HcclComm c)
     return p;
 }
 
-uint64_t ScratchBytesDefault()
+uint64_t CclBytesDefault()
 {
-    // HCCL_BUFFSIZE is in MB, as in HCCL; the default is sized for 288 GB HBM (reference: 200 MB).
+    // HCCL_BUFFSIZE in MB, default 200 (docs/zh/user_guide/hccl_env/HCCL_BUFFSIZE.md; the reference simulator's CCL
+    // buffer, sim_npu.cc:47). It sizes the executor loops, and so the slicing of the ownership-dependent orders.
     const char* e = std::getenv("HCCL_BUFFSIZE");
-    uint64_t mb = 256;
+    uint64_t mb = 200;
     if (e != nullptr && e[0] != '\0') {
         char* end = nullptr;
         unsigned long long v = std::strtoull(e, &end, 10);
@@ -29,6 +30,9 @@ uint64_t ScratchBytesDefault()
     }
     return mb << 20;
 }
+
+// Every communicator holds 2 x HCCL_BUFFSIZE (HCCL_BUFFSIZE.md: "2*HCCL_BUFFSIZE", send and receive halves).
+uint64_t ScratchBytesDefault() { return 2 * CclBytesDefault(); }
 
 uint64_t SingleStreamBytes()
 {
@@ -51,7 +55,8 @@ HcclResult Comm::Init(int dev)
     HIP_CHK(hipStreamCreateWithPriority(&commStream, hipStreamNonBlocking, hi));
     HIP_CHK(hipStreamCreateWithPriority(&reduceStream, hipStreamNonBlocking, lo));
     if (nRanks > 1) {
-        scratchBytes = ScratchBytesDefault();
+        cclBytes = CclBytesDefault();
+        scratchBytes = 2 * cclBytes;
         HIP_CHK(hipMalloc(&scratch, scratchBytes));
     }
     return HCCL_SUCCESS;

@@ -55,7 +55,8 @@ struct Comm {
     hipStream_t commStream = nullptr;
     hipStream_t reduceStream = nullptr;
     void* scratch = nullptr;
-    uint64_t scratchBytes = 0;
+    uint64_t cclBytes = 0;      // HCCL_BUFFSIZE: sizes the executor loops (ScheduleParams::cclBytes)
+    uint64_t scratchBytes = 0;  // 2 x cclBytes
     int32_t algoOverride = HCCL_AMD_ALGO_AUTO;
     uint64_t pieceBytes = 0;
     int32_t lastAlgo = -1;
@@ -83,8 +84,9 @@ void IpcRelease(Comm& c);
 
 Comm* AsComm(HcclComm c);
 
-// Staging bytes per communicator: HCCL_BUFFSIZE (MB) if set, else 256 MB. Must be equal on every rank: the
-// pipelining granule is derived from it.
+// HCCL_BUFFSIZE (MB, default 200) in bytes; staging per communicator is twice that. Must be equal on every rank: the
+// executor loops and the pipelining granule are derived from it.
+uint64_t CclBytesDefault();
 uint64_t ScratchBytesDefault();
 
 // Runs one rank's schedule. bufs = {sendBuf, recvBuf, scratch}. Stream-ordered after `user`; `user` waits for the

@@ -174,35 +174,65 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, const void* sendBuf, void* 
     a.n = n;
     a.kind = kind;
     a.root = root;
-    if (kind == kIpcReduceScatter) {
-        // block c of the input (recvCount elements) is chunk c (reduce_scatter_op.cc:158-159)
-        a.total = uint64_t(n) * count;
-        a.chunkStride = a.chunkLen = count;
-    } else {
-        // ceil(count / n) rounded up to HCCL_MIN_SLICE_ALIGN = 128 B (alg_template_base.h:34), as the RCCL path and
-        // the reference's two-shot templates slice: the Reduce order (chunk owner first) depends on these bounds
-        const uint64_t align = 128 / es;
-        const uint64_t cs = ((count + n - 1) / n + align - 1) / align * align;
-        a.total = count;
-        a.chunkStride = a.chunkLen = cs;
-    }
-    const uint64_t slotCap = (s.stgInBytes / es / n) / V * V;
-    a.piece = std::min(slotCap, (a.chunkLen + V - 1) / V * V);
-    a.blockElems = ((a.piece + s.blocks - 1) / s.blocks + V - 1) / V * V;
-    a.rounds = static_cast<uint32_t>((a.chunkLen + a.piece - 1) / a.piece);
     a.timeoutTicks = IpcTimeoutTicks();  // a lost peer ends the kernel with status bit 0, never a hang
     a.status = s.status;
-    a.epochBase = s.epoch;
-    s.epoch += 2 * a.rounds;
-    const bool strideAligned = (a.chunkStride * es) % 16 == 0;
+    const uint64_t slotCap = (s.stgInBytes / es / n) / V * V;
+
+    // One launch per executor loop [off, off + cnt) with the geometry the reference's template uses for it.
+    struct Launch {
+        uint64_t off, cnt;
+    };
+    std::vector<Launch> launches;
+    if (kind == kIpcReduce) {
+        // ReduceSoleExecutor loops (reduce_sole_executor.cc:120-170): min(UB_MAX_DATA_SIZE, ccl / n) rounded down to
+        // 128 B, each sliced by ReduceMesh1DTwoShot::CalcSlice on its own
+        const uint64_t loopBytes = std::min<uint64_t>(256ull << 20, c.cclBytes / n / 128 * 128);
+        const uint64_t per = std::max<uint64_t>(1, loopBytes / es);
+        for (uint64_t off = 0; off < count; off += per) launches.push_back({off, std::min(per, count - off)});
+    } else {
+        launches.push_back({0, count});
+    }
+    auto geometry = [&](IpcArgs& g, uint64_t cnt) {
+        if (kind == kIpcReduceScatter) {
+            // block c of the input (recvCount elements) is chunk c (reduce_scatter_op.cc:158-159)
+            g.balanced = false;
+            g.total = uint64_t(n) * cnt;
+            g.chunkStride = g.chunkLen = cnt;
+            g.rem = 0;
+        } else if (kind == kIpcReduce) {
+            g.balanced = true;  // reduce_mesh_1D_two_shot.cc:108-131
+            g.total = cnt;
+            g.chunkLen = cnt / n;
+            g.rem = cnt % n;
+            g.chunkStride = 0;
+        } else {
+            // ceil(count / n) rounded up to HCCL_MIN_SLICE_ALIGN = 128 B (order O2 does not depend on it)
+            const uint64_t align = 128 / es;
+            g.balanced = false;
+            g.total = cnt;
+            g.chunkStride = g.chunkLen = ((cnt + n - 1) / n + align - 1) / align * align;
+            g.rem = 0;
+        }
+        const uint64_t widest = g.chunkLen + (g.rem != 0 ? 1 : 0);
+        g.piece = std::max<uint64_t>(V, std::min(slotCap, (widest + V - 1) / V * V));
+        g.blockElems = ((g.piece + s.blocks - 1) / s.blocks + V - 1) / V * V;
+        g.rounds = static_cast<uint32_t>((widest + g.piece - 1) / g.piece);
+        g.epochBase = s.epoch;
+        s.epoch += 2 * g.rounds;
+    };
+    auto at = [es](const void* p, uint64_t off) { return static_cast<char*>(const_cast<void*>(p)) + off * es; };
 
     if (!c.transport->SharedDevice()) {
         a.me = static_cast<int32_t>(c.rank);
-        a.in[c.rank] = sendBuf;
-        a.out[c.rank] = recvBuf;
-        a.aligned = strideAligned && Aligned16(sendBuf, recvBuf);
+        a.aligned = Aligned16(sendBuf, recvBuf);
         HIP_CHK(hipMemsetAsync(s.status + 1, 0, sizeof(uint32_t), stream));  // wait diagnostic of this call
-        return LaunchIpcCollective(a, s.blocks, 0, dt, op, stream);
+        for (const Launch& l : launches) {
+            a.in[c.rank] = at(sendBuf, l.off);
+            a.out[c.rank] = at(recvBuf, kind == kIpcReduceScatter ? 0 : l.off);
+            geometry(a, l.cnt);
+            HCCL_CHK(LaunchIpcCollective(a, s.blocks, 0, dt, op, stream));
+        }
+        return HCCL_SUCCESS;
     }
 
     // loopback world: one launch for every rank, issued by rank 0 behind every rank's stream
@@ -220,15 +250,20 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, const void* sendBuf, void* 
     hipEvent_t done = nullptr;
     if (c.rank == 0) {
         a.me = -1;
-        a.aligned = strideAligned;
+        a.aligned = true;
         for (uint32_t r = 0; r < n; ++r) {
-            a.in[r] = all[r].in;
-            a.out[r] = all[r].out;
             a.aligned = a.aligned && Aligned16(all[r].in, all[r].out);
             HIP_CHK(hipStreamWaitEvent(stream, all[r].ready, 0));
         }
         HIP_CHK(hipMemsetAsync(s.status + 1, 0, sizeof(uint32_t), stream));
-        HCCL_CHK(LaunchIpcCollective(a, s.blocks, n, dt, op, stream));
+        for (const Launch& l : launches) {
+            for (uint32_t r = 0; r < n; ++r) {
+                a.in[r] = at(all[r].in, l.off);
+                a.out[r] = at(all[r].out, kind == kIpcReduceScatter ? 0 : l.off);
+            }
+            geometry(a, l.cnt);
+            HCCL_CHK(LaunchIpcCollective(a, s.blocks, n, dt, op, stream));
+        }
         HCCL_CHK(c.NextEvent(&done));
         HIP_CHK(hipEventRecord(done, stream));
     }

@@ -22,7 +22,8 @@ enum IpcKind : uint32_t {
 // full and blockIdx.y is the rank.
 //
 // Geometry (elements): chunk c of the input starts at c * chunkStride and holds min(chunkLen, total - c*chunkStride)
-// elements (clamped at 0); rank c owns chunk c. Round k handles piece k of every chunk: chunk elements
+// elements (clamped at 0), or, balanced (the two-shot Reduce's split), starts at c*chunkLen + min(c, rem) and holds
+// chunkLen + (c < rem); rank c owns chunk c. Round k handles piece k of every chunk: chunk elements
 // [k*piece, (k+1)*piece). Block b always handles piece coordinates [b*blockElems, (b+1)*blockElems), so every round
 // of a launch touches the same slot and result addresses per block and the per-block barrier is sound.
 // Staging: owner c's slot q = stgIn[c] + q*piece; results of chunk c at stgRes[p] + c*piece.
@@ -39,13 +40,15 @@ struct IpcArgs {
     uint64_t total;
     uint64_t chunkStride;
     uint64_t chunkLen;
+    uint64_t rem;   // balanced: chunk c starts at c*chunkLen + min(c, rem) and holds chunkLen + (c < rem) elements
+    bool balanced;
     uint64_t piece;
     uint64_t blockElems;
     uint32_t rounds;
     uint32_t epochBase;
     uint64_t timeoutTicks;  // per barrier wait, in s_memrealtime ticks (100 MHz)
     uint32_t* status;  // [0] bit 0: a barrier timed out (sticky per communicator); [1]: longest wait, in polls
-    bool aligned;      // every in[] / out[] and chunk start the launch touches is 16-B aligned (else element-wise)
+    bool aligned;      // every in[] / out[] is 16-B aligned (chunks whose start is not are still element-wise)
 };
 
 HcclResult LaunchIpcCollective(const IpcArgs& a, uint32_t blocks, uint32_t worldRanks, HcclDataType dt,

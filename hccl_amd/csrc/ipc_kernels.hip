@@ -81,11 +81,29 @@ struct Range {
     uint64_t lo, hi;  // piece coordinates
 };
 
+__device__ __forceinline__ uint64_t ChunkStart(const IpcArgs& a, uint32_t c)
+{
+    return a.balanced ? uint64_t(c) * a.chunkLen + min(uint64_t(c), a.rem) : uint64_t(c) * a.chunkStride;
+}
+
+__device__ __forceinline__ uint64_t ChunkElems(const IpcArgs& a, uint32_t c)
+{
+    if (a.balanced) return a.chunkLen + (c < a.rem ? 1 : 0);
+    const uint64_t start = uint64_t(c) * a.chunkStride;
+    return start >= a.total ? 0 : min(a.chunkLen, a.total - start);
+}
+
+// 16-B vectors for chunk c: the user buffers are aligned and so is the chunk's first element
+template <typename S>
+__device__ __forceinline__ bool ChunkVec(const IpcArgs& a, uint32_t c)
+{
+    return a.aligned && ChunkStart(a, c) % (16 / sizeof(S)) == 0;
+}
+
 // Elements of chunk c in round k (piece coordinates [0, len)), and the block's fixed window clipped to it.
 __device__ __forceinline__ uint64_t PieceLen(const IpcArgs& a, uint32_t c, uint64_t kP)
 {
-    const uint64_t start = uint64_t(c) * a.chunkStride;
-    const uint64_t clen = start >= a.total ? 0 : min(a.chunkLen, a.total - start);
+    const uint64_t clen = ChunkElems(a, c);
     return kP >= clen ? 0 : min(a.piece, clen - kP);
 }
 
@@ -122,7 +140,7 @@ __device__ __forceinline__ void CopyRange(S* dst, const S* src, Range r, bool ve
 //   reduce-scatter / reduce (O1): operand 0 = rank me (the owner), then the others ascending
 template <class E, int OP, class Dst>
 __device__ __forceinline__ void FoldRange(const IpcArgs& a, uint32_t me, const typename E::S* own,
-                                          const typename E::S* slots, Dst dsts, uint32_t ndst, Range r)
+                                          const typename E::S* slots, Dst dsts, uint32_t ndst, Range r, bool vec)
 {
     using S = typename E::S;
     constexpr uint64_t V = 16 / sizeof(S);
@@ -132,7 +150,7 @@ __device__ __forceinline__ void FoldRange(const IpcArgs& a, uint32_t me, const t
         const uint32_t q = o2 ? i : (i == 0 ? me : (i <= me ? i - 1 : i));
         return q == me ? own : slots + uint64_t(q) * a.piece;
     };
-    const uint64_t vlo = r.lo / V, vhi = a.aligned ? max(vlo, r.hi / V) : vlo;
+    const uint64_t vlo = r.lo / V, vhi = vec ? max(vlo, r.hi / V) : vlo;
     uint64_t v = vlo + threadIdx.x;
     for (; v + (kIpcU - 1) * kIpcBlock < vhi; v += kIpcU * kIpcBlock) {
         u32x4 acc[kIpcU];
@@ -180,26 +198,26 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
             if (c == me) continue;
             const Range r = BlockWindow(a, PieceLen(a, c, kP));
             S* slot = static_cast<S*>(a.stgIn[c]) + uint64_t(me) * a.piece;
-            CopyRange<S>(slot, in + uint64_t(c) * a.chunkStride + kP, r, a.aligned);
+            CopyRange<S>(slot, in + ChunkStart(a, c) + kP, r, ChunkVec<S>(a, c));
         }
         if (!Barrier(a, me, ++epoch)) return;
         // phase 1: fold my chunk's piece over the slots (my own operand straight from my input)
         {
             const Range r = BlockWindow(a, PieceLen(a, me, kP));
-            const S* own = in + uint64_t(me) * a.chunkStride + kP;
+            const S* own = in + ChunkStart(a, me) + kP;
             const S* slots = static_cast<const S*>(a.stgIn[me]);
             // destination 0: my output (or, for a non-root Reduce rank, the root's result area); all-reduce also
             // pushes to every peer's result area (destinations 1 .. n-1 = the peers in ascending order)
             S* first = a.kind == kIpcReduceScatter ? out + kP
                      : (a.kind == kIpcReduce && me != a.root)
                          ? static_cast<S*>(a.stgRes[a.root]) + uint64_t(me) * a.piece
-                         : out + uint64_t(me) * a.chunkStride + kP;
+                         : out + ChunkStart(a, me) + kP;
             auto dst = [&](uint32_t d) {
                 if (d == 0) return first;
                 const uint32_t p = d - 1 < me ? d - 1 : d;
                 return static_cast<S*>(a.stgRes[p]) + uint64_t(me) * a.piece;
             };
-            FoldRange<E, OP>(a, me, own, slots, dst, a.kind == kIpcAllReduce ? n : 1u, r);
+            FoldRange<E, OP>(a, me, own, slots, dst, a.kind == kIpcAllReduce ? n : 1u, r, ChunkVec<S>(a, me));
         }
         if (!Barrier(a, me, ++epoch)) return;
         // phase 2: the other chunks' results from my own result area (all-reduce: every rank; reduce: the root)
@@ -207,8 +225,8 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
             for (uint32_t c = 0; c < n; ++c) {
                 if (c == me) continue;
                 const Range r = BlockWindow(a, PieceLen(a, c, kP));
-                CopyRange<S>(out + uint64_t(c) * a.chunkStride + kP,
-                             static_cast<const S*>(a.stgRes[me]) + uint64_t(c) * a.piece, r, a.aligned);
+                CopyRange<S>(out + ChunkStart(a, c) + kP,
+                             static_cast<const S*>(a.stgRes[me]) + uint64_t(c) * a.piece, r, ChunkVec<S>(a, c));
             }
         }
     }

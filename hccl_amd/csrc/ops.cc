@@ -95,6 +95,7 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     p.root = root;
     p.pieceBytes = c.pieceBytes;
     p.scratchCapBytes = c.scratchBytes;
+    p.cclBytes = c.cclBytes;
     Schedule s;
     HcclResult r = static_cast<HcclResult>(BuildSchedule(p, &s));
     if (r != HCCL_SUCCESS) return r;
@@ -315,6 +316,7 @@ HcclResult HcclAmdBuildSchedule(int32_t opType, int32_t algo, uint32_t nRanks, u
     p.root = root;
     p.pieceBytes = pieceBytes;
     p.scratchCapBytes = ScratchBytesDefault();
+    p.cclBytes = CclBytesDefault();
     Schedule s;
     HcclResult r = static_cast<HcclResult>(BuildSchedule(p, &s));
     if (r != HCCL_SUCCESS) return r;

@@ -36,6 +36,9 @@ public:
     std::vector<HcclAmdIrOp> ops;
     uint64_t scratchHigh = 0;
     int32_t group = 0;
+    // Element offset added to every INPUT / OUTPUT reference: a generator written for [0, count) then runs one
+    // executor loop [ioBase, ioBase + count) of the reference's OrchestrateLoop.
+    uint64_t ioBase = 0;
 
     void Copy(Ref dst, Ref src, uint64_t count)
     {
@@ -90,16 +93,17 @@ private:
     {
         if (r.buf == HCCL_AMD_BUF_SCRATCH) scratchHigh = std::max(scratchHigh, r.off + count);
     }
+    uint64_t Base(Ref r) const { return r.buf == HCCL_AMD_BUF_SCRATCH ? r.off : r.off + ioBase; }
     void SetDst(HcclAmdIrOp& o, Ref r, uint64_t count)
     {
         o.dstBuf = r.buf;
-        o.dstOff = r.off;
+        o.dstOff = Base(r);
         Track(r, count);
     }
     void AddSrc(HcclAmdIrOp& o, Ref r, uint64_t count)
     {
         o.srcBuf[o.nsrc] = r.buf;
-        o.srcOff[o.nsrc] = r.off;
+        o.srcOff[o.nsrc] = Base(r);
         o.nsrc++;
         Track(r, count);
     }
@@ -123,6 +127,57 @@ Span Chunk(uint64_t count, uint32_t n, uint32_t c, uint64_t alignElems)
     uint64_t b = std::min<uint64_t>(count, uint64_t(c) * sc);
     uint64_t e = std::min<uint64_t>(count, b + sc);
     return {b, e - b};
+}
+
+// The reference's executor loop (InsV2AllReduceSoleExecutor::OrchestrateLoop,
+// ins_v2_all_reduce_sole_executor.cc:160-208; ReduceSoleExecutor, reduce_sole_executor.cc:120-170): at most
+// min(transportBound, ccl / scratchMultiple rounded down to 128 B) bytes per loop, and the template slices each loop's
+// data on its own. Orders that depend on which rank owns an element (NHR, Reduce two-shot) therefore follow these
+// loops. ccl = HCCL_BUFFSIZE (the reference's simulator and default: 200 MB).
+constexpr uint64_t kUbMaxDataSize = 256ull << 20;  // UB_MAX_DATA_SIZE, alg_param.h:37
+
+uint64_t RefLoopElems(const ScheduleParams& p, uint64_t transportBoundBytes, uint64_t scratchMultiple)
+{
+    const uint64_t ccl = p.cclBytes;
+    uint64_t bytes = transportBoundBytes;
+    if (scratchMultiple != 0) bytes = std::min(bytes, ccl / scratchMultiple / kAlignBytes * kAlignBytes);
+    return std::max<uint64_t>(1, bytes / p.elemSize);
+}
+
+// Runs gen(loopParams) once per executor loop, with the builder's I/O base at the loop's first element.
+template <class Gen>
+void ForEachRefLoop(const ScheduleParams& p, Builder& b, uint64_t loopElems, Gen gen)
+{
+    for (uint64_t off = 0; off < p.count; off += loopElems) {
+        ScheduleParams lp = p;
+        lp.count = std::min(loopElems, p.count - off);
+        b.ioBase = off;
+        gen(lp);
+    }
+    b.ioBase = 0;
+}
+
+// ReduceMesh1DTwoShot::CalcSlice (reduce_mesh_1D_two_shot.cc:108-131): the first count % n ranks get one element more.
+Span BalancedSlice(uint64_t count, uint32_t n, uint32_t c)
+{
+    const uint64_t base = count / n, rem = count % n;
+    return {uint64_t(c) * base + std::min<uint64_t>(c, rem), base + (c < rem ? 1 : 0)};
+}
+
+// ReduceNHR::CalcSlice (reduce_nhr.cc:114-138): chunk = RoundUpWithDivisor(bytes, n * elemSize) / n, i.e.
+// ceil(count / n) elements; trailing slices short or empty.
+Span CeilSlice(uint64_t count, uint32_t n, uint32_t c)
+{
+    const uint64_t cs = CeilDiv(count, n);
+    const uint64_t b = std::min<uint64_t>(count, uint64_t(c) * cs);
+    return {b, std::min<uint64_t>(count, b + cs) - b};
+}
+
+// InsTempAllReduceNHR::KernelRun (ins_temp_all_reduce_nhr.cc:171-173): floor(count / n), the tail on the last slice.
+Span FloorSlice(uint64_t count, uint32_t n, uint32_t c)
+{
+    const uint64_t se = count / n;
+    return c == n - 1 ? Span{uint64_t(c) * se, count - se * (n - 1)} : Span{uint64_t(c) * se, se};
 }
 
 // Piece p of a span cut into pieces of pe elements (the last may be short, those past the end are empty).
@@ -376,14 +431,10 @@ std::vector<NhrStep> NhrSteps(uint32_t n, uint32_t me, bool gather)
     return out;
 }
 
-void AllReduceNhr(const ScheduleParams& p, Builder& b)
+void AllReduceNhrLoop(const ScheduleParams& p, Builder& b)
 {
     const uint32_t n = p.nRanks, me = p.rank;
-    const uint64_t sliceElems = p.count / n;
-    auto slice = [&](uint32_t i) {
-        return i == n - 1 ? Span{uint64_t(i) * sliceElems, p.count - sliceElems * (n - 1)}
-                          : Span{uint64_t(i) * sliceElems, sliceElems};
-    };
+    auto slice = [&](uint32_t i) { return FloorSlice(p.count, n, i); };
     const uint64_t kSlots = 2;
     const uint64_t maxSlices = (n + 1) / 2;
     const uint64_t tail = slice(n - 1).len;
@@ -420,6 +471,48 @@ void AllReduceNhr(const ScheduleParams& p, Builder& b)
             }
             b.EndGroup();
         }
+    }
+}
+
+void AllReduceNhr(const ScheduleParams& p, Builder& b)
+{
+    ForEachRefLoop(p, b, RefLoopElems(p, p.cclBytes, 1), [&](const ScheduleParams& lp) { AllReduceNhrLoop(lp, b); });
+}
+
+// NHR ReduceScatter (ins_temp_reduce_scatter_nhr.cc:104-197, 278-397, 407-456): the NHR reduce-scatter steps with the
+// ReduceScatter blocks as slices (block i = slice i, whatever the executor loop, so the order does not depend on the
+// loop size), write-reduce receiver partial (dst) (op) sender partial (src), then block `me` to recvBuf. Blocks are
+// processed in columns of W elements: n working columns in the first ccl bytes of staging, receive slots after them.
+void ReduceScatterNhr(const ScheduleParams& p, Builder& b)
+{
+    const uint32_t n = p.nRanks, me = p.rank;
+    const uint64_t rc = p.count;
+    const uint64_t alignElems = std::max<uint64_t>(1, kAlignBytes / p.elemSize);
+    const uint64_t W = std::min(rc, std::max(alignElems, p.cclBytes / n / p.elemSize / alignElems * alignElems));
+    const uint64_t kSlots = 2;
+    const uint64_t maxSlices = (n + 1) / 2;
+    for (uint64_t col = 0; col < rc; col += W) {
+        const uint64_t w = std::min(W, rc - col);
+        auto work = [&](uint32_t i, uint64_t off) { return Scr(uint64_t(i) * W + off); };
+        ScheduleParams pp = p;
+        if (pp.scratchCapBytes != 0) pp.scratchCapBytes -= std::min(pp.scratchCapBytes, n * W * p.elemSize);
+        const uint64_t pe = PieceElems(pp, w, kSlots * maxSlices);
+        const uint64_t np = std::max<uint64_t>(1, CeilDiv(w, pe));
+        auto slot = [&](uint64_t unit, size_t i) { return Scr(n * W + ((unit % kSlots) * maxSlices + i) * pe); };
+        for (uint32_t i = 0; i < n; ++i) b.Copy(work(i, 0), In(uint64_t(i) * rc + col), w);  // LocalDataCopy
+        uint64_t unit = 0;
+        for (const NhrStep& st : NhrSteps(n, me, false)) {
+            for (uint64_t t = 0; t < np; ++t, ++unit) {
+                const Span s = Piece({0, w}, pe, t);
+                for (size_t i = 0; i < st.tx.size(); ++i) b.Send(st.to, work(st.tx[i], s.begin), s.len);
+                for (size_t i = 0; i < st.rx.size(); ++i) b.Recv(st.from, slot(unit, i), s.len);
+                b.EndGroup();
+                for (size_t i = 0; i < st.rx.size(); ++i) {
+                    b.Reduce(work(st.rx[i], s.begin), {work(st.rx[i], s.begin), slot(unit, i)}, s.len);
+                }
+            }
+        }
+        b.Copy(Out(col), work(me, 0), w);  // PostLocalCopy
     }
 }
 
@@ -596,14 +689,14 @@ void ReduceOneShot(const ScheduleParams& p, Builder& b)
 }
 
 // Two-shot: mesh reduce-scatter with O1 per chunk owner (reduce_mesh_1D_two_shot.cc:209-249), then the owners send
-// their reduced chunks to the root. Non-roots fold into a staging slot, so their recvBuf is not touched.
-void ReduceTwoShot(const ScheduleParams& p, Builder& b)
+// their reduced chunks to the root. Non-roots fold into a staging slot, so their recvBuf is not touched. Slices are
+// the template's balanced split of each executor loop (scratch multiple n, transport bound UB_MAX_DATA_SIZE).
+void ReduceTwoShotLoop(const ScheduleParams& p, Builder& b)
 {
     const uint32_t n = p.nRanks, me = p.rank, root = p.root;
-    const uint64_t alignElems = std::max<uint64_t>(1, kAlignBytes / p.elemSize);
     const uint64_t kSlots = 2;
-    const Span mine = Chunk(p.count, n, me, alignElems);
-    const uint64_t maxChunk = Chunk(p.count, n, 0, alignElems).len;
+    const Span mine = BalancedSlice(p.count, n, me);
+    const uint64_t maxChunk = BalancedSlice(p.count, n, 0).len;
     // slots: kSlots x (n-1) receive pieces + kSlots reduced pieces (non-root)
     const uint64_t pe = PieceElems(p, maxChunk, kSlots * n);
     const uint64_t np = std::max<uint64_t>(1, CeilDiv(maxChunk, pe));
@@ -613,7 +706,7 @@ void ReduceTwoShot(const ScheduleParams& p, Builder& b)
         if (t < np) {
             Span rs = Piece(mine, pe, t);
             for (uint32_t q : PeerOrder(n, me)) {
-                Span out = Piece(Chunk(p.count, n, q, alignElems), pe, t);
+                Span out = Piece(BalancedSlice(p.count, n, q), pe, t);
                 b.Send(q, In(out.begin), out.len);
                 b.Recv(q, slot(t, q), rs.len);
             }
@@ -622,7 +715,7 @@ void ReduceTwoShot(const ScheduleParams& p, Builder& b)
             uint64_t g = t - 2;
             if (me == root) {
                 for (uint32_t q : PeerOrder(n, me)) {
-                    Span theirs = Piece(Chunk(p.count, n, q, alignElems), pe, g);
+                    Span theirs = Piece(BalancedSlice(p.count, n, q), pe, g);
                     b.Recv(q, Out(theirs.begin), theirs.len);
                 }
             } else {
@@ -639,6 +732,69 @@ void ReduceTwoShot(const ScheduleParams& p, Builder& b)
             b.Reduce(me == root ? Out(rs.begin) : red(t), srcs, rs.len);
         }
     }
+}
+
+void ReduceTwoShot(const ScheduleParams& p, Builder& b)
+{
+    ForEachRefLoop(p, b, RefLoopElems(p, kUbMaxDataSize, p.nRanks),
+                   [&](const ScheduleParams& lp) { ReduceTwoShotLoop(lp, b); });
+}
+
+// NHR Reduce (reduce_nhr.cc:56-106, 164-267, 294-368): the NHR reduce-scatter and all-gather steps over ceil-sized
+// slices of each executor loop (scratch multiple 1, transport bound UB_MAX_DATA_SIZE); only the root keeps the result
+// (PostCopy :269-292). The working buffer is recvBuf on the root and staging elsewhere (a non-root recvBuf is never
+// written); receive slots follow it in staging.
+void ReduceNhrLoop(const ScheduleParams& p, Builder& b)
+{
+    const uint32_t n = p.nRanks, me = p.rank;
+    const bool isRoot = me == p.root;
+    auto slice = [&](uint32_t i) { return CeilSlice(p.count, n, i); };
+    // every rank reserves the working area in its staging (the root does not use it), so that all ranks cut the
+    // same pieces
+    const uint64_t workElems = AlignUp(p.count, std::max<uint64_t>(1, kAlignBytes / p.elemSize));
+    auto work = [&](uint64_t off) { return isRoot ? Out(off) : Scr(off); };
+    const uint64_t kSlots = 2;
+    const uint64_t maxSlices = (n + 1) / 2;
+    const uint64_t widest = slice(0).len;
+    ScheduleParams pp = p;
+    if (pp.scratchCapBytes != 0) pp.scratchCapBytes -= std::min(pp.scratchCapBytes, workElems * p.elemSize);
+    const uint64_t pe = PieceElems(pp, widest, kSlots * maxSlices);
+    const uint64_t np = std::max<uint64_t>(1, CeilDiv(widest, pe));
+    auto slot = [&](uint64_t unit, size_t i) { return Scr(workElems + ((unit % kSlots) * maxSlices + i) * pe); };
+    b.Copy(work(0), In(0), p.count);  // PreCopy (reduce_nhr.cc:140-162)
+    uint64_t unit = 0;
+    for (const NhrStep& st : NhrSteps(n, me, false)) {
+        for (uint64_t t = 0; t < np; ++t, ++unit) {
+            for (size_t i = 0; i < st.tx.size(); ++i) {
+                Span s = Piece(slice(st.tx[i]), pe, t);
+                b.Send(st.to, work(s.begin), s.len);
+            }
+            for (size_t i = 0; i < st.rx.size(); ++i) b.Recv(st.from, slot(unit, i), Piece(slice(st.rx[i]), pe, t).len);
+            b.EndGroup();
+            for (size_t i = 0; i < st.rx.size(); ++i) {
+                Span s = Piece(slice(st.rx[i]), pe, t);
+                b.Reduce(work(s.begin), {work(s.begin), slot(unit, i)}, s.len);
+            }
+        }
+    }
+    for (const NhrStep& st : NhrSteps(n, me, true)) {
+        for (uint64_t t = 0; t < np; ++t) {
+            for (size_t i = 0; i < st.tx.size(); ++i) {
+                Span s = Piece(slice(st.tx[i]), pe, t);
+                b.Send(st.to, work(s.begin), s.len);
+            }
+            for (size_t i = 0; i < st.rx.size(); ++i) {
+                Span s = Piece(slice(st.rx[i]), pe, t);
+                b.Recv(st.from, work(s.begin), s.len);
+            }
+            b.EndGroup();
+        }
+    }
+}
+
+void ReduceNhr(const ScheduleParams& p, Builder& b)
+{
+    ForEachRefLoop(p, b, RefLoopElems(p, kUbMaxDataSize, 1), [&](const ScheduleParams& lp) { ReduceNhrLoop(lp, b); });
 }
 
 // ------------------------------------------------------------------------------------------- AllGather
@@ -710,8 +866,8 @@ int BuildSchedule(const ScheduleParams& p, Schedule* out)
     int32_t algo = p.algo;
     uint64_t bytes = p.count * p.elemSize;
     if (algo == HCCL_AMD_ALGO_AUTO) algo = SelectAlgo(p.opType, p.nRanks, bytes);
-    // The one-sided IPC AllReduce runs as one kernel, not as IR; its IR twin (same order O2, same bits) is the
-    // two-shot, which is also what runs when the IPC path cannot (unaligned buffers).
+    // The one-sided IPC collectives run as one kernel per executor loop, not as IR; their IR twins (same orders, same
+    // bits) are the two-shot AllReduce / Reduce and the mesh ReduceScatter, which also run when the IPC path cannot.
     if (algo == HCCL_AMD_ALGO_IPC_TWOSHOT) algo = HCCL_AMD_ALGO_MESH_TWOSHOT;
     if (p.nRanks == 1) {
         // SingleRankProc (op_common.cc:3042-3098): a copy when the buffers differ.
@@ -735,24 +891,23 @@ int BuildSchedule(const ScheduleParams& p, Schedule* out)
             }
             break;
         case HCCL_AMD_OP_REDUCE_SCATTER:
-            if (algo == HCCL_AMD_ALGO_MESH_TWOSHOT || algo == HCCL_AMD_ALGO_RHD || algo == HCCL_AMD_ALGO_NHR) {
-                algo = HCCL_AMD_ALGO_MESH_ONESHOT;
-            }
+            if (algo == HCCL_AMD_ALGO_MESH_TWOSHOT || algo == HCCL_AMD_ALGO_RHD) algo = HCCL_AMD_ALGO_MESH_ONESHOT;
             switch (algo) {
                 case HCCL_AMD_ALGO_MESH_ONESHOT: ReduceScatterMesh(p, b); break;
+                case HCCL_AMD_ALGO_NHR: ReduceScatterNhr(p, b); break;
                 case HCCL_AMD_ALGO_RING: ReduceScatterRing(p, b); break;
                 case HCCL_AMD_ALGO_ORDER_PRESERVED: ReduceScatterTree(p, b); break;
                 default: return HCCL_E_PARA;
             }
             break;
         case HCCL_AMD_OP_REDUCE:
-            if (algo == HCCL_AMD_ALGO_RING || algo == HCCL_AMD_ALGO_RHD || algo == HCCL_AMD_ALGO_NHR ||
-                algo == HCCL_AMD_ALGO_ORDER_PRESERVED) {
+            if (algo == HCCL_AMD_ALGO_RING || algo == HCCL_AMD_ALGO_RHD || algo == HCCL_AMD_ALGO_ORDER_PRESERVED) {
                 algo = HCCL_AMD_ALGO_MESH_TWOSHOT;
             }
             switch (algo) {
                 case HCCL_AMD_ALGO_MESH_ONESHOT: ReduceOneShot(p, b); break;
                 case HCCL_AMD_ALGO_MESH_TWOSHOT: ReduceTwoShot(p, b); break;
+                case HCCL_AMD_ALGO_NHR: ReduceNhr(p, b); break;
                 default: return HCCL_E_PARA;
             }
             break;

@@ -23,6 +23,7 @@ struct ScheduleParams {
     uint32_t root = 0;
     uint64_t pieceBytes = 0;        // 0 = default
     uint64_t scratchCapBytes = 0;   // 0 = unbounded
+    uint64_t cclBytes = 200ull << 20;  // HCCL_BUFFSIZE: sizes the reference's executor loops (see RefLoopElems)
 };
 
 struct Schedule {

@@ -16,6 +16,53 @@ from oracle import oracle as O
 ALIGN = 128
 
 
+UB_MAX_DATA_SIZE = 256 << 20  # alg_param.h:37
+
+
+def ccl_bytes_from_env():
+    """HCCL_BUFFSIZE in MB (default 200), as the library reads it."""
+    import os
+    v = os.environ.get("HCCL_BUFFSIZE", "")
+    try:
+        mb = int(v) if v else 200
+    except ValueError:
+        mb = 200
+    return (mb if mb > 0 else 200) << 20
+
+
+def ref_loops(count, es, transport_bound, scratch_multiple, ccl):
+    """Executor loops (ins_v2_all_reduce_sole_executor.cc:160-208, reduce_sole_executor.cc:120-170): at most
+    min(transport bound, ccl / multiple rounded down to 128 B) bytes each; the template slices every loop alone."""
+    nbytes = transport_bound
+    if scratch_multiple:
+        nbytes = min(nbytes, ccl // scratch_multiple // ALIGN * ALIGN)
+    per = max(1, nbytes // es)
+    return [(off, min(per, count - off)) for off in range(0, count, per)]
+
+
+def balanced_bounds(count, n):
+    """ReduceMesh1DTwoShot::CalcSlice (reduce_mesh_1D_two_shot.cc:108-131)."""
+    base, rem = divmod(count, n)
+    out, b = [], 0
+    for c in range(n):
+        ln = base + (1 if c < rem else 0)
+        out.append((b, b + ln))
+        b += ln
+    return out
+
+
+def ceil_bounds(count, n):
+    """ReduceNHR::CalcSlice (reduce_nhr.cc:114-138): ceil(count / n) elements, trailing slices short or empty."""
+    cs = -(-count // n)
+    return [(min(count, c * cs), min(count, (c + 1) * cs)) for c in range(n)]
+
+
+def floor_bounds(count, n):
+    """InsTempAllReduceNHR (ins_temp_all_reduce_nhr.cc:171-173): floor(count / n), the tail on the last slice."""
+    se = count // n
+    return [(i * se, (i + 1) * se if i < n - 1 else count) for i in range(n)]
+
+
 def chunk_bounds(count, n, es):
     align = max(1, ALIGN // es)
     sc = -(-count // n)
@@ -128,29 +175,73 @@ def nhr_steps(n, me, gather):
     return steps
 
 
-def allreduce_nhr(dtype, op, xs):
-    """Simulates the NHR template with write-reduce semantics: the receiver's slice becomes
-    sender_partial (src) (op) receiver_partial (dst); slices are floor(count/n), tail on the last."""
+def nhr_reduce_scatter(dtype, op, work, bounds):
+    """NHR reduce-scatter steps in place on per-rank working arrays: at each step the receiver's slice becomes
+    sender_partial (src) (op) receiver_partial (dst) (write-reduce)."""
+    n = len(work)
+    per_rank = [nhr_steps(n, r, False) for r in range(n)]
+    for step in range(len(per_rank[0])):
+        old = [w.copy() for w in work]
+        for r in range(n):
+            _, frm, _, rxs = per_rank[r][step]
+            for s_idx in rxs:
+                b, e = bounds[s_idx]
+                if e > b:
+                    work[r][b:e] = apply(dtype, op, old[frm][b:e], old[r][b:e])
+
+
+def nhr_all_gather(work, bounds):
+    n = len(work)
+    per_rank = [nhr_steps(n, r, True) for r in range(n)]
+    for step in range(len(per_rank[0])):
+        old = [w.copy() for w in work]
+        for r in range(n):
+            _, frm, _, rxs = per_rank[r][step]
+            for s_idx in rxs:
+                b, e = bounds[s_idx]
+                if e > b:
+                    work[r][b:e] = old[frm][b:e]
+
+
+def allreduce_nhr(dtype, op, xs, ccl=None):
+    """NHR AllReduce per executor loop (AICPU_TS: transport bound = ccl, scratch multiple 1), floor slicing."""
+    ccl = ccl_bytes_from_env() if ccl is None else ccl
     n = len(xs)
-    count = xs[0].size
-    se = count // n
-    bounds = [(i * se, (i + 1) * se if i < n - 1 else count) for i in range(n)]
-    work = [x.copy() for x in xs]
-    for gather in (False, True):
-        per_rank = [nhr_steps(n, r, gather) for r in range(n)]
-        for step in range(len(per_rank[0])):
-            old = [w.copy() for w in work]
-            for r in range(n):
-                _, frm, _, rxs = per_rank[r][step]
-                for s_idx in rxs:
-                    b, e = bounds[s_idx]
-                    if e <= b:
-                        continue
-                    if gather:
-                        work[r][b:e] = old[frm][b:e]
-                    else:
-                        work[r][b:e] = apply(dtype, op, old[frm][b:e], old[r][b:e])
-    return work
+    es = xs[0].itemsize
+    outs = [np.empty_like(x) for x in xs]
+    for off, cnt in ref_loops(xs[0].size, es, ccl, 1, ccl):
+        work = [x[off:off + cnt].copy() for x in xs]
+        bounds = floor_bounds(cnt, n)
+        nhr_reduce_scatter(dtype, op, work, bounds)
+        nhr_all_gather(work, bounds)
+        for r in range(n):
+            outs[r][off:off + cnt] = work[r]
+    return outs
+
+
+def reduce_nhr(dtype, op, xs, root, ccl=None):
+    """NHR Reduce per executor loop (transport bound UB_MAX_DATA_SIZE, scratch multiple 1), ceil slicing; the root's
+    result after the NHR all-gather."""
+    ccl = ccl_bytes_from_env() if ccl is None else ccl
+    n = len(xs)
+    es = xs[0].itemsize
+    out = np.empty_like(xs[0])
+    for off, cnt in ref_loops(xs[0].size, es, UB_MAX_DATA_SIZE, 1, ccl):
+        work = [x[off:off + cnt].copy() for x in xs]
+        bounds = ceil_bounds(cnt, n)
+        nhr_reduce_scatter(dtype, op, work, bounds)
+        nhr_all_gather(work, bounds)
+        out[off:off + cnt] = work[root]
+    return out
+
+
+def reduce_scatter_nhr(dtype, op, xs, rc):
+    """NHR ReduceScatter: slices are the blocks (ins_temp_reduce_scatter_nhr.cc:278-397, 407-456)."""
+    n = len(xs)
+    work = [x[:n * rc].copy() for x in xs]
+    bounds = [(i * rc, (i + 1) * rc) for i in range(n)]
+    nhr_reduce_scatter(dtype, op, work, bounds)
+    return [work[me][me * rc:(me + 1) * rc].copy() for me in range(n)]
 
 
 def reduce_scatter_o1(dtype, op, xs, rc):
@@ -176,13 +267,18 @@ def reduce_oneshot(dtype, op, xs, root):
     return fold(dtype, op, [xs[root]] + [xs[q] for q in range(n) if q != root])
 
 
-def reduce_twoshot(dtype, op, xs, root):
+def reduce_twoshot(dtype, op, xs, root, ccl=None):
+    """Two-shot Reduce per executor loop (transport bound UB_MAX_DATA_SIZE, scratch multiple n), balanced slicing;
+    slice c is folded in order O1 with its owner c first (reduce_mesh_1D_two_shot.cc:209-249)."""
+    ccl = ccl_bytes_from_env() if ccl is None else ccl
     n = len(xs)
     es = xs[0].itemsize
     out = np.empty_like(xs[0])
-    for c, (b, e) in enumerate(chunk_bounds(xs[0].size, n, es)):
-        if e > b:
-            out[b:e] = fold(dtype, op, [xs[c][b:e]] + [xs[q][b:e] for q in range(n) if q != c])
+    for off, cnt in ref_loops(xs[0].size, es, UB_MAX_DATA_SIZE, n, ccl):
+        for c, (b, e) in enumerate(balanced_bounds(cnt, n)):
+            if e > b:
+                b0, e0 = off + b, off + e
+                out[b0:e0] = fold(dtype, op, [xs[c][b0:e0]] + [xs[q][b0:e0] for q in range(n) if q != c])
     return out
 
 
@@ -226,13 +322,13 @@ def expected(op_type, algo, dtype, op, xs, count, root=0):
                 ALGO_RHD: allreduce_rhd, ALGO_NHR: allreduce_nhr, ALGO_TREE: allreduce_tree,
                 ALGO_IPC: allreduce_o2}[algo](dtype, op, xs)
     if op_type == 1:
-        return {ALGO_ONESHOT: reduce_scatter_o1, ALGO_RING: reduce_scatter_ring,
+        return {ALGO_ONESHOT: reduce_scatter_o1, ALGO_RING: reduce_scatter_ring, ALGO_NHR: reduce_scatter_nhr,
                 ALGO_TREE: reduce_scatter_tree, ALGO_IPC: reduce_scatter_o1}[algo](dtype, op, xs, count)
     if op_type == 3:
         full = np.concatenate([x[:count] for x in xs])
         return [full.copy() for _ in xs]
     if op_type == 2:
-        r = {ALGO_ONESHOT: reduce_oneshot, ALGO_TWOSHOT: reduce_twoshot, ALGO_IPC: reduce_twoshot}[algo](
-            dtype, op, xs, root)
+        r = {ALGO_ONESHOT: reduce_oneshot, ALGO_TWOSHOT: reduce_twoshot, ALGO_NHR: reduce_nhr,
+             ALGO_IPC: reduce_twoshot}[algo](dtype, op, xs, root)
         return [r if q == root else None for q in range(len(xs))]
     raise ValueError(op_type)

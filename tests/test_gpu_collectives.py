@@ -101,8 +101,8 @@ def oracle_replay(op_type, algo, n, count, dtype, op, xs, root, piece_bytes):
     return [b[1] for b in bufs]
 
 
-CASES = [(AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5), (AR, 6), (AR, 7), (RS, 1), (RS, 3), (RS, 6), (RS, 7),
-         (RED, 1), (RED, 2), (RED, 7), (AG, 1), (AG, 3)]
+CASES = [(AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5), (AR, 6), (AR, 7), (RS, 1), (RS, 3), (RS, 5), (RS, 6),
+         (RS, 7), (RED, 1), (RED, 2), (RED, 5), (RED, 7), (AG, 1), (AG, 3)]
 
 
 def ipc_status(comm):
@@ -145,6 +145,33 @@ def test_ipc_reduce_scatter_and_reduce(worlds, op_type, n, count):
             assert not outs[r].any(), "non-root recvBuf written"
             continue
         assert O.equal_bits(O.FP32, outs[r], want[r]), r
+
+
+@pytest.mark.parametrize("op_type,algo,n,count", [(RED, 2, 3, 300001), (RED, 5, 5, 600001), (AR, 5, 6, 700001),
+                                                   (RED, 7, 4, 300001), (RED, 7, 3, 250003), (RS, 5, 3, 200003)])
+def test_ownership_orders_follow_executor_loops(monkeypatch, op_type, algo, n, count):
+    """With HCCL_BUFFSIZE = 1 MB the reference's executor loops are 1 MiB / n (Reduce two-shot, also on the IPC path)
+    or 1 MiB (NHR): every loop is sliced on its own, which decides which rank's value is folded first."""
+    monkeypatch.setenv("HCCL_BUFFSIZE", "1")
+    comms = H.loopback_world(n)
+    try:
+        root = 1
+        in_count = count * n if op_type == RS else count
+        xs = [O.random_operands(O.FP32, in_count, seed=700 + r, edge=False) for r in range(n)]
+        used, outs = collective(comms, op_type, algo, O.FP32, O.SUM, xs, count, root=root)
+        assert used == algo
+        if algo == 7:
+            assert ipc_status(comms[0]) & 1 == 0
+        want = R.expected(op_type, used, O.FP32, O.SUM, xs, count, root=root)
+        for r in range(n):
+            if op_type == RED and r != root:
+                assert not outs[r].any(), "non-root recvBuf written"
+                continue
+            assert O.equal_bits(O.FP32, outs[r], want[r]), r
+    finally:
+        torch.cuda.synchronize()
+        for c in comms:
+            c.destroy()
 
 
 @pytest.mark.parametrize("shift", [(1, 1), (0, 3), (2, 0)])

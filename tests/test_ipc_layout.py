@@ -16,24 +16,28 @@ AR, RS, RED = 0, 1, 2
 
 
 def geometry(kind, n, count, es):
-    """RunIpcCollective: (total, chunk stride = chunk length, piece, block elems, rounds)."""
+    """RunIpcCollective for one launch: (chunks [(start, len)] in input coordinates, piece, block elems, rounds).
+    AllReduce: ceil(count/n) rounded to 128 B; ReduceScatter: the blocks; Reduce: the balanced two-shot split."""
     v = 16 // es
     if kind == RS:
-        total, clen = n * count, count
+        chunks = [(c * count, count) for c in range(n)]
+    elif kind == RED:
+        base, rem = divmod(count, n)
+        chunks = [(c * base + min(c, rem), base + (1 if c < rem else 0)) for c in range(n)]
     else:
         align = 128 // es
-        clen = -(-(-(-count // n)) // align) * align
-        total = count
+        cs = -(-(-(-count // n)) // align) * align
+        chunks = [(min(count, c * cs), max(0, min(count, c * cs + cs) - min(count, c * cs))) for c in range(n)]
+    widest = max(ln for _, ln in chunks)
     slot_cap = (STG_BYTES // es // n) // v * v
-    piece = min(slot_cap, -(-clen // v) * v)
+    piece = max(v, min(slot_cap, -(-widest // v) * v))
     block = -(-(-(-piece // BLOCKS)) // v) * v
-    rounds = -(-clen // piece)
-    return total, clen, piece, block, rounds
+    rounds = -(-widest // piece)
+    return chunks, piece, block, rounds
 
 
-def piece_len(total, clen, c, kp, piece):
-    start = c * clen
-    cl = 0 if start >= total else min(clen, total - start)
+def piece_len(chunks, c, kp, piece):
+    cl = chunks[c][1]
     return 0 if kp >= cl else min(piece, cl - kp)
 
 
@@ -46,8 +50,8 @@ def touched(lo, hi, v, vec=True):
 
 def check(kind, n, count, es, vec, root=0):
     v = 16 // es
-    total, clen, piece, block, rounds = geometry(kind, n, count, es)
-    in_len = total
+    chunks, piece, block, rounds = geometry(kind, n, count, es)
+    total = n * count if kind == RS else count
     out_len = count
     assert n * piece <= STG_BYTES // es
     for me in range(n):
@@ -56,16 +60,18 @@ def check(kind, n, count, es, vec, root=0):
             kp = k * piece
             for b in range(BLOCKS):
                 for c in range(n):
-                    plen = piece_len(total, clen, c, kp, piece)
+                    start = chunks[c][0]
+                    cvec = vec and start % v == 0  # ChunkVec: element-wise unless the chunk start is aligned
+                    plen = piece_len(chunks, c, kp, piece)
                     lo = min(plen, b * block)
                     hi = min(plen, lo + block)
                     assert b * block <= lo or lo == hi          # block b's fixed window, whatever the round
-                    for a0, a1 in touched(lo, hi, v, vec):
+                    for a0, a1 in touched(lo, hi, v, cvec):
                         if a1 <= a0:
                             continue
                         assert lo <= a0 and a1 <= hi
-                        g0, g1 = c * clen + kp + a0, c * clen + kp + a1   # input coordinates
-                        assert 0 <= g0 and g1 <= in_len
+                        g0, g1 = start + kp + a0, start + kp + a1   # input coordinates
+                        assert 0 <= g0 and g1 <= total
                         if c != me:
                             assert me * piece + a1 <= n * piece          # owner c's slot me
                             cover[0][g0:g1] += 1
@@ -84,8 +90,7 @@ def check(kind, n, count, es, vec, root=0):
                                 assert g1 <= out_len
                             cover[1][g0:g1] += 1
         for c in range(n):
-            start = c * clen
-            cl = 0 if start >= total else min(clen, total - start)
+            start, cl = chunks[c]
             seg = slice(start, start + cl)
             if c == me:
                 assert np.all(cover[1][seg] == 1), (me, c)
@@ -93,6 +98,8 @@ def check(kind, n, count, es, vec, root=0):
                 assert np.all(cover[0][seg] == 1), (me, c)
                 if kind == AR or (kind == RED and me == root):
                     assert np.all(cover[2][seg] == 1), (me, c)
+        if kind != RS:
+            assert sum(cl for _, cl in chunks) == count  # the chunks tile the launch exactly
 
 
 @pytest.mark.parametrize("kind", [AR, RS, RED])
@@ -104,10 +111,10 @@ def test_ipc_in_bounds_and_exact_cover(kind, n, es, count):
     check(kind, n, count, es, vec=False, root=0)
 
 
-@pytest.mark.parametrize("kind,n,count", [(AR, 2, (36 << 20) + 11), (RS, 4, (9 << 20) + 3), (RED, 4, (36 << 20) + 7)])
+@pytest.mark.parametrize("kind,n,count", [(AR, 2, (36 << 20) + 11), (RS, 4, (9 << 20) + 3), (RED, 2, (40 << 20) + 7)])
 def test_ipc_multi_round_geometry(kind, n, count):
     """Counts that need several pieces per chunk (fp32): still in bounds, exact cover, fixed block windows."""
-    total, clen, piece, block, rounds = geometry(kind, n, count, 4)
+    chunks, piece, block, rounds = geometry(kind, n, count, 4)
     assert rounds >= 2
     check(kind, n, count, 4, vec=True, root=1)
 

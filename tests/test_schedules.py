@@ -51,8 +51,8 @@ def run(op_type, algo, n, count, dtype, op, root=0, piece_bytes=0, inplace=False
 
 CASES = [
     (AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5), (AR, 6),
-    (RS, 1), (RS, 3), (RS, 6),
-    (RED, 1), (RED, 2),
+    (RS, 1), (RS, 3), (RS, 5), (RS, 6),
+    (RED, 1), (RED, 2), (RED, 5),
     (AG, 1), (AG, 3),
 ]
 
@@ -137,12 +137,45 @@ def test_rhd_non_power_of_two_falls_back_to_ring():
 
 
 def test_schedule_scratch_is_bounded():
-    """The staging a schedule addresses never exceeds the communicator's CCL buffer (256 MiB default)."""
+    """The staging a schedule addresses never exceeds the communicator's 2 x HCCL_BUFFSIZE (400 MiB default)."""
     for op_type, algo in CASES:
         for n in (2, 8):
             count = (4 << 30) // 4 // (n if op_type in (RS, AG) else 1)
             _, _, scratch = programs(op_type, algo, n, count, O.FP32)
-            assert scratch * 4 <= 256 << 20, (op_type, algo, n, scratch)
+            assert scratch * 4 <= 2 * (200 << 20), (op_type, algo, n, scratch)
+
+
+# Orders that depend on which rank owns an element follow the reference's executor loops (a loop is at most
+# min(transport bound, HCCL_BUFFSIZE / scratch multiple) bytes and is sliced on its own). With HCCL_BUFFSIZE = 1 MB:
+# Reduce two-shot loops of 1 MiB / n, NHR AllReduce and Reduce loops of 1 MiB.
+@pytest.mark.parametrize("op_type,algo,n,count", [
+    (RED, 2, 3, 300001), (RED, 2, 8, 100003), (RED, 5, 5, 600001), (AR, 5, 6, 700001), (RS, 5, 3, 200003),
+    (AR, 2, 4, 400003),
+])
+def test_ownership_orders_follow_executor_loops(monkeypatch, op_type, algo, n, count):
+    monkeypatch.setenv("HCCL_BUFFSIZE", "1")
+    used, xs, outs = run(op_type, algo, n, count, O.FP32, O.SUM, root=1, seed=11)
+    assert used == algo
+    want = R.expected(op_type, used, O.FP32, O.SUM, xs, count, root=1)
+    for r in range(n):
+        if op_type == RED and r != 1:
+            continue
+        assert O.equal_bits(O.FP32, outs[r], want[r]), r
+
+
+def test_reduce_two_shot_slicing_is_balanced_not_aligned():
+    """ReduceMesh1DTwoShot::CalcSlice gives the first count % n ranks one more element
+    (reduce_mesh_1D_two_shot.cc:108-131); the 128-B aligned ceil split used by the AllReduce two-shot would make other
+    ranks own (and fold first) some elements, which changes fp32 sums."""
+    n, count = 3, 1000
+    used, xs, outs = run(RED, 2, n, count, O.FP32, O.SUM, root=0, seed=3)
+    want = R.reduce_twoshot(O.FP32, O.SUM, xs, 0)
+    assert O.equal_bits(O.FP32, outs[0], want)
+    aligned = np.empty_like(xs[0])
+    for c, (b, e) in enumerate(R.chunk_bounds(count, n, 4)):
+        if e > b:
+            aligned[b:e] = R.fold(O.FP32, O.SUM, [xs[c][b:e]] + [xs[q][b:e] for q in range(n) if q != c])
+    assert not O.equal_bits(O.FP32, outs[0], aligned)
 
 
 def test_sends_and_recvs_pair_up():
