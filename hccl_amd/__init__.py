@@ -216,3 +216,24 @@ def comm_init_host_exchange(n_ranks: int, rank: int, all_gather) -> Comm:
     c = Comm(h.value)
     c._keepalive = fn  # the library calls it for the communicator's lifetime
     return c
+
+
+def rank_table_info(path: str, rank: int):
+    """(n_ranks, device_id of rank) of a rank table file, validated as HcclCommInitClusterInfo validates it."""
+    n = ctypes.c_uint32(0)
+    dev = ctypes.c_int32(-1)
+    check("HcclAmdRankTableInfo", lib.HcclAmdRankTableInfo(path.encode(), rank, ctypes.byref(n), ctypes.byref(dev)))
+    return n.value, dev.value
+
+
+def comm_init_cluster_info(path: str, rank: int) -> Comm:
+    h = ctypes.c_void_p(0)
+    check("HcclCommInitClusterInfo", lib.HcclCommInitClusterInfo(path.encode(), rank, ctypes.byref(h)))
+    return Comm(h.value)
+
+
+def comm_init_all(devices) -> List[Comm]:
+    arr_dev = (ctypes.c_int32 * len(devices))(*devices)
+    arr = (ctypes.c_void_p * len(devices))()
+    check("HcclCommInitAll", lib.HcclCommInitAll(len(devices), arr_dev, arr))
+    return [Comm(arr[i]) for i in range(len(devices))]

@@ -155,6 +155,9 @@ SIGNATURES = {
     "HcclAmdCommLastAlgo": (_i32, [_vp]),
     "HcclAmdCommIpcStatus": (_res, [_vp, ctypes.POINTER(_u32)]),
     "HcclAmdCommInitHostExchange": (_res, [_u32, _u32, _vp, _vp, ctypes.POINTER(_vp)]),
+    "HcclAmdRankTableInfo": (_res, [ctypes.c_char_p, _u32, ctypes.POINTER(_u32), ctypes.POINTER(ctypes.c_int32)]),
+    "HcclCommInitClusterInfo": (_res, [ctypes.c_char_p, _u32, ctypes.POINTER(_vp)]),
+    "HcclCommInitAll": (_res, [_u32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(_vp)]),
 }
 
 

@@ -177,6 +177,21 @@ std::unique_ptr<Transport> MakeRcclTransport(void* uniqueId, uint32_t nRanks, ui
     return t;
 }
 
+HcclResult MakeRcclTransportsAll(uint32_t ndev, const int32_t* devices, std::vector<std::unique_ptr<Transport>>* out)
+{
+    std::vector<ncclComm_t> comms(ndev, nullptr);
+    std::vector<int> devs(devices, devices + ndev);
+    HcclResult r = FromNccl(ncclCommInitAll(comms.data(), static_cast<int>(ndev), devs.data()), "ncclCommInitAll");
+    if (r != HCCL_SUCCESS) return r;
+    out->clear();
+    for (uint32_t i = 0; i < ndev; ++i) {
+        auto t = std::make_unique<RcclTransport>();
+        t->comm = comms[i];
+        out->push_back(std::move(t));
+    }
+    return HCCL_SUCCESS;
+}
+
 // ------------------------------------------------------------------------------------------------ loopback
 
 // nRanks ranks in one process on one device. A send posts {source, bytes, ready event} into the (from, to) FIFO;

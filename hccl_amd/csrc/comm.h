@@ -39,6 +39,8 @@ public:
 };
 
 std::unique_ptr<Transport> MakeRcclTransport(void* uniqueId, uint32_t nRanks, uint32_t rank, HcclResult* err);
+// One RCCL communicator per listed device, all in this process (ncclCommInitAll); (*out)[r] is rank r.
+HcclResult MakeRcclTransportsAll(uint32_t ndev, const int32_t* devices, std::vector<std::unique_ptr<Transport>>* out);
 HcclResult RcclGetUniqueId(void* id128);
 
 class LoopbackWorld;

@@ -13,7 +13,8 @@
  * (examples/02_collectives/01_allreduce/main.cc:75,100,122; test/st/.../all_reduce_testcase.cc:80);
  * they are external to the reference repo and are implemented here over RCCL:
  *
- *   HcclGetRootInfo, HcclCommInitRootInfo, HcclCommDestroy, HcclGetRankSize, HcclGetRankId
+ *   HcclGetRootInfo, HcclCommInitRootInfo, HcclCommInitClusterInfo, HcclCommInitAll, HcclCommDestroy,
+ *   HcclGetRankSize, HcclGetRankId
  *
  * Semantics: stream-ordered and asynchronous with respect to the host, like the reference
  * (op_common.cc:962-970): work is enqueued behind everything already on `stream`, internal
@@ -49,6 +50,14 @@ extern HcclResult HcclAllGather(void* sendBuf, void* recvBuf, uint64_t sendCount
 extern HcclResult HcclGetRootInfo(HcclRootInfo* rootInfo);
 extern HcclResult HcclCommInitRootInfo(uint32_t nRanks, const HcclRootInfo* rootInfo, uint32_t rank,
                                        HcclComm* comm);
+/* Rank `rank` of the communicator described by the rank table file `clusterInfo` (JSON, docs/.../cluster_info_config/rank_table_config_a2.md;
+ * test/st/algorithm/testcase/all_reduce_testcase.cc:80). The rank runs on its entry's device_id. Rank 0 publishes the
+ * transport's unique id over TCP at the rank-0 server's host_ip (else HCCL_IF_IP, else 127.0.0.1 for one server) and
+ * the rank-0 device's host_port (else HCCL_IF_BASE_PORT, default 60000), waiting at most HCCL_CONNECT_TIMEOUT + 20 s. */
+extern HcclResult HcclCommInitClusterInfo(const char* clusterInfo, uint32_t rank, HcclComm* comm);
+/* One communicator per listed device in this process (single-node batch creation); comms[i] is rank i on
+ * devices[i]. Drive each rank from its own host thread. */
+extern HcclResult HcclCommInitAll(uint32_t ndev, int32_t* devices, HcclComm* comms);
 extern HcclResult HcclCommDestroy(HcclComm comm);
 extern HcclResult HcclGetRankSize(HcclComm comm, uint32_t* rankSize);
 extern HcclResult HcclGetRankId(HcclComm comm, uint32_t* rank);

@@ -131,6 +131,10 @@ extern int32_t HcclAmdCommLastAlgo(HcclComm comm);
  * AllReduce, in polls (diagnostic; 0 = no block ever waited). */
 extern HcclResult HcclAmdCommIpcStatus(HcclComm comm, uint32_t* status);
 
+/* Parse and validate a rank table (as HcclCommInitClusterInfo does): *nRanks = number of ranks, *deviceId = the
+ * device_id of `rank`. HCCL_E_PARA for a malformed table or a rank outside it. */
+extern HcclResult HcclAmdRankTableInfo(const char* clusterInfo, uint32_t rank, uint32_t* nRanks, int32_t* deviceId);
+
 /* Blocking host all-gather supplied by the caller's bootstrap (a TCP store, MPI, torch.distributed gloo ...):
  * gathers `bytes` bytes from every rank into all[nRanks * bytes] in rank order; returns 0 on success. */
 typedef int32_t (*HcclAmdHostAllGatherFn)(void* ctx, const void* mine, uint64_t bytes, void* all);
