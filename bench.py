@@ -281,10 +281,23 @@ def bench_c4(comm, send, recv, world) -> dict:
     t_rs = _timed(lambda: comm.reduce_scatter(x, shard, H.HcclReduceOp.SUM, s), 5)
     t_ag = _timed(lambda: comm.all_gather(shard, full, s), 5)
     f = (world - 1) / world
-    return {"workload": "C4: ReduceScatter + AllGather bf16 SUM, 2 GiB per rank",
-            "rs_ms": round(t_rs * 1e3, 3), "ag_ms": round(t_ag * 1e3, 3),
-            "rs_busbw_GBps": round(nbytes / t_rs / 1e9 * f, 2), "ag_busbw_GBps": round(nbytes / t_ag / 1e9 * f, 2),
-            "rs_ag_busbw_GBps": round(2 * nbytes / (t_rs + t_ag) / 1e9 * f, 2)}
+    out = {"workload": "C4: ReduceScatter + AllGather bf16 SUM, 2 GiB per rank",
+           "rs_ms": round(t_rs * 1e3, 3), "ag_ms": round(t_ag * 1e3, 3),
+           "rs_busbw_GBps": round(nbytes / t_rs / 1e9 * f, 2), "ag_busbw_GBps": round(nbytes / t_ag / 1e9 * f, 2),
+           "rs_ag_busbw_GBps": round(2 * nbytes / (t_rs + t_ag) / 1e9 * f, 2)}
+    # the same ReduceScatter on the one-sided IPC kernel (same order O1 as the mesh schedule: same bits)
+    ref = shard.view(torch.int16)[:: 1 << 10].clone()
+    comm.set_algo(H.Algo.IPC_TWOSHOT)
+    try:
+        t_ipc = _timed(lambda: comm.reduce_scatter(x, shard, H.HcclReduceOp.SUM, s), 5)
+        out["rs_ipc_ms"] = round(t_ipc * 1e3, 3)
+        out["rs_ipc_busbw_GBps"] = round(nbytes / t_ipc / 1e9 * f, 2)
+        out["rs_ipc_ran"] = H.Algo(comm.last_algo).name
+        out["rs_ipc_matches_mesh"] = bool(torch.equal(ref, shard.view(torch.int16)[:: 1 << 10]))
+        out["rs_ipc_barrier_timeouts"] = comm.ipc_status() & 1
+    finally:
+        comm.set_algo(H.Algo.AUTO)
+    return out
 
 
 def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:

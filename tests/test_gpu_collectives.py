@@ -243,7 +243,8 @@ def test_fp32_sum(worlds, op_type, algo, n, count, streams, monkeypatch):
 @pytest.mark.parametrize("dtype", [O.INT8, O.INT16, O.INT32, O.INT64, O.UINT64, O.FP16, O.BFP16, O.FP64],
                          ids=lambda v: O.DTYPE_NAMES[v])
 @pytest.mark.parametrize("op", O.OPS, ids=lambda v: O.OP_NAMES[v])
-@pytest.mark.parametrize("op_type,algo", [(AR, 1), (AR, 2), (AR, 3), (AR, 7), (RS, 1), (RS, 7), (RED, 2), (RED, 7)])
+@pytest.mark.parametrize("op_type,algo", [(AR, 1), (AR, 2), (AR, 3), (AR, 5), (AR, 7), (RS, 1), (RS, 5), (RS, 7),
+                                          (RED, 2), (RED, 5), (RED, 7)])
 def test_dtypes_ops(worlds, op_type, algo, dtype, op):
     n, count, root = 4, 40961, 2
     comms = worlds(n)
