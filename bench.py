@@ -194,7 +194,8 @@ def bench_local(args) -> dict:
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic (uniform [-1,1) fp32, device-generated)",
+        "data": "synthetic (uniform [-1,1) fp32, device-generated)" + (
+            "; HARNESS MODE (all ranks on one GPU, IPC-only communicator): not a result" if harness else ""),
         "config": {
             "workload": "C2: 1-GPU local reduce dst = src + dst (HcclAmdLocalReduce), 2 x 1 GiB fp32 in HBM",
             "count": C2_COUNT,
@@ -354,15 +355,40 @@ def bench_c3_algos(comm, send, recv, world) -> dict:
 
 
 def bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
+    """Runs the N > 1 measurement on a dedicated stream: every HCCL call gets a real stream (the null default stream
+    is rejected with HCCL_E_PTR, as the reference's entry check does) and every event is recorded on it."""
+    if os.environ.get("HCCL_AMD_BENCH_HOST_EXCHANGE") == "1":
+        local_rank = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_rank)
+    with torch.cuda.stream(torch.cuda.Stream()):
+        return _bench_allreduce(args, rank, world, local_rank)
+
+
+def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     import torch.distributed as dist
 
+    # HCCL_AMD_BENCH_HOST_EXCHANGE=1 is a harness mode for a one-GPU box: every rank shares the device and the
+    # communicator is the IPC-only one (HcclAmdCommInitHostExchange, bootstrapped over the gloo group), so the N > 1
+    # code path runs end to end; the RCCL-dependent rows then report HCCL_E_NOT_SUPPORT. Never used for results.
+    harness = os.environ.get("HCCL_AMD_BENCH_HOST_EXCHANGE") == "1"
+    if harness:
+        local_rank = local_rank % max(1, torch.cuda.device_count())
+        args.no_rccl_ref = True
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    # root info out of band, exactly as the reference's callers do (examples/.../01_allreduce/main.cc:122-136)
-    obj = [H.get_root_info() if rank == 0 else None]
-    dist.broadcast_object_list(obj, src=0)
-    comm = H.comm_init_root_info(world, obj[0], rank)
+    if harness:
+        def _all_gather(b):
+            out = [None] * world
+            dist.all_gather_object(out, b)
+            return out
+
+        comm = H.comm_init_host_exchange(world, rank, _all_gather)
+    else:
+        # root info out of band, exactly as the reference's callers do (examples/.../01_allreduce/main.cc:122-136)
+        obj = [H.get_root_info() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm = H.comm_init_root_info(world, obj[0], rank)
     count = C3_BYTES // 4
     g = torch.Generator(device=dev).manual_seed(0x5EED0003 + rank)
     send = torch.rand(count, device=dev, generator=g).mul_(2).sub_(1)
@@ -418,7 +444,8 @@ def bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic (uniform [-1,1) fp32, device-generated)",
+        "data": "synthetic (uniform [-1,1) fp32, device-generated)" + (
+            "; HARNESS MODE (all ranks on one GPU, IPC-only communicator): not a result" if harness else ""),
         "config": {
             "workload": "C3: HcclAllReduce fp32 SUM, 4 GiB per rank, RCCL send/recv over xGMI + HIP reduce kernels",
             "bytes_per_rank": C3_BYTES,
