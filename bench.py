@@ -194,8 +194,7 @@ def bench_local(args) -> dict:
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic (uniform [-1,1) fp32, device-generated)" + (
-            "; HARNESS MODE (all ranks on one GPU, IPC-only communicator): not a result" if harness else ""),
+        "data": "synthetic (uniform [-1,1) fp32, device-generated)",
         "config": {
             "workload": "C2: 1-GPU local reduce dst = src + dst (HcclAmdLocalReduce), 2 x 1 GiB fp32 in HBM",
             "count": C2_COUNT,
@@ -233,21 +232,21 @@ def rccl_allreduce_reference(send, recv, world, args):
     try:
         g = dist.new_group(backend="nccl")
         recv.copy_(send)
-        for _ in range(2):
-            dist.all_reduce(recv, group=g)
-        torch.cuda.synchronize()
-        dist.barrier()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        f = (world - 1) / world
         n = max(3, args.steps // 2)
-        e0.record()
-        for _ in range(n):
-            dist.all_reduce(recv, group=g)
-        e1.record()
-        torch.cuda.synchronize()
-        t = torch.tensor([e0.elapsed_time(e1) / 1e3 / n], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        algbw = C3_BYTES / float(t[0]) / 1e9
-        return {"ms_per_step": round(float(t[0]) * 1e3, 3), "busbw_GBps": round(algbw * 2 * (world - 1) / world, 2)}
+        t = _timed(lambda: dist.all_reduce(recv, group=g), n)
+        out = {"ms_per_step": round(t * 1e3, 3), "busbw_GBps": round(C3_BYTES / t / 1e9 * 2 * f, 2)}
+        # The two data movements of the two-shot on RCCL's own kernels, same bytes per rank: the all-to-all that
+        # the scatter phase is (every rank sends 1/n of its buffer to each peer) and the ring all-gather of the
+        # gather phase. They bound what p2p groups over the same links can reach.
+        t = _timed(lambda: dist.all_to_all_single(recv, send, group=g), 3)
+        out["alltoall_ms"] = round(t * 1e3, 3)
+        out["alltoall_busbw_GBps"] = round(C3_BYTES / t / 1e9 * f, 2)
+        shard = send[: send.numel() // world]
+        t = _timed(lambda: dist.all_gather_into_tensor(recv, shard, group=g), 3)
+        out["allgather_ms"] = round(t * 1e3, 3)
+        out["allgather_busbw_GBps"] = round(C3_BYTES / t / 1e9 * f, 2)
+        return out
     except Exception as e:  # noqa: BLE001
         return {"error": f"{type(e).__name__}: {e}"}
 
