@@ -279,16 +279,20 @@ def bench_c4(comm, send, recv, world) -> dict:
     shard = torch.empty(x.numel() // world, dtype=torch.bfloat16, device=x.device)
     s = torch.cuda.current_stream()
     t_rs = _timed(lambda: comm.reduce_scatter(x, shard, H.HcclReduceOp.SUM, s), 5)
+    rs_algo = H.Algo(comm.last_algo).name  # MESH_CHUNK at this size, as the reference selects
     t_ag = _timed(lambda: comm.all_gather(shard, full, s), 5)
     f = (world - 1) / world
-    out = {"workload": "C4: ReduceScatter + AllGather bf16 SUM, 2 GiB per rank",
+    out = {"workload": "C4: ReduceScatter + AllGather bf16 SUM, 2 GiB per rank", "rs_algo": rs_algo,
            "rs_ms": round(t_rs * 1e3, 3), "ag_ms": round(t_ag * 1e3, 3),
            "rs_busbw_GBps": round(nbytes / t_rs / 1e9 * f, 2), "ag_busbw_GBps": round(nbytes / t_ag / 1e9 * f, 2),
            "rs_ag_busbw_GBps": round(2 * nbytes / (t_rs + t_ag) / 1e9 * f, 2)}
-    # the same ReduceScatter on the one-sided IPC kernel (same order O1 as the mesh schedule: same bits)
-    ref = shard.view(torch.int16)[:: 1 << 10].clone()
-    comm.set_algo(H.Algo.IPC_TWOSHOT)
+    # the mesh ReduceScatter (order O1) and the one-sided IPC kernel with the same order: same bits
     try:
+        comm.set_algo(H.Algo.MESH_ONESHOT)
+        t_mesh = _timed(lambda: comm.reduce_scatter(x, shard, H.HcclReduceOp.SUM, s), 3, warmup=1)
+        out["rs_mesh_ms"] = round(t_mesh * 1e3, 3)
+        ref = shard.view(torch.int16)[:: 1 << 10].clone()
+        comm.set_algo(H.Algo.IPC_TWOSHOT)
         t_ipc = _timed(lambda: comm.reduce_scatter(x, shard, H.HcclReduceOp.SUM, s), 5)
         out["rs_ipc_ms"] = round(t_ipc * 1e3, 3)
         out["rs_ipc_busbw_GBps"] = round(nbytes / t_ipc / 1e9 * f, 2)
@@ -328,8 +332,8 @@ def bench_c3_algos(comm, send, recv, world) -> dict:
     out = {}
     ref = None
     try:
-        for algo in (H.Algo.MESH_TWOSHOT, H.Algo.IPC_TWOSHOT, H.Algo.RING, H.Algo.RHD, H.Algo.NHR,
-                     H.Algo.MESH_ONESHOT):
+        for algo in (H.Algo.MESH_TWOSHOT, H.Algo.IPC_TWOSHOT, H.Algo.MESH_CHUNK, H.Algo.RING, H.Algo.RHD,
+                     H.Algo.NHR, H.Algo.MESH_ONESHOT):
             comm.set_algo(algo)
             t = _timed(lambda: comm.all_reduce(send, recv, H.HcclReduceOp.SUM, s), 3, warmup=1)
             row = {"ms": round(t * 1e3, 3), "busbw_GBps": round(C3_BYTES / t / 1e9 * 2 * (world - 1) / world, 2)}

@@ -109,6 +109,11 @@ def build_schedule(op_type: int, algo: int, n_ranks: int, rank: int, count: int,
     return arr, nops.value, used.value, scratch.value
 
 
+def select_algo(op_type: int, n_ranks: int, nbytes: int, special: bool = False) -> int:
+    """The algorithm HCCL_AMD_ALGO_AUTO picks (HcclAmdSelectAlgo)."""
+    return lib.HcclAmdSelectAlgo(int(op_type), n_ranks, nbytes, 1 if special else 0)
+
+
 # ----------------------------------------------------------------------------------------- communicators
 
 

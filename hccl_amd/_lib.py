@@ -80,6 +80,7 @@ class Algo(enum.IntEnum):
     NHR = 5
     ORDER_PRESERVED = 6
     IPC_TWOSHOT = 7
+    MESH_CHUNK = 8
 
 
 class OpType(enum.IntEnum):
@@ -144,6 +145,7 @@ SIGNATURES = {
     "HcclAmdSetReduceLaunch": (_res, [_u32, _u32, _u32]),
     "HcclAmdDataTypeSize": (_u32, [_i32]),
     "HcclAmdGetErrorString": (ctypes.c_char_p, [_i32]),
+    "HcclAmdSelectAlgo": (_i32, [_i32, _u32, _u64, _i32]),
     "HcclAmdBuildSchedule": (
         _res,
         [_i32, _i32, _u32, _u32, _u64, _i32, _u32, _u64, ctypes.POINTER(HcclAmdIrOp), _u64,

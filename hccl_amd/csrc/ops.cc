@@ -55,6 +55,14 @@ bool NeedStrictOrder(int32_t opType, HcclDataType dt, HcclReduceOp op, uint32_t 
     return fp && (op == HCCL_REDUCE_SUM || op == HCCL_REDUCE_PROD) && nRanks > 2;
 }
 
+// isDataTypeOrReduceTypeSpecial of the selectors (all_reduce_auto_selector.cc:525-528,
+// reduce_scatter_auto_selector.cc:477): 64-bit data or PROD.
+bool IsSpecialForSelector(HcclDataType dt, HcclReduceOp op)
+{
+    return dt == HCCL_DATA_TYPE_INT64 || dt == HCCL_DATA_TYPE_UINT64 || dt == HCCL_DATA_TYPE_FP64 ||
+           op == HCCL_REDUCE_PROD;
+}
+
 HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, uint64_t count, HcclDataType dt,
                          HcclReduceOp op, uint32_t root, hipStream_t stream)
 {
@@ -96,6 +104,7 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     p.pieceBytes = c.pieceBytes;
     p.scratchCapBytes = c.scratchBytes;
     p.cclBytes = c.cclBytes;
+    p.special = IsSpecialForSelector(dt, op);
     Schedule s;
     HcclResult r = static_cast<HcclResult>(BuildSchedule(p, &s));
     if (r != HCCL_SUCCESS) return r;
@@ -280,7 +289,7 @@ HcclResult HcclAmdCommSetAlgo(HcclComm comm, int32_t algo)
 {
     Comm* c = AsComm(comm);
     if (c == nullptr) return HCCL_E_PTR;
-    if (algo < HCCL_AMD_ALGO_AUTO || algo > HCCL_AMD_ALGO_IPC_TWOSHOT) return HCCL_E_PARA;
+    if (algo < HCCL_AMD_ALGO_AUTO || algo > HCCL_AMD_ALGO_MESH_CHUNK) return HCCL_E_PARA;
     c->algoOverride = algo;
     return HCCL_SUCCESS;
 }
@@ -297,6 +306,11 @@ int32_t HcclAmdCommLastAlgo(HcclComm comm)
 {
     Comm* c = AsComm(comm);
     return c == nullptr ? -1 : c->lastAlgo;
+}
+
+int32_t HcclAmdSelectAlgo(int32_t opType, uint32_t nRanks, uint64_t bytes, int32_t special)
+{
+    return SelectAlgo(opType, nRanks, bytes, special != 0);
 }
 
 HcclResult HcclAmdBuildSchedule(int32_t opType, int32_t algo, uint32_t nRanks, uint32_t rank, uint64_t count,
@@ -317,6 +331,7 @@ HcclResult HcclAmdBuildSchedule(int32_t opType, int32_t algo, uint32_t nRanks, u
     p.pieceBytes = pieceBytes;
     p.scratchCapBytes = ScratchBytesDefault();
     p.cclBytes = CclBytesDefault();
+    p.special = IsSpecialForSelector(dataType, HCCL_REDUCE_SUM);  // the op is not an argument here
     Schedule s;
     HcclResult r = static_cast<HcclResult>(BuildSchedule(p, &s));
     if (r != HCCL_SUCCESS) return r;

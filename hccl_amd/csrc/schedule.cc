@@ -289,6 +289,176 @@ void AllReduceTwoShot(const ScheduleParams& p, Builder& b)
     }
 }
 
+// ------------------------------------------------------------------------------------------- MeshChunk (O6)
+//
+// The reference's MeshChunk templates (ins_temp_all_reduce_mesh_1D_two_shot_mesh_chunk.cc:161-275,
+// ins_temp_reduce_scatter_mesh_1D_meshchunk.cc:139-252) cut the chunk that rank t owns into n-1 sub-slices and run
+// n-1 steps; in step s every rank write-reduces its raw input of sub-slice i of peer (me - nextNum)'s chunk into
+// that peer's CCL buffer, nextNum = s + i + 1, plus one when it reaches n (:207-212 / :200-204). Receiver t thus
+// gets sub-slice j at step s from sender t + f(s + j + 1), f(x) = x < n ? x : x + 1. Writes into one receiver are
+// serialised step by step: a sender waits for the receiver's ACK of step s+1, which the receiver posts only after all
+// of its threads have seen the DATA signals of step s and synchronised (PostSyncInterThreads / PreSyncInterThreads,
+// :264-273; SendRecvBatchWriteReduce's handshake, alg_data_trans_wrapper.cc:247-272, 481-514). The CCL buffer starts
+// as the receiver's own input (PreCopy), so sub-slice j of owner t is the left fold
+//     acc = x_t;  acc = x_{t+o} (op) acc  for o = j+1, ..., n-1, 1, ..., j   (peers by rank offset, mod n)  — O6.
+// Here the raw inputs are exchanged into staging slots (as in the two-shot) and every (piece, sub-slice) segment is
+// one ordered n-ary fold with that operand order; the data movement granule does not affect the bits.
+
+// Sub-slices of a chunk of `count` elements, AllReduce form (…mesh_chunk.cc:166-183): n-1 slices, the first
+// count % (n-1) one element longer.
+std::vector<Span> SubSlicesEven(uint64_t count, uint32_t parts)
+{
+    std::vector<Span> v;
+    const uint64_t base = count / parts, big = count % parts;
+    uint64_t b = 0;
+    for (uint32_t i = 0; i < parts; ++i) {
+        const uint64_t len = base + (i < big ? 1 : 0);
+        v.push_back({b, len});
+        b += len;
+    }
+    return v;
+}
+
+// ReduceScatter form (…meshchunk.cc:155-180): n-2 slices of floor(bytes / (n-1)) rounded down to AICPU_ALIGN_SIZE
+// (4 KiB, alg_param.h:91) and the remainder last; the even split when that alignment leaves nothing.
+std::vector<Span> SubSlicesRs(uint64_t count, uint32_t parts, uint32_t es)
+{
+    constexpr uint64_t kAicpuAlign = 4096;
+    const uint64_t align = count * es / parts / kAicpuAlign * kAicpuAlign;
+    if (parts < 2 || align == 0) return SubSlicesEven(count, parts);
+    std::vector<Span> v;
+    const uint64_t a = align / es;
+    for (uint32_t i = 0; i + 1 < parts; ++i) v.push_back({uint64_t(i) * a, a});
+    v.push_back({uint64_t(parts - 1) * a, count - uint64_t(parts - 1) * a});
+    return v;
+}
+
+// Peers of owner t in the O6 order of sub-slice j (rank offsets j+1 .. n-1, then 1 .. j).
+std::vector<uint32_t> O6Peers(uint32_t n, uint32_t t, uint32_t j)
+{
+    std::vector<uint32_t> v;
+    for (uint32_t s = 0; s + 1 < n; ++s) {
+        uint32_t x = s + j + 1;
+        if (x >= n) x += 1;
+        v.push_back((t + x) % n);
+    }
+    return v;
+}
+
+// Emits the folds of one piece [pc.begin, pc.begin + pc.len) of my chunk (chunk-relative coordinates in `subs`):
+// own operand at own(e), peer q's at slotOf(q) + (e - pc.begin), result at out(e) — one REDUCE per sub-slice segment.
+template <class OwnRef, class OutRef, class SlotRef>
+void EmitO6Folds(Builder& b, uint32_t n, uint32_t me, Span pc, const std::vector<Span>& subs, OwnRef own, OutRef out,
+                 SlotRef slotOf)
+{
+    for (uint32_t j = 0; j < subs.size(); ++j) {
+        const uint64_t lo = std::max(pc.begin, subs[j].begin);
+        const uint64_t hi = std::min(pc.begin + pc.len, subs[j].begin + subs[j].len);
+        if (lo >= hi) continue;
+        std::vector<Ref> srcs{own(lo)};
+        for (uint32_t q : O6Peers(n, me, j)) {
+            Ref s = slotOf(q);
+            s.off += lo - pc.begin;
+            srcs.push_back(s);
+        }
+        b.Reduce(out(lo), srcs, hi - lo);
+    }
+}
+
+// AllReduce MeshChunk: executor loops of min(ccl, ccl / 2) (scratch multiple 2, …mesh_chunk.cc:48-55), each sliced
+// into n chunks of ceil(count / n) elements (CalcSliceInfoVec :79-97, no 128-B alignment), O6 fold per sub-slice,
+// then the mesh all-gather. Pieces of all loops form one pipeline as in the two-shot: step u scatters piece u and
+// gathers piece u-2 in one group while piece u-1 is folded.
+void AllReduceMeshChunk(const ScheduleParams& p, Builder& b)
+{
+    const uint32_t n = p.nRanks, me = p.rank;
+    const uint64_t loopElems = RefLoopElems(p, p.cclBytes, 2);
+    struct Unit {
+        uint64_t loopOff, loopCount, t;
+    };
+    const uint64_t kSlots = 2;
+    const uint64_t firstChunk = CeilSlice(std::min(loopElems, p.count), n, 0).len;
+    // one staging piece per chunk of a loop when it fits (the loop is already the reference's transfer unit)
+    const uint64_t pe = PieceElems(p, 4 * std::max<uint64_t>(1, firstChunk), kSlots * (n - 1));
+    std::vector<Unit> units;
+    for (uint64_t off = 0; off < p.count; off += loopElems) {
+        const uint64_t cnt = std::min(loopElems, p.count - off);
+        const uint64_t np = std::max<uint64_t>(1, CeilDiv(CeilSlice(cnt, n, 0).len, pe));
+        for (uint64_t t = 0; t < np; ++t) units.push_back({off, cnt, t});
+    }
+    auto slot = [&](uint64_t u, uint32_t q) { return Scr(((u % kSlots) * (n - 1) + PeerSlot(q, me)) * pe); };
+    auto chunk = [&](const Unit& x, uint32_t c) {
+        Span s = CeilSlice(x.loopCount, n, c);
+        s.begin += x.loopOff;
+        return s;
+    };
+    const uint64_t nu = units.size();
+    for (uint64_t u = 0; u < nu + 2; ++u) {
+        if (u < nu) {
+            const Unit& x = units[u];
+            const Span rs = Piece(chunk(x, me), pe, x.t);
+            for (uint32_t q : PeerOrder(n, me)) {
+                const Span out = Piece(chunk(x, q), pe, x.t);
+                b.Send(q, In(out.begin), out.len);
+                b.Recv(q, slot(u, q), rs.len);
+            }
+        }
+        if (u >= 2) {
+            const Unit& x = units[u - 2];
+            const Span mineP = Piece(chunk(x, me), pe, x.t);
+            for (uint32_t q : PeerOrder(n, me)) {
+                const Span theirs = Piece(chunk(x, q), pe, x.t);
+                b.Send(q, Out(mineP.begin), mineP.len);
+                b.Recv(q, Out(theirs.begin), theirs.len);
+            }
+        }
+        b.EndGroup();
+        if (u < nu) {
+            const Unit& x = units[u];
+            const Span mine = chunk(x, me);
+            Span pc = Piece({0, mine.len}, pe, x.t);  // chunk-relative
+            if (pc.len == 0) continue;
+            EmitO6Folds(b, n, me, pc, SubSlicesEven(mine.len, n - 1),
+                        [&](uint64_t e) { return In(mine.begin + e); }, [&](uint64_t e) { return Out(mine.begin + e); },
+                        [&](uint32_t q) { return slot(u, q); });
+        }
+    }
+}
+
+// ReduceScatter MeshChunk: executor loops of min(ccl - 1 MiB, (ccl - 1 MiB) / (n-1)) (TMP_MEM_RESERVE_SIZE and
+// scratch multiple n-1, ins_v2_reduce_scatter_sole_executor.cc:32,160-175; …meshchunk.cc:66-72) over recvCount,
+// each block cut into the 4-KiB-aligned sub-slices, O6 fold per sub-slice.
+void ReduceScatterMeshChunk(const ScheduleParams& p, Builder& b)
+{
+    const uint32_t n = p.nRanks, me = p.rank;
+    const uint64_t rc = p.count;
+    constexpr uint64_t kReserve = 1ull << 20;
+    // the reference has no loop at all when HCCL_BUFFSIZE <= 1 MiB (maxDataCountPerLoop == 0 → HCCL_E_INTERNAL);
+    // here the whole CCL size is used then
+    const uint64_t tmp = p.cclBytes > kReserve ? p.cclBytes - kReserve : p.cclBytes;
+    const uint64_t loopBytes = std::min(tmp, tmp / (n - 1) / kAlignBytes * kAlignBytes);
+    const uint64_t loopElems = std::max<uint64_t>(1, loopBytes / p.elemSize);
+    const uint64_t kSlots = 2;
+    const uint64_t pe = PieceElems(p, std::min(rc, loopElems), kSlots * (n - 1));
+    auto slot = [&](uint64_t u, uint32_t q) { return Scr(((u % kSlots) * (n - 1) + PeerSlot(q, me)) * pe); };
+    uint64_t u = 0;
+    for (uint64_t off = 0; off < rc; off += loopElems) {
+        const uint64_t cnt = std::min(loopElems, rc - off);
+        const std::vector<Span> subs = SubSlicesRs(cnt, n - 1, p.elemSize);
+        const uint64_t np = std::max<uint64_t>(1, CeilDiv(cnt, pe));
+        for (uint64_t t = 0; t < np; ++t, ++u) {
+            const Span pc = Piece({0, cnt}, pe, t);  // loop-relative
+            for (uint32_t q : PeerOrder(n, me)) {
+                b.Send(q, In(uint64_t(q) * rc + off + pc.begin), pc.len);
+                b.Recv(q, slot(u, q), pc.len);
+            }
+            b.EndGroup();
+            EmitO6Folds(b, n, me, pc, subs, [&](uint64_t e) { return In(uint64_t(me) * rc + off + e); },
+                        [&](uint64_t e) { return Out(off + e); }, [&](uint32_t q) { return slot(u, q); });
+        }
+    }
+}
+
 // Ring: n-1 reduce-scatter steps (rank r receives chunk r-s-2 from r-1 and folds it into its own copy), then n-1
 // all-gather steps; rank r owns chunk r. Pieces pipeline the steps.
 void AllReduceRing(const ScheduleParams& p, Builder& b)
@@ -843,12 +1013,20 @@ bool IsPow2(uint32_t n) { return n != 0 && (n & (n - 1)) == 0; }
 
 }  // namespace
 
-int32_t SelectAlgo(int32_t opType, uint32_t nRanks, uint64_t bytes)
+int32_t SelectAlgo(int32_t opType, uint32_t nRanks, uint64_t bytes, bool special)
 {
+    // DEFAULT_RANK_SIZE = 8.0 (auto_selector_base.h:28): AllReduce ratio 8/n/n, ReduceScatter (8/n)^2, in double
+    const double n = nRanks == 0 ? 8.0 : double(nRanks);
     switch (opType) {
         case HCCL_AMD_OP_ALLREDUCE:
-            return bytes <= kOneShotMaxBytes ? HCCL_AMD_ALGO_MESH_ONESHOT : HCCL_AMD_ALGO_MESH_TWOSHOT;
-        case HCCL_AMD_OP_REDUCE_SCATTER: return HCCL_AMD_ALGO_MESH_ONESHOT;
+            if (bytes <= kOneShotMaxBytes) return HCCL_AMD_ALGO_MESH_ONESHOT;
+            if (!special && double(bytes) * (8.0 / n / n) > double(32ull << 20)) return HCCL_AMD_ALGO_MESH_CHUNK;
+            return HCCL_AMD_ALGO_MESH_TWOSHOT;
+        case HCCL_AMD_OP_REDUCE_SCATTER:
+            if (!special && double(bytes) * (8.0 / n) * (8.0 / n) > double(16ull << 20)) {
+                return HCCL_AMD_ALGO_MESH_CHUNK;
+            }
+            return HCCL_AMD_ALGO_MESH_ONESHOT;
         case HCCL_AMD_OP_REDUCE:
             return bytes < kOneShotMaxBytes ? HCCL_AMD_ALGO_MESH_ONESHOT : HCCL_AMD_ALGO_MESH_TWOSHOT;
         case HCCL_AMD_OP_ALLGATHER: return HCCL_AMD_ALGO_MESH_ONESHOT;
@@ -865,7 +1043,7 @@ int BuildSchedule(const ScheduleParams& p, Schedule* out)
     Builder b;
     int32_t algo = p.algo;
     uint64_t bytes = p.count * p.elemSize;
-    if (algo == HCCL_AMD_ALGO_AUTO) algo = SelectAlgo(p.opType, p.nRanks, bytes);
+    if (algo == HCCL_AMD_ALGO_AUTO) algo = SelectAlgo(p.opType, p.nRanks, bytes, p.special);
     // The one-sided IPC collectives run as one kernel per executor loop, not as IR; their IR twins (same orders, same
     // bits) are the two-shot AllReduce / Reduce and the mesh ReduceScatter, which also run when the IPC path cannot.
     if (algo == HCCL_AMD_ALGO_IPC_TWOSHOT) algo = HCCL_AMD_ALGO_MESH_TWOSHOT;
@@ -887,6 +1065,7 @@ int BuildSchedule(const ScheduleParams& p, Schedule* out)
                 case HCCL_AMD_ALGO_RHD: AllReduceRhd(p, b); break;
                 case HCCL_AMD_ALGO_NHR: AllReduceNhr(p, b); break;
                 case HCCL_AMD_ALGO_ORDER_PRESERVED: AllReduceTree(p, b); break;
+                case HCCL_AMD_ALGO_MESH_CHUNK: AllReduceMeshChunk(p, b); break;
                 default: return HCCL_E_PARA;
             }
             break;
@@ -897,11 +1076,13 @@ int BuildSchedule(const ScheduleParams& p, Schedule* out)
                 case HCCL_AMD_ALGO_NHR: ReduceScatterNhr(p, b); break;
                 case HCCL_AMD_ALGO_RING: ReduceScatterRing(p, b); break;
                 case HCCL_AMD_ALGO_ORDER_PRESERVED: ReduceScatterTree(p, b); break;
+                case HCCL_AMD_ALGO_MESH_CHUNK: ReduceScatterMeshChunk(p, b); break;
                 default: return HCCL_E_PARA;
             }
             break;
         case HCCL_AMD_OP_REDUCE:
-            if (algo == HCCL_AMD_ALGO_RING || algo == HCCL_AMD_ALGO_RHD || algo == HCCL_AMD_ALGO_ORDER_PRESERVED) {
+            if (algo == HCCL_AMD_ALGO_RING || algo == HCCL_AMD_ALGO_RHD || algo == HCCL_AMD_ALGO_ORDER_PRESERVED ||
+                algo == HCCL_AMD_ALGO_MESH_CHUNK) {
                 algo = HCCL_AMD_ALGO_MESH_TWOSHOT;
             }
             switch (algo) {

@@ -24,6 +24,7 @@ struct ScheduleParams {
     uint64_t pieceBytes = 0;        // 0 = default
     uint64_t scratchCapBytes = 0;   // 0 = unbounded
     uint64_t cclBytes = 200ull << 20;  // HCCL_BUFFSIZE: sizes the reference's executor loops (see RefLoopElems)
+    bool special = false;  // INT64 / UINT64 / FP64 data or PROD: the selectors' isDataTypeOrReduceTypeSpecial
 };
 
 struct Schedule {
@@ -32,11 +33,13 @@ struct Schedule {
     uint64_t scratchElems = 0;
 };
 
-// Reference selector policy for a single-node full mesh (Level0Shape::MESH_1D):
-//   AllReduce  <= 8 MiB one-shot, else two-shot      all_reduce_auto_selector.cc:517-550
-//   ReduceScatter mesh                               reduce_scatter_auto_selector.cc:473-500
-//   Reduce     <  8 MiB one-shot mesh, else two-shot reduce_auto_selector.cc:312-324
-int32_t SelectAlgo(int32_t opType, uint32_t nRanks, uint64_t bytes);
+// Reference selector policy for a single-node full mesh (Level0Shape::MESH_1D, one net layer), bytes = count x size:
+//   AllReduce   special: <= 8 MiB one-shot, else two-shot; otherwise <= 8 MiB one-shot,
+//               bytes * 8/n^2 > 32 MiB MeshChunk, else two-shot            all_reduce_auto_selector.cc:517-550
+//   ReduceScatter (bytes of recvCount)  special: mesh; bytes * (8/n)^2 > 16 MiB MeshChunk, else mesh
+//                                                                            reduce_scatter_auto_selector.cc:473-512
+//   Reduce      <  8 MiB one-shot mesh, else two-shot                      reduce_auto_selector.cc:312-324
+int32_t SelectAlgo(int32_t opType, uint32_t nRanks, uint64_t bytes, bool special);
 
 // Returns HCCL_E_PARA for an invalid combination, HCCL_SUCCESS otherwise.
 int BuildSchedule(const ScheduleParams& p, Schedule* out);

@@ -100,7 +100,9 @@ typedef enum {
     HCCL_AMD_ALGO_RHD = 4,          /* recursive halving / doubling (power-of-two rank counts) */
     HCCL_AMD_ALGO_NHR = 5,          /* AllReduce: the reference's NHR template, order O5 (any rank count) */
     HCCL_AMD_ALGO_ORDER_PRESERVED = 6, /* AllReduce / ReduceScatter: HCCL_DETERMINISTIC=STRICT tree, order O4 */
-    HCCL_AMD_ALGO_IPC_TWOSHOT = 7      /* AllReduce: one kernel over peer-mapped staging (AIV GM_IN model), O2 */
+    HCCL_AMD_ALGO_IPC_TWOSHOT = 7,     /* AllReduce: one kernel over peer-mapped staging (AIV GM_IN model), O2 */
+    HCCL_AMD_ALGO_MESH_CHUNK = 8       /* AllReduce / ReduceScatter: the reference's MeshChunk templates, order O6
+                                          (owner first, then the peers in a per-sub-slice rotated order) */
 } HcclAmdAlgo;
 
 /* Build rank `rank`'s schedule. If ops == NULL only *numOps is written. scratchElems receives the number of
@@ -109,6 +111,11 @@ extern HcclResult HcclAmdBuildSchedule(int32_t opType, int32_t algo, uint32_t nR
                                        HcclDataType dataType, uint32_t root, uint64_t pieceBytes, HcclAmdIrOp* ops,
                                        uint64_t capacity, uint64_t* numOps, int32_t* algoUsed,
                                        uint64_t* scratchElems);
+
+/* The algorithm HCCL_AMD_ALGO_AUTO selects for an operation of `bytes` bytes per rank (ReduceScatter: recvCount
+ * bytes) on nRanks ranks; special = 64-bit data type or PROD (the reference selectors' isDataTypeOrReduceTypeSpecial).
+ * Mirrors AllReduceAutoSelector / ReduceScatterAutoSelector / ReduceAutoSelector for a single-node MESH_1D. */
+extern int32_t HcclAmdSelectAlgo(int32_t opType, uint32_t nRanks, uint64_t bytes, int32_t special);
 
 /* ---------------------------------------------------------------- communicator extensions */
 

@@ -8,6 +8,10 @@ or later operand is src, as in the reference's LocalReduce / write-reduce / read
   O2  two-shot AllReduce:                              acc = x_0;  acc = x_q (op) acc, q = 1 .. n-1
   ring (chunk c, owner c):   acc = x_{c+1}; acc = acc (op) x_{c+k}   (the travelling partial is src)
   RHD  pairwise: at distance d the kept half becomes partner_partial (op) my_partial
+  O6  MeshChunk AllReduce / ReduceScatter, sub-slice j of owner t: acc = x_t; acc = x_{t+o} (op) acc for the rank
+      offsets o = j+1 .. n-1, 1 .. j (ins_temp_all_reduce_mesh_1D_two_shot_mesh_chunk.cc:204-275,
+      ins_temp_reduce_scatter_mesh_1D_meshchunk.cc:190-252: in step s, sub-slice j of receiver t is written by sender
+      t + nextNum, nextNum = s + j + 1, plus one once it reaches n)
 """
 import numpy as np
 
@@ -312,7 +316,76 @@ def reduce_scatter_tree(dtype, op, xs, rc):
     return [tree_fold(dtype, op, [x[me * rc:(me + 1) * rc] for x in xs]) for me in range(n)]
 
 
-ALGO_ONESHOT, ALGO_TWOSHOT, ALGO_RING, ALGO_RHD, ALGO_NHR, ALGO_TREE, ALGO_IPC = 1, 2, 3, 4, 5, 6, 7
+def o6_peers(n, t, j):
+    """Senders into sub-slice j of owner t, step by step (nextNum = s + j + 1, skipping n)."""
+    out = []
+    for s in range(n - 1):
+        x = s + j + 1
+        if x >= n:
+            x += 1
+        out.append((t + x) % n)
+    return out
+
+
+def even_subslices(count, parts):
+    """…mesh_chunk.cc:166-183: `parts` slices, the first count % parts one element longer."""
+    base, big = divmod(count, parts)
+    out, b = [], 0
+    for i in range(parts):
+        ln = base + (1 if i < big else 0)
+        out.append((b, b + ln))
+        b += ln
+    return out
+
+
+def rs_subslices(count, parts, es):
+    """…meshchunk.cc:155-180: parts-1 slices of floor(bytes / parts) rounded down to 4 KiB, the rest last; the even
+    split when that leaves nothing (or parts < 2)."""
+    align = count * es // parts // 4096 * 4096
+    if parts < 2 or align == 0:
+        return even_subslices(count, parts)
+    a = align // es
+    return [(i * a, (i + 1) * a) for i in range(parts - 1)] + [((parts - 1) * a, count)]
+
+
+def allreduce_meshchunk(dtype, op, xs, ccl=None):
+    """MeshChunk AllReduce per executor loop (AICPU_TS bound = ccl, scratch multiple 2), chunks of ceil(cnt / n)
+    elements (no 128-B alignment), O6 per sub-slice."""
+    ccl = ccl_bytes_from_env() if ccl is None else ccl
+    n = len(xs)
+    es = xs[0].itemsize
+    out = np.empty_like(xs[0])
+    for off, cnt in ref_loops(xs[0].size, es, ccl, 2, ccl):
+        for t, (b, e) in enumerate(ceil_bounds(cnt, n)):
+            for j, (sb, se) in enumerate(even_subslices(e - b, n - 1)):
+                if se > sb:
+                    lo, hi = off + b + sb, off + b + se
+                    out[lo:hi] = fold(dtype, op, [xs[t][lo:hi]] + [xs[q][lo:hi] for q in o6_peers(n, t, j)])
+    return [out.copy() for _ in xs]
+
+
+def reduce_scatter_meshchunk(dtype, op, xs, rc, ccl=None):
+    """MeshChunk ReduceScatter per executor loop of min(ccl - 1 MiB, (ccl - 1 MiB) / (n-1)) over recvCount
+    (ins_v2_reduce_scatter_sole_executor.cc:32,160-175), 4-KiB sub-slices, O6 per sub-slice."""
+    ccl = ccl_bytes_from_env() if ccl is None else ccl
+    n = len(xs)
+    es = xs[0].itemsize
+    tmp = ccl - (1 << 20) if ccl > (1 << 20) else ccl
+    loop_bytes = min(tmp, tmp // (n - 1) // ALIGN * ALIGN)
+    per = max(1, loop_bytes // es)
+    outs = [np.empty(rc, xs[0].dtype) for _ in xs]
+    for off in range(0, rc, per):
+        cnt = min(per, rc - off)
+        for t in range(n):
+            for j, (sb, se) in enumerate(rs_subslices(cnt, n - 1, es)):
+                if se > sb:
+                    lo, hi = t * rc + off + sb, t * rc + off + se
+                    outs[t][off + sb:off + se] = fold(
+                        dtype, op, [xs[t][lo:hi]] + [xs[q][lo:hi] for q in o6_peers(n, t, j)])
+    return outs
+
+
+ALGO_ONESHOT, ALGO_TWOSHOT, ALGO_RING, ALGO_RHD, ALGO_NHR, ALGO_TREE, ALGO_IPC, ALGO_MESHCHUNK = 1, 2, 3, 4, 5, 6, 7, 8
 
 
 def expected(op_type, algo, dtype, op, xs, count, root=0):
@@ -320,10 +393,11 @@ def expected(op_type, algo, dtype, op, xs, count, root=0):
     if op_type == 0:
         return {ALGO_ONESHOT: allreduce_o1, ALGO_TWOSHOT: allreduce_o2, ALGO_RING: allreduce_ring,
                 ALGO_RHD: allreduce_rhd, ALGO_NHR: allreduce_nhr, ALGO_TREE: allreduce_tree,
-                ALGO_IPC: allreduce_o2}[algo](dtype, op, xs)
+                ALGO_IPC: allreduce_o2, ALGO_MESHCHUNK: allreduce_meshchunk}[algo](dtype, op, xs)
     if op_type == 1:
         return {ALGO_ONESHOT: reduce_scatter_o1, ALGO_RING: reduce_scatter_ring, ALGO_NHR: reduce_scatter_nhr,
-                ALGO_TREE: reduce_scatter_tree, ALGO_IPC: reduce_scatter_o1}[algo](dtype, op, xs, count)
+                ALGO_TREE: reduce_scatter_tree, ALGO_IPC: reduce_scatter_o1,
+                ALGO_MESHCHUNK: reduce_scatter_meshchunk}[algo](dtype, op, xs, count)
     if op_type == 3:
         full = np.concatenate([x[:count] for x in xs])
         return [full.copy() for _ in xs]

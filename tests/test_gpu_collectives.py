@@ -101,8 +101,8 @@ def oracle_replay(op_type, algo, n, count, dtype, op, xs, root, piece_bytes):
     return [b[1] for b in bufs]
 
 
-CASES = [(AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5), (AR, 6), (AR, 7), (RS, 1), (RS, 3), (RS, 5), (RS, 6),
-         (RS, 7), (RED, 1), (RED, 2), (RED, 5), (RED, 7), (AG, 1), (AG, 3)]
+CASES = [(AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5), (AR, 6), (AR, 7), (AR, 8), (RS, 1), (RS, 3), (RS, 5), (RS, 6),
+         (RS, 7), (RS, 8), (RED, 1), (RED, 2), (RED, 5), (RED, 7), (AG, 1), (AG, 3)]
 
 
 def ipc_status(comm):
@@ -243,8 +243,8 @@ def test_fp32_sum(worlds, op_type, algo, n, count, streams, monkeypatch):
 @pytest.mark.parametrize("dtype", [O.INT8, O.INT16, O.INT32, O.INT64, O.UINT64, O.FP16, O.BFP16, O.FP64],
                          ids=lambda v: O.DTYPE_NAMES[v])
 @pytest.mark.parametrize("op", O.OPS, ids=lambda v: O.OP_NAMES[v])
-@pytest.mark.parametrize("op_type,algo", [(AR, 1), (AR, 2), (AR, 3), (AR, 5), (AR, 7), (RS, 1), (RS, 5), (RS, 7),
-                                          (RED, 2), (RED, 5), (RED, 7)])
+@pytest.mark.parametrize("op_type,algo", [(AR, 1), (AR, 2), (AR, 3), (AR, 5), (AR, 7), (AR, 8), (RS, 1), (RS, 5),
+                                          (RS, 7), (RS, 8), (RED, 2), (RED, 5), (RED, 7)])
 def test_dtypes_ops(worlds, op_type, algo, dtype, op):
     n, count, root = 4, 40961, 2
     comms = worlds(n)
@@ -263,7 +263,7 @@ def test_dtypes_ops(worlds, op_type, algo, dtype, op):
         assert O.equal_bits(dtype, outs[r], want[r]), r
 
 
-@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_allreduce_inplace(worlds, algo):
     n, count = 4, 300007
     comms = worlds(n)
@@ -284,6 +284,26 @@ def test_default_selection_large_allreduce(worlds):
     want = R.expected(AR, used, O.FP32, O.SUM, xs, count)
     for r in range(n):
         assert O.equal_bits(O.FP32, outs[r], want[r]), r
+
+
+@pytest.mark.parametrize("op_type,n,count", [(AR, 2, (17 << 20) // 4 + 3), (RS, 4, (4 << 20) // 4 + 5)])
+def test_default_selection_meshchunk(monkeypatch, op_type, n, count):
+    """Auto selection picks MeshChunk where the reference does (AllReduce bytes * 8/n^2 > 32 MiB, ReduceScatter
+    recv bytes * (8/n)^2 > 16 MiB) and reproduces its order O6 over several executor loops (HCCL_BUFFSIZE = 4 MB)."""
+    monkeypatch.setenv("HCCL_BUFFSIZE", "4")
+    comms = H.loopback_world(n)
+    try:
+        in_count = count * n if op_type == RS else count
+        xs = [O.random_operands(O.FP32, in_count, seed=450 + r, edge=False) for r in range(n)]
+        used, outs = collective(comms, op_type, 0, O.FP32, O.SUM, xs, count)
+        assert used == R.ALGO_MESHCHUNK
+        want = R.expected(op_type, used, O.FP32, O.SUM, xs, count)
+        for r in range(n):
+            assert O.equal_bits(O.FP32, outs[r], want[r]), r
+    finally:
+        torch.cuda.synchronize()
+        for c in comms:
+            c.destroy()
 
 
 def test_reference_sample_known_answer(worlds):

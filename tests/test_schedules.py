@@ -50,8 +50,8 @@ def run(op_type, algo, n, count, dtype, op, root=0, piece_bytes=0, inplace=False
 
 
 CASES = [
-    (AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5), (AR, 6),
-    (RS, 1), (RS, 3), (RS, 5), (RS, 6),
+    (AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5), (AR, 6), (AR, 8),
+    (RS, 1), (RS, 3), (RS, 5), (RS, 6), (RS, 8),
     (RED, 1), (RED, 2), (RED, 5),
     (AG, 1), (AG, 3),
 ]
@@ -113,7 +113,7 @@ def test_order_preserved_tree_matches_o4():
         assert O.equal_bits(O.FP32, outs[me], want), me
 
 
-@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5, 6, 8])
 def test_allreduce_inplace(algo):
     n, count = 4, 50000
     used, xs, outs = run(AR, algo, n, count, O.FP32, O.SUM, piece_bytes=8192, inplace=True, seed=3)
@@ -130,6 +130,57 @@ def test_auto_selection_follows_reference_thresholds():
     assert programs(RS, 0, 8, 1024, O.FP32)[1] == R.ALGO_ONESHOT
     assert programs(RED, 0, 8, 8 * mib // 4 - 1, O.FP32)[1] == R.ALGO_ONESHOT   # < 8 MiB
     assert programs(RED, 0, 8, 8 * mib // 4, O.FP32)[1] == R.ALGO_TWOSHOT
+
+
+def test_auto_selection_meshchunk_thresholds():
+    """MeshChunk (all_reduce_auto_selector.cc:546-548: bytes * 8/n/n > 32 MiB, DEFAULT_RANK_SIZE = 8.0 in double;
+    reduce_scatter_auto_selector.cc:491-495,512: recv bytes * (8/n)^2 > 16 MiB), never for 64-bit data (or PROD)."""
+    mib = 1 << 20
+    assert H.select_algo(AR, 8, 256 * mib, False) == R.ALGO_TWOSHOT              # 256 MiB * 1/8 = 32 MiB, not >
+    assert H.select_algo(AR, 8, 256 * mib + 4, False) == R.ALGO_MESHCHUNK
+    assert H.select_algo(AR, 8, 4 << 30, False) == R.ALGO_MESHCHUNK               # C3
+    assert H.select_algo(AR, 8, 4 << 30, True) == R.ALGO_TWOSHOT                  # FP64 / INT64 / PROD
+    assert H.select_algo(AR, 2, 16 * mib + 4, False) == R.ALGO_MESHCHUNK          # ratio 2 at n = 2
+    assert H.select_algo(AR, 2, 16 * mib, False) == R.ALGO_TWOSHOT
+    assert H.select_algo(AR, 3, 36 * mib, False) == R.ALGO_TWOSHOT                # 36 MiB * 8/9 = 32 MiB, not >
+    assert H.select_algo(AR, 3, 37 * mib, False) == R.ALGO_MESHCHUNK
+    assert H.select_algo(RS, 8, 16 * mib, False) == R.ALGO_ONESHOT
+    assert H.select_algo(RS, 8, 16 * mib + 2, False) == R.ALGO_MESHCHUNK          # C4: 256 MiB per rank
+    assert H.select_algo(RS, 4, 4 * mib + 2, False) == R.ALGO_MESHCHUNK          # ratio 4
+    assert H.select_algo(RS, 8, 1 << 30, True) == R.ALGO_ONESHOT
+    assert H.select_algo(RED, 8, 1 << 30, False) == R.ALGO_TWOSHOT
+    # through the schedule builder (special = 64-bit data type)
+    assert programs(AR, 0, 8, 64 * mib + 1, O.FP32)[1] == R.ALGO_MESHCHUNK
+    assert programs(AR, 0, 8, 32 * mib + 1, O.FP64)[1] == R.ALGO_TWOSHOT
+
+
+def test_meshchunk_o6_closed_form_n8():
+    """O6 written out for n = 8: sub-slice j of owner t folds x_t, then x_{t+j+1}, ..., x_{t+7}, x_{t+1}, ..., x_{t+j}."""
+    n, count = 8, 8 * 7 * 3 + 5
+    used, xs, outs = run(AR, 8, n, count, O.FP32, O.SUM, piece_bytes=256, seed=61)
+    assert used == R.ALGO_MESHCHUNK
+    cs = -(-count // n)
+    for t in range(n):
+        b, e = t * cs, min(count, (t + 1) * cs)
+        subs = R.even_subslices(e - b, n - 1)
+        for j, (sb, se) in enumerate(subs):
+            order = [t] + [(t + o) % n for o in list(range(j + 1, n)) + list(range(1, j + 1))]
+            assert order == [t] + R.o6_peers(n, t, j)
+            want = R.fold(O.FP32, O.SUM, [xs[q][b + sb:b + se] for q in order])
+            for r in range(n):
+                assert O.equal_bits(O.FP32, outs[r][b + sb:b + se], want), (t, j, r)
+
+
+@pytest.mark.parametrize("op_type,n,count", [(AR, 3, 300007), (AR, 8, 140001), (RS, 3, 200003), (RS, 8, 70001),
+                                              (AR, 2, 262147), (RS, 2, 300001)])
+def test_meshchunk_follows_executor_loops(monkeypatch, op_type, n, count):
+    """HCCL_BUFFSIZE = 1 MB: AllReduce loops of 512 KiB, ReduceScatter loops of 1 MiB / (n-1); every loop is sliced
+    into chunks and sub-slices on its own, which decides each element's O6 rotation."""
+    monkeypatch.setenv("HCCL_BUFFSIZE", "1")
+    used, xs, outs = run(op_type, 8, n, count, O.FP32, O.SUM, piece_bytes=64 << 10, seed=n)
+    want = R.expected(op_type, used, O.FP32, O.SUM, xs, count)
+    for r in range(n):
+        assert O.equal_bits(O.FP32, outs[r], want[r]), r
 
 
 def test_rhd_non_power_of_two_falls_back_to_ring():
