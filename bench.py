@@ -305,23 +305,62 @@ def bench_c4(comm, send, recv, world) -> dict:
 
 
 def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
-    """C5: AllReduce fp16 SUM with the RHD schedule, 1 KiB .. 4 GiB: latency at small sizes, busbw at large."""
-    comm.set_algo(H.Algo.RHD)
+    """C5: AllReduce fp16 SUM, 1 KiB .. 4 GiB: latency at small sizes, busbw at large. Each size runs the RHD schedule
+    (the config's algorithm) and the auto selection (what the reference would run: one-shot / two-shot / MeshChunk)."""
     s = torch.cuda.current_stream()
     rows = []
     nbytes = 1 << 10
+    f = 2 * (world - 1) / world
     try:
         while nbytes <= max_bytes:
             a = send.view(torch.float16)[: nbytes // 2]
             b = recv.view(torch.float16)[: nbytes // 2]
             iters = 20 if nbytes <= (64 << 20) else 3
-            t = _timed(lambda: comm.all_reduce(a, b, H.HcclReduceOp.SUM, s), iters)
-            rows.append({"bytes": nbytes, "us": round(t * 1e6, 1),
-                         "busbw_GBps": round(nbytes / t / 1e9 * 2 * (world - 1) / world, 2)})
+            row = {"bytes": nbytes}
+            for algo in (H.Algo.RHD, H.Algo.AUTO):
+                comm.set_algo(algo)
+                t = _timed(lambda: comm.all_reduce(a, b, H.HcclReduceOp.SUM, s), iters)
+                key = "rhd" if algo == H.Algo.RHD else "auto"
+                row[f"{key}_us"] = round(t * 1e6, 1)
+                row[f"{key}_busbw_GBps"] = round(nbytes / t / 1e9 * f, 2)
+                if algo == H.Algo.AUTO:
+                    row["auto_algo"] = H.Algo(comm.last_algo).name
+            rows.append(row)
             nbytes *= 2
     finally:
         comm.set_algo(H.Algo.AUTO)
-    return {"workload": "C5: AllReduce fp16 SUM, RHD schedule, size sweep", "algo": "RHD", "points": rows}
+    return {"workload": "C5: AllReduce fp16 SUM, size sweep (RHD schedule and auto selection)", "points": rows}
+
+
+def bench_e2e_allreduce(comm, world, nbytes: int = 256 << 20, iters: int = 5) -> dict:
+    """Gradient bucket that starts and ends in host memory (BASELINE.json): pinned H2D, HcclAllReduce fp32 SUM, D2H,
+    all on one stream; nbytes per rank. Rate = bucket bytes per rank / max-over-ranks time per step."""
+    import torch.distributed as dist
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    h = torch.empty(nbytes // 4, dtype=torch.float32).pin_memory()
+    h.uniform_(-1, 1)
+    d = torch.empty(nbytes // 4, device=dev)
+    s = torch.cuda.current_stream()
+
+    def step():
+        d.copy_(h, non_blocking=True)
+        comm.all_reduce(d, d, H.HcclReduceOp.SUM, s)
+        h.copy_(d, non_blocking=True)
+
+    step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        step()
+    torch.cuda.synchronize()
+    t = torch.tensor([(time.perf_counter() - t0) / iters], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    per = float(t[0])
+    return {"bytes_per_rank": nbytes, "ms_per_step": round(per * 1e3, 3), "GiBps_per_rank": round(nbytes / per / GIB, 2),
+            "algo": H.Algo(comm.last_algo).name,
+            "note": "pinned host bucket -> H2D -> in-place HcclAllReduce -> D2H on one stream (PCIe-bound)"}
 
 
 def bench_c3_algos(comm, send, recv, world) -> dict:
@@ -425,7 +464,8 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     if not args.no_extra_configs:
         for name, fn in (("c3_schedules", lambda: bench_c3_algos(comm, send, recv, world)),
                          ("c4", lambda: bench_c4(comm, send, recv, world)),
-                         ("c5", lambda: bench_c5(comm, send, recv, world))):
+                         ("c5", lambda: bench_c5(comm, send, recv, world)),
+                         ("end_to_end_host_buffers", lambda: bench_e2e_allreduce(comm, world))):
             try:
                 extra[name] = fn()
             except Exception as e:  # noqa: BLE001  (a secondary config never hides the headline line)
