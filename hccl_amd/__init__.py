@@ -114,6 +114,14 @@ def select_algo(op_type: int, n_ranks: int, nbytes: int, special: bool = False) 
     return lib.HcclAmdSelectAlgo(int(op_type), n_ranks, nbytes, 1 if special else 0)
 
 
+def ring_table(n_ranks: int) -> List[List[int]]:
+    """The directed rings of HCCL_AMD_ALGO_RING (HcclAmdRingTable), as rank lists."""
+    r = lib.HcclAmdRingTable(n_ranks, None, 0)
+    buf = (ctypes.c_uint32 * max(1, r * n_ranks))()
+    lib.HcclAmdRingTable(n_ranks, buf, r)
+    return [list(buf[k * n_ranks:(k + 1) * n_ranks]) for k in range(r)]
+
+
 # ----------------------------------------------------------------------------------------- communicators
 
 

@@ -6,7 +6,8 @@
 //       reduce_mesh_1D.cc:232-246, reduce_mesh_1D_two_shot.cc:226-247
 //   two-shot AllReduce                               O2: acc = x_0, then x_1 .. x_{n-1}
 //       ins_temp_all_reduce_mesh_1D_two_shot.cc:312-338
-//   ring (build-side; the reference has no ring AllReduce template)   chunk c: acc = x_{c+1}, then x_{c+2} .. x_c
+//   rings (build-side; the reference has no ring AllReduce template): R arc-disjoint Hamiltonian cycles, part k on
+//       ring k; chunk at position c: acc = x_{cyc[c+1]}, then x_{cyc[c+2]} .. x_{cyc[c]}
 //   RHD (docs/zh/user_guide/coll_algo_intro/RHD.md)  pairwise tree, partner = rank ^ d, d = n/2, n/4, .., 1
 //   NHR AllReduce                                    O5: ins_temp_all_reduce_nhr.cc:230-301, 390-482
 //
@@ -459,39 +460,136 @@ void ReduceScatterMeshChunk(const ScheduleParams& p, Builder& b)
     }
 }
 
-// Ring: n-1 reduce-scatter steps (rank r receives chunk r-s-2 from r-1 and folds it into its own copy), then n-1
-// all-gather steps; rank r owns chunk r. Pieces pipeline the steps.
+// ------------------------------------------------------------------------------------------- rings over xGMI
+//
+// xGMI is point to point: a single directed ring moves every byte over ONE link per rank, 1/7 of what an 8-GPU
+// node offers. The ring schedules therefore run R arc-disjoint directed Hamiltonian cycles at once (RingTable):
+// the complete digraph on n ranks decomposes into n-1 of them for n != 4, 6 (Tillson), so at n = 8 seven rings use
+// all seven outgoing and incoming links of every GPU. The buffer is split into R parts; part k travels around ring
+// k. Inside a ring, ranks are addressed by their position v on the cycle (rank = cycle[v]), which is the reference's
+// ring neighbour convention prev = v-1, next = v+1 (scatter_ring.cc:186-187) applied to the cycle.
+
+// The rings for n ranks (every rank computes the same table): found by search and checked in tests/test_schedules.py
+// (each is a Hamiltonian cycle, no arc is used twice); n > 8: the rotations v -> v + k with gcd(k, n) = 1.
+}  // namespace
+
+std::vector<std::vector<uint32_t>> RingTable(uint32_t n)
+{
+    switch (n) {
+        case 1: return {{0}};
+        case 2: return {{0, 1}};
+        case 3: return {{0, 1, 2}, {0, 2, 1}};
+        case 4: return {{0, 1, 3, 2}, {0, 2, 3, 1}};
+        case 5: return {{0, 3, 1, 2, 4}, {0, 1, 4, 3, 2}, {0, 4, 2, 1, 3}, {0, 2, 3, 4, 1}};
+        case 6: return {{0, 3, 1, 2, 5, 4}, {0, 4, 5, 2, 1, 3}, {0, 2, 3, 4, 1, 5}, {0, 5, 1, 4, 3, 2}};
+        case 7:
+            return {{0, 5, 1, 6, 4, 3, 2}, {0, 2, 3, 6, 1, 4, 5}, {0, 3, 1, 2, 5, 4, 6}, {0, 4, 1, 5, 2, 6, 3},
+                    {0, 1, 3, 5, 6, 2, 4}, {0, 6, 5, 3, 4, 2, 1}};
+        case 8:
+            return {{0, 5, 6, 3, 7, 2, 1, 4}, {0, 4, 2, 3, 5, 7, 1, 6}, {0, 3, 2, 7, 5, 4, 6, 1},
+                    {0, 7, 6, 2, 4, 1, 5, 3}, {0, 2, 6, 5, 1, 3, 4, 7}, {0, 1, 7, 3, 6, 4, 5, 2},
+                    {0, 6, 7, 4, 3, 1, 2, 5}};
+        default: {
+            std::vector<std::vector<uint32_t>> t;
+            for (uint32_t k = 1; k < n; ++k) {
+                uint32_t a = k, bb = n;
+                while (bb != 0) {
+                    const uint32_t r = a % bb;
+                    a = bb;
+                    bb = r;
+                }
+                if (a != 1) continue;
+                std::vector<uint32_t> c;
+                for (uint32_t v = 0; v < n; ++v) c.push_back(uint32_t((uint64_t(v) * k) % n));
+                t.push_back(c);
+            }
+            return t;
+        }
+    }
+}
+
+namespace {
+
+// One ring of the table as seen from rank `me`: its cycle and my position on it.
+struct RingView {
+    std::vector<uint32_t> cyc;
+    uint32_t pos;
+    uint32_t At(int64_t v) const
+    {
+        const int64_t n = int64_t(cyc.size());
+        return cyc[size_t(((v % n) + n) % n)];
+    }
+    uint32_t Next() const { return At(int64_t(pos) + 1); }
+    uint32_t Prev() const { return At(int64_t(pos) - 1); }
+};
+
+std::vector<RingView> Rings(uint32_t n, uint32_t me)
+{
+    std::vector<RingView> v;
+    for (auto& c : RingTable(n)) {
+        RingView r{c, 0};
+        for (uint32_t i = 0; i < n; ++i) {
+            if (c[i] == me) r.pos = i;
+        }
+        v.push_back(r);
+    }
+    return v;
+}
+
+// Part k of R of a buffer of `count` elements: ceil(count / R) rounded up to 128 B; trailing parts short or empty.
+Span RingPart(uint64_t count, uint32_t R, uint32_t k, uint64_t alignElems) { return Chunk(count, R, k, alignElems); }
+
+// AllReduce over R rings: in part k, position v owns chunk v; n-1 reduce-scatter steps (position v receives chunk
+// v-s-2 from v-1 and folds it into its own copy: acc = travelling partial (src) (op) own input), then n-1 all-gather
+// steps. Every step posts all rings' transfers in one group; pieces pipeline the steps.
 void AllReduceRing(const ScheduleParams& p, Builder& b)
 {
     const uint32_t n = p.nRanks, me = p.rank;
     const uint64_t alignElems = std::max<uint64_t>(1, kAlignBytes / p.elemSize);
+    const std::vector<RingView> rings = Rings(n, me);
+    const uint32_t R = static_cast<uint32_t>(rings.size());
     const uint64_t kSlots = 4;
-    const uint64_t maxChunk = Chunk(p.count, n, 0, alignElems).len;
-    const uint64_t pe = PieceElems(p, maxChunk, kSlots);
+    const Span part0 = RingPart(p.count, R, 0, alignElems);
+    const uint64_t maxChunk = Chunk(part0.len, n, 0, alignElems).len;
+    const uint64_t pe = PieceElems(p, maxChunk, kSlots * R);
     const uint64_t np = std::max<uint64_t>(1, CeilDiv(maxChunk, pe));
-    const uint32_t next = (me + 1) % n, prev = (me + n - 1) % n;
+    auto chunkOf = [&](uint32_t k, uint32_t c) {
+        const Span part = RingPart(p.count, R, k, alignElems);
+        Span ch = Chunk(part.len, n, c, alignElems);
+        ch.begin += part.begin;
+        return ch;
+    };
     uint64_t unit = 0;
     for (uint32_t s = 0; s + 1 < n; ++s) {
-        const uint32_t cs = (me + 2 * n - s - 1) % n;
-        const uint32_t cr = (me + 2 * n - s - 2) % n;
         for (uint64_t t = 0; t < np; ++t, ++unit) {
-            Span snd = Piece(Chunk(p.count, n, cs, alignElems), pe, t);
-            Span rcv = Piece(Chunk(p.count, n, cr, alignElems), pe, t);
-            Ref stage = Scr((unit % kSlots) * pe);
-            b.Send(next, s == 0 ? In(snd.begin) : Out(snd.begin), snd.len);
-            b.Recv(prev, stage, rcv.len);
+            for (uint32_t k = 0; k < R; ++k) {
+                const RingView& r = rings[k];
+                const uint32_t cs = (r.pos + 2 * n - s - 1) % n;
+                const uint32_t cr = (r.pos + 2 * n - s - 2) % n;
+                const Span snd = Piece(chunkOf(k, cs), pe, t);
+                const Span rcv = Piece(chunkOf(k, cr), pe, t);
+                b.Send(r.Next(), s == 0 ? In(snd.begin) : Out(snd.begin), snd.len);
+                b.Recv(r.Prev(), Scr(((unit % kSlots) * R + k) * pe), rcv.len);
+            }
             b.EndGroup();
-            b.Reduce(Out(rcv.begin), {In(rcv.begin), stage}, rcv.len);
+            for (uint32_t k = 0; k < R; ++k) {
+                const uint32_t cr = (rings[k].pos + 2 * n - s - 2) % n;
+                const Span rcv = Piece(chunkOf(k, cr), pe, t);
+                b.Reduce(Out(rcv.begin), {In(rcv.begin), Scr(((unit % kSlots) * R + k) * pe)}, rcv.len);
+            }
         }
     }
     for (uint32_t s = 0; s + 1 < n; ++s) {
-        const uint32_t cs = (me + n - s) % n;
-        const uint32_t cr = (me + 2 * n - s - 1) % n;
         for (uint64_t t = 0; t < np; ++t) {
-            Span snd = Piece(Chunk(p.count, n, cs, alignElems), pe, t);
-            Span rcv = Piece(Chunk(p.count, n, cr, alignElems), pe, t);
-            b.Send(next, Out(snd.begin), snd.len);
-            b.Recv(prev, Out(rcv.begin), rcv.len);
+            for (uint32_t k = 0; k < R; ++k) {
+                const RingView& r = rings[k];
+                const uint32_t cs = (r.pos + n - s) % n;
+                const uint32_t cr = (r.pos + 2 * n - s - 1) % n;
+                const Span snd = Piece(chunkOf(k, cs), pe, t);
+                const Span rcv = Piece(chunkOf(k, cr), pe, t);
+                b.Send(r.Next(), Out(snd.begin), snd.len);
+                b.Recv(r.Prev(), Out(rcv.begin), rcv.len);
+            }
             b.EndGroup();
         }
     }
@@ -800,31 +898,43 @@ void ReduceScatterMesh(const ScheduleParams& p, Builder& b)
     }
 }
 
-// Ring reduce-scatter: step s, rank r sends block r-s-1 (its partial) to r+1 and folds block r-s-2 received from
-// r-1 into its own input; partials live in staging slots until forwarded, the last step writes recvBuf. Rounds of
-// kRound pieces bound the staging to 2 * kRound pieces.
+// Ring reduce-scatter over R rings: every block is split into R parts and part k of every block travels around ring
+// k. Step s, position v sends block cycle[v-s-1] (its partial) to v+1 and folds block cycle[v-s-2] received from v-1
+// into its own input (acc = travelling partial (src) (op) own input); position v ends with block cycle[v] = its own.
+// Partials live in staging until forwarded, the last step writes recvBuf. Rounds of kRound pieces bound the staging.
 void ReduceScatterRing(const ScheduleParams& p, Builder& b)
 {
     const uint32_t n = p.nRanks, me = p.rank;
     const uint64_t rc = p.count;
+    const uint64_t alignElems = std::max<uint64_t>(1, kAlignBytes / p.elemSize);
+    const std::vector<RingView> rings = Rings(n, me);
+    const uint32_t R = static_cast<uint32_t>(rings.size());
     const uint64_t kRound = 4;
-    const uint64_t pe = PieceElems(p, rc, 2 * kRound);
-    const uint64_t np = std::max<uint64_t>(1, CeilDiv(rc, pe));
-    const uint32_t next = (me + 1) % n, prev = (me + n - 1) % n;
+    const uint64_t maxPart = RingPart(rc, R, 0, alignElems).len;
+    const uint64_t pe = PieceElems(p, maxPart, 2 * kRound * R);
+    const uint64_t np = std::max<uint64_t>(1, CeilDiv(maxPart, pe));
+    auto slotAt = [&](uint32_t parity, uint32_t k, uint64_t tr) { return Scr(((parity * R + k) * kRound + tr) * pe); };
     for (uint64_t r0 = 0; r0 < np; r0 += kRound) {
         const uint64_t r1 = std::min(np, r0 + kRound);
         for (uint32_t s = 0; s + 1 < n; ++s) {
-            const uint32_t cs = (me + 2 * n - s - 1) % n;
-            const uint32_t cr = (me + 2 * n - s - 2) % n;
             for (uint64_t t = r0; t < r1; ++t) {
-                Span piece = Piece({0, rc}, pe, t);
-                Ref cur = Scr(((s % 2) * kRound + (t - r0)) * pe);
-                Ref prevSlot = Scr((((s + 1) % 2) * kRound + (t - r0)) * pe);
-                b.Send(next, s == 0 ? In(uint64_t(cs) * rc + piece.begin) : prevSlot, piece.len);
-                b.Recv(prev, cur, piece.len);
+                for (uint32_t k = 0; k < R; ++k) {
+                    const RingView& r = rings[k];
+                    const uint32_t bs = r.At(int64_t(r.pos) - s - 1);
+                    const Span piece = Piece(RingPart(rc, R, k, alignElems), pe, t);
+                    b.Send(r.Next(), s == 0 ? In(uint64_t(bs) * rc + piece.begin) : slotAt((s + 1) % 2, k, t - r0),
+                           piece.len);
+                    b.Recv(r.Prev(), slotAt(s % 2, k, t - r0), piece.len);
+                }
                 b.EndGroup();
-                Ref dst = (s + 2 == n) ? Out(piece.begin) : cur;
-                b.Reduce(dst, {In(uint64_t(cr) * rc + piece.begin), cur}, piece.len);
+                for (uint32_t k = 0; k < R; ++k) {
+                    const RingView& r = rings[k];
+                    const uint32_t br = r.At(int64_t(r.pos) - s - 2);
+                    const Span piece = Piece(RingPart(rc, R, k, alignElems), pe, t);
+                    const Ref cur = slotAt(s % 2, k, t - r0);
+                    b.Reduce((s + 2 == n) ? Out(piece.begin) : cur, {In(uint64_t(br) * rc + piece.begin), cur},
+                             piece.len);
+                }
             }
         }
     }
@@ -988,22 +1098,29 @@ void AllGatherMesh(const ScheduleParams& p, Builder& b)
     }
 }
 
-// Ring: step s forwards block me-s to me+1 and receives block me-s-1 from me-1.
+// All-gather over R rings: part k of every block travels around ring k; step s forwards block cycle[v-s] to v+1 and
+// receives block cycle[v-s-1] from v-1.
 void AllGatherRing(const ScheduleParams& p, Builder& b)
 {
     const uint32_t n = p.nRanks, me = p.rank;
     const uint64_t sc = p.count;
-    const uint64_t pe = PieceElems(p, sc, 0);
-    const uint64_t np = std::max<uint64_t>(1, CeilDiv(sc, pe));
-    const uint32_t next = (me + 1) % n, prev = (me + n - 1) % n;
+    const uint64_t alignElems = std::max<uint64_t>(1, kAlignBytes / p.elemSize);
+    const std::vector<RingView> rings = Rings(n, me);
+    const uint32_t R = static_cast<uint32_t>(rings.size());
+    const uint64_t maxPart = RingPart(sc, R, 0, alignElems).len;
+    const uint64_t pe = PieceElems(p, maxPart, 0);
+    const uint64_t np = std::max<uint64_t>(1, CeilDiv(maxPart, pe));
     b.Copy(Out(uint64_t(me) * sc), In(0), sc);
     for (uint32_t s = 0; s + 1 < n; ++s) {
-        const uint32_t cs = (me + n - s) % n;
-        const uint32_t cr = (me + 2 * n - s - 1) % n;
         for (uint64_t t = 0; t < np; ++t) {
-            Span piece = Piece({0, sc}, pe, t);
-            b.Send(next, s == 0 ? In(piece.begin) : Out(uint64_t(cs) * sc + piece.begin), piece.len);
-            b.Recv(prev, Out(uint64_t(cr) * sc + piece.begin), piece.len);
+            for (uint32_t k = 0; k < R; ++k) {
+                const RingView& r = rings[k];
+                const uint32_t bs = r.At(int64_t(r.pos) - s);
+                const uint32_t br = r.At(int64_t(r.pos) - s - 1);
+                const Span piece = Piece(RingPart(sc, R, k, alignElems), pe, t);
+                b.Send(r.Next(), s == 0 ? In(piece.begin) : Out(uint64_t(bs) * sc + piece.begin), piece.len);
+                b.Recv(r.Prev(), Out(uint64_t(br) * sc + piece.begin), piece.len);
+            }
             b.EndGroup();
         }
     }

@@ -41,6 +41,9 @@ struct Schedule {
 //   Reduce      <  8 MiB one-shot mesh, else two-shot                      reduce_auto_selector.cc:312-324
 int32_t SelectAlgo(int32_t opType, uint32_t nRanks, uint64_t bytes, bool special);
 
+// The directed rings the ring schedules run for n ranks: arc-disjoint Hamiltonian cycles (rank lists).
+std::vector<std::vector<uint32_t>> RingTable(uint32_t n);
+
 // Returns HCCL_E_PARA for an invalid combination, HCCL_SUCCESS otherwise.
 int BuildSchedule(const ScheduleParams& p, Schedule* out);
 

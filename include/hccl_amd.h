@@ -117,6 +117,11 @@ extern HcclResult HcclAmdBuildSchedule(int32_t opType, int32_t algo, uint32_t nR
  * Mirrors AllReduceAutoSelector / ReduceScatterAutoSelector / ReduceAutoSelector for a single-node MESH_1D. */
 extern int32_t HcclAmdSelectAlgo(int32_t opType, uint32_t nRanks, uint64_t bytes, int32_t special);
 
+/* The rings HCCL_AMD_ALGO_RING runs on nRanks ranks: arc-disjoint directed Hamiltonian cycles (n-1 of them for
+ * n <= 8 except 4 and 6, where n-2 is the maximum). Writes up to `capacity` cycles of nRanks ranks each, row-major,
+ * into cycles (may be NULL) and returns the number of rings (0 for nRanks == 0). */
+extern int32_t HcclAmdRingTable(uint32_t nRanks, uint32_t* cycles, uint32_t capacity);
+
 /* ---------------------------------------------------------------- communicator extensions */
 
 /* nRanks communicators on the current HIP device, joined by device-to-device copies. comms[r] is rank r.

@@ -6,7 +6,8 @@ or later operand is src, as in the reference's LocalReduce / write-reduce / read
 
   O1  one-shot AllReduce, mesh ReduceScatter, Reduce:  acc = x_me; acc = x_q (op) acc, q ascending, q != me
   O2  two-shot AllReduce:                              acc = x_0;  acc = x_q (op) acc, q = 1 .. n-1
-  ring (chunk c, owner c):   acc = x_{c+1}; acc = acc (op) x_{c+k}   (the travelling partial is src)
+  rings (R arc-disjoint Hamiltonian cycles, part k on ring k; chunk at position c):
+      acc = x_{cyc[c+1]}; acc = acc (op) x_{cyc[c+k]}   (the travelling partial is src)
   RHD  pairwise: at distance d the kept half becomes partner_partial (op) my_partial
   O6  MeshChunk AllReduce / ReduceScatter, sub-slice j of owner t: acc = x_t; acc = x_{t+o} (op) acc for the rank
       offsets o = j+1 .. n-1, 1 .. j (ins_temp_all_reduce_mesh_1D_two_shot_mesh_chunk.cc:204-275,
@@ -98,21 +99,36 @@ def allreduce_o2(dtype, op, xs):
     return [r.copy() for _ in xs]
 
 
-def ring_chunk(dtype, op, xs, c, sl):
+def ring_table(n):
+    """The library's rings (HcclAmdRingTable); tests/test_schedules.py checks they are arc-disjoint Hamiltonian
+    cycles."""
+    import hccl_amd as H
+    return H.ring_table(n)
+
+
+def ring_parts(count, n_rings, es):
+    """Part k of the buffer travels around ring k (ceil split, 128-B aligned, as chunk_bounds)."""
+    return chunk_bounds(count, n_rings, es)
+
+
+def ring_chunk(dtype, op, xs, cyc, c, sl):
+    """Chunk at ring position c: acc = x_{cyc[c+1]}; acc = acc (op) x_{cyc[c+k]} (the travelling partial is src)."""
     n = len(xs)
-    acc = xs[(c + 1) % n][sl].copy()
+    acc = xs[cyc[(c + 1) % n]][sl].copy()
     for k in range(2, n + 1):
-        acc = apply(dtype, op, acc, xs[(c + k) % n][sl])
+        acc = apply(dtype, op, acc, xs[cyc[(c + k) % n]][sl])
     return acc
 
 
 def allreduce_ring(dtype, op, xs):
     n = len(xs)
     es = xs[0].itemsize
+    rings = ring_table(n)
     out = np.empty_like(xs[0])
-    for c, (b, e) in enumerate(chunk_bounds(xs[0].size, n, es)):
-        if e > b:
-            out[b:e] = ring_chunk(dtype, op, xs, c, slice(b, e))
+    for k, (pb, pe) in enumerate(ring_parts(xs[0].size, len(rings), es)):
+        for c, (b, e) in enumerate(chunk_bounds(pe - pb, n, es)):
+            if e > b:
+                out[pb + b:pb + e] = ring_chunk(dtype, op, xs, rings[k], c, slice(pb + b, pb + e))
     return [out.copy() for _ in xs]
 
 
@@ -255,14 +271,22 @@ def reduce_scatter_o1(dtype, op, xs, rc):
 
 
 def reduce_scatter_ring(dtype, op, xs, rc):
+    """Part k of every block travels ring k; rank me at position v gets acc = x_{cyc[v+1]}, then (op) x_{cyc[v+2]}
+    .. x_{cyc[v+n]} = its own block, the travelling partial being src."""
     n = len(xs)
-    outs = []
-    for me in range(n):
-        blocks = [x[me * rc:(me + 1) * rc] for x in xs]
-        acc = blocks[(me + 1) % n].copy()
-        for k in range(2, n + 1):
-            acc = apply(dtype, op, acc, blocks[(me + k) % n])
-        outs.append(acc)
+    es = xs[0].itemsize
+    rings = ring_table(n)
+    outs = [np.empty(rc, xs[0].dtype) for _ in range(n)]
+    for k, (pb, pe) in enumerate(ring_parts(rc, len(rings), es)):
+        if pe <= pb:
+            continue
+        cyc = rings[k]
+        for v, me in enumerate(cyc):
+            sl = slice(me * rc + pb, me * rc + pe)
+            acc = xs[cyc[(v + 1) % n]][sl].copy()
+            for j in range(2, n + 1):
+                acc = apply(dtype, op, acc, xs[cyc[(v + j) % n]][sl])
+            outs[me][pb:pe] = acc
     return outs
 
 

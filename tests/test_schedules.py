@@ -183,6 +183,39 @@ def test_meshchunk_follows_executor_loops(monkeypatch, op_type, n, count):
         assert O.equal_bits(O.FP32, outs[r], want[r]), r
 
 
+@pytest.mark.parametrize("n", list(range(1, 17)))
+def test_ring_table_is_arc_disjoint_hamiltonian(n):
+    """Every ring visits every rank once, no directed link (arc) carries two rings, and the count is the maximum
+    (n-1: the complete digraph decomposes into Hamiltonian cycles for n != 4, 6 — Tillson) for n <= 8."""
+    rings = H.ring_table(n)
+    arcs = set()
+    for c in rings:
+        assert sorted(c) == list(range(n)), c
+        if n > 1:
+            for i in range(n):
+                a = (c[i], c[(i + 1) % n])
+                assert a not in arcs, (n, a)
+                arcs.add(a)
+    if n == 1:
+        assert len(rings) == 1
+    elif n <= 8:
+        assert len(rings) == (n - 2 if n in (4, 6) else n - 1)
+    else:
+        import math
+        assert len(rings) == sum(1 for k in range(1, n) if math.gcd(k, n) == 1)
+
+
+def test_ring_uses_every_link_at_eight_ranks():
+    """At n = 8 every rank sends to and receives from all 7 peers in every ring step (one ring per link)."""
+    progs, used, _ = programs(AR, 3, 8, 1 << 16, O.FP32)
+    assert used == R.ALGO_RING
+    for arr, nops in progs:
+        first = [o for o in arr[:nops] if o.kind in (2, 3) and o.group == 0]
+        assert sorted(o.peer for o in first if o.kind == 2) == sorted(set(o.peer for o in first if o.kind == 2))
+        assert len({o.peer for o in first if o.kind == 2}) == 7
+        assert len({o.peer for o in first if o.kind == 3}) == 7
+
+
 def test_rhd_non_power_of_two_falls_back_to_ring():
     assert programs(AR, 4, 6, 1000, O.FP32)[1] == R.ALGO_RING
 
