@@ -122,6 +122,14 @@ def ring_table(n_ranks: int) -> List[List[int]]:
     return [list(buf[k * n_ranks:(k + 1) * n_ranks]) for k in range(r)]
 
 
+def rhd_table(n_ranks: int) -> List[List[int]]:
+    """The RHD instances (HcclAmdRhdTable): per instance, the real rank of each virtual rank."""
+    r = lib.HcclAmdRhdTable(n_ranks, None, 0)
+    buf = (ctypes.c_uint32 * max(1, r * n_ranks))()
+    lib.HcclAmdRhdTable(n_ranks, buf, r)
+    return [list(buf[k * n_ranks:(k + 1) * n_ranks]) for k in range(r)]
+
+
 # ----------------------------------------------------------------------------------------- communicators
 
 

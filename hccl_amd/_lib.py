@@ -147,6 +147,7 @@ SIGNATURES = {
     "HcclAmdGetErrorString": (ctypes.c_char_p, [_i32]),
     "HcclAmdSelectAlgo": (_i32, [_i32, _u32, _u64, _i32]),
     "HcclAmdRingTable": (_i32, [_u32, ctypes.POINTER(_u32), _u32]),
+    "HcclAmdRhdTable": (_i32, [_u32, ctypes.POINTER(_u32), _u32]),
     "HcclAmdBuildSchedule": (
         _res,
         [_i32, _i32, _u32, _u32, _u64, _i32, _u32, _u64, ctypes.POINTER(HcclAmdIrOp), _u64,

@@ -318,6 +318,16 @@ int32_t HcclAmdRingTable(uint32_t nRanks, uint32_t* cycles, uint32_t capacity)
     return static_cast<int32_t>(t.size());
 }
 
+int32_t HcclAmdRhdTable(uint32_t nRanks, uint32_t* realOfVirtual, uint32_t capacity)
+{
+    if (nRanks == 0) return 0;
+    const std::vector<std::vector<uint32_t>> t = RhdTable(nRanks);
+    for (uint32_t k = 0; realOfVirtual != nullptr && k < t.size() && k < capacity; ++k) {
+        std::memcpy(realOfVirtual + size_t(k) * nRanks, t[k].data(), nRanks * sizeof(uint32_t));
+    }
+    return static_cast<int32_t>(t.size());
+}
+
 int32_t HcclAmdSelectAlgo(int32_t opType, uint32_t nRanks, uint64_t bytes, int32_t special)
 {
     return SelectAlgo(opType, nRanks, bytes, special != 0);

@@ -595,62 +595,154 @@ void AllReduceRing(const ScheduleParams& p, Builder& b)
     }
 }
 
-// Recursive halving (reduce-scatter) then recursive doubling (all-gather), power-of-two n. Region = chunk range
-// [lo, hi); at distance d the rank keeps the half selected by bit d of its rank and exchanges the other half with
-// rank ^ d. Ends with rank r owning chunk r.
+// Recursive halving (reduce-scatter) then recursive doubling (all-gather), power-of-two n = 2^m
+// (docs/zh/user_guide/coll_algo_intro/RHD.md). One RHD instance uses one link per step (partner = rank ^ d), 3 of an
+// 8-GPU node's 7. The ranks of a power-of-two world are the vectors of GF(2)^m and the 7 XOR matchings r <-> r ^ v
+// (v != 0) partition its links, so the schedule runs n-1 instances at once, one per part of the buffer: instance j
+// relabels ranks by the linear map whose step-s partner vector is alpha^(s+j) in GF(2^m) (alpha primitive). At every
+// step the instances' vectors alpha^(s+j), j = 0..n-2, are all the nonzero vectors: every link carries exactly one.
+// Inside instance j the classic RHD runs on virtual ranks: region = virtual chunk range [lo, hi); at virtual distance
+// d the rank keeps the half selected by bit d of its virtual rank and exchanges the other half with its partner.
+// It ends with virtual rank v owning chunk v of the part.
+
+// Multiplication in GF(2^m) modulo a primitive polynomial (m <= 4: x^2+x+1, x^3+x+1, x^4+x+1).
+uint32_t Gf2Mul(uint32_t a, uint32_t b, uint32_t m)
+{
+    static const uint32_t kPoly[5] = {0, 0x3, 0x7, 0xB, 0x13};
+    uint32_t r = 0;
+    for (uint32_t i = 0; i < m; ++i) {
+        if ((b >> i) & 1u) r ^= a << i;
+    }
+    for (uint32_t i = 2 * m; i-- > m;) {
+        if ((r >> i) & 1u) r ^= kPoly[m] << (i - m);
+    }
+    return r;
+}
+
+}  // namespace
+
+std::vector<std::vector<uint32_t>> RhdTable(uint32_t n)
+{
+    // returns, per instance, virt->real rank (index = virtual rank)
+    uint32_t m = 0;
+    while ((1u << m) < n) ++m;
+    if ((1u << m) != n || m > 4) return {};
+    if (m == 0) return {{0}};
+    std::vector<std::vector<uint32_t>> t;
+    for (uint32_t j = 0; j + 1 < n; ++j) {
+        // partner vector of step s (virtual bit m-1-s) is alpha^(s+j), alpha = 2
+        std::vector<uint32_t> vec(m);
+        for (uint32_t s2 = 0; s2 < m; ++s2) {
+            uint32_t x = 1;
+            for (uint32_t k = 0; k < s2 + j; ++k) x = Gf2Mul(x, 2, m);
+            vec[s2] = x;
+        }
+        std::vector<uint32_t> real(n);
+        for (uint32_t v = 0; v < n; ++v) {
+            uint32_t r = 0;
+            for (uint32_t s2 = 0; s2 < m; ++s2) {
+                if ((v >> (m - 1 - s2)) & 1u) r ^= vec[s2];
+            }
+            real[v] = r;
+        }
+        t.push_back(real);
+    }
+    return t;
+}
+
+namespace {
+
 void AllReduceRhd(const ScheduleParams& p, Builder& b)
 {
     const uint32_t n = p.nRanks, me = p.rank;
     const uint64_t alignElems = std::max<uint64_t>(1, kAlignBytes / p.elemSize);
-    const uint64_t kSlots = 4;
-    auto range = [&](uint32_t lo, uint32_t hi) {
-        Span a = Chunk(p.count, n, lo, alignElems);
-        Span z = Chunk(p.count, n, hi - 1, alignElems);
-        return Span{a.begin, z.begin + z.len - a.begin};
+    const std::vector<std::vector<uint32_t>> table = RhdTable(n);
+    const uint32_t R = static_cast<uint32_t>(table.size());
+    struct Inst {
+        std::vector<uint32_t> real;
+        uint32_t v;  // my virtual rank
+        Span part;
+        uint32_t lo, hi;
     };
-    const uint64_t pe = PieceElems(p, range(0, n / 2).len, kSlots);
+    std::vector<Inst> inst(R);
+    for (uint32_t j = 0; j < R; ++j) {
+        inst[j].real = table[j];
+        for (uint32_t v = 0; v < n; ++v) {
+            if (table[j][v] == me) inst[j].v = v;
+        }
+        inst[j].part = Chunk(p.count, R, j, alignElems);
+        inst[j].lo = 0;
+        inst[j].hi = n;
+    }
+    auto range = [&](const Inst& I, uint32_t lo, uint32_t hi) {
+        Span a = Chunk(I.part.len, n, lo, alignElems);
+        Span z = Chunk(I.part.len, n, hi - 1, alignElems);
+        return Span{I.part.begin + a.begin, z.begin + z.len - a.begin};
+    };
+    const uint64_t kSlots = 4;
+    const uint64_t pe = PieceElems(p, range(inst[0], 0, n / 2).len, kSlots * R);
     uint64_t unit = 0;
-    uint32_t lo = 0, hi = n;
     bool first = true;
     for (uint32_t d = n / 2; d >= 1; d /= 2) {
-        const uint32_t partner = me ^ d;
-        const uint32_t mid = lo + d;
-        const bool keepLow = (me & d) == 0;
-        const Span keep = keepLow ? range(lo, mid) : range(mid, hi);
-        const Span give = keepLow ? range(mid, hi) : range(lo, mid);
-        const uint64_t np = std::max<uint64_t>(1, CeilDiv(std::max(keep.len, give.len), pe));
-        for (uint64_t t = 0; t < np; ++t, ++unit) {
-            Span g = Piece(give, pe, t);
-            Span k = Piece(keep, pe, t);
-            Ref stage = Scr((unit % kSlots) * pe);
-            b.Send(partner, first ? In(g.begin) : Out(g.begin), g.len);
-            b.Recv(partner, stage, k.len);
-            b.EndGroup();
-            b.Reduce(Out(k.begin), {first ? In(k.begin) : Out(k.begin), stage}, k.len);
+        // the piece count is the same on every rank (partners of different instances share groups): the widest
+        // half any rank can hold at this distance is the first d chunks of part 0
+        const uint64_t np = std::max<uint64_t>(1, CeilDiv(range(inst[0], 0, d).len, pe));
+        std::vector<Span> keep(R), give(R);
+        for (uint32_t j = 0; j < R; ++j) {
+            const Inst& I = inst[j];
+            const uint32_t mid = I.lo + d;
+            const bool keepLow = (I.v & d) == 0;
+            keep[j] = keepLow ? range(I, I.lo, mid) : range(I, mid, I.hi);
+            give[j] = keepLow ? range(I, mid, I.hi) : range(I, I.lo, mid);
         }
-        if (keepLow) {
-            hi = mid;
-        } else {
-            lo = mid;
+        for (uint64_t t = 0; t < np; ++t, ++unit) {
+            for (uint32_t j = 0; j < R; ++j) {
+                const uint32_t partner = inst[j].real[inst[j].v ^ d];
+                const Span g = Piece(give[j], pe, t);
+                const Span k = Piece(keep[j], pe, t);
+                b.Send(partner, first ? In(g.begin) : Out(g.begin), g.len);
+                b.Recv(partner, Scr(((unit % kSlots) * R + j) * pe), k.len);
+            }
+            b.EndGroup();
+            for (uint32_t j = 0; j < R; ++j) {
+                const Span k = Piece(keep[j], pe, t);
+                b.Reduce(Out(k.begin), {first ? In(k.begin) : Out(k.begin), Scr(((unit % kSlots) * R + j) * pe)},
+                         k.len);
+            }
+        }
+        for (Inst& I : inst) {
+            const uint32_t mid = I.lo + d;
+            if ((I.v & d) == 0) {
+                I.hi = mid;
+            } else {
+                I.lo = mid;
+            }
         }
         first = false;
         if (d == 1) break;
     }
     for (uint32_t d = 1; d < n; d *= 2) {
-        const uint32_t partner = me ^ d;
-        // my region is [lo, lo + d) chunks; the partner's is the adjacent block of d chunks
-        const uint32_t plo = (me & d) == 0 ? lo + d : lo - d;
-        const Span mine = range(lo, lo + d);
-        const Span theirs = range(plo, plo + d);
-        const uint64_t np = std::max<uint64_t>(1, CeilDiv(std::max(mine.len, theirs.len), pe));
+        const uint64_t np = std::max<uint64_t>(1, CeilDiv(range(inst[0], 0, d).len, pe));
+        std::vector<Span> mine(R), theirs(R);
+        std::vector<uint32_t> plo(R);
+        for (uint32_t j = 0; j < R; ++j) {
+            const Inst& I = inst[j];
+            // my region is [lo, lo + d) virtual chunks; the partner's is the adjacent block of d chunks
+            plo[j] = (I.v & d) == 0 ? I.lo + d : I.lo - d;
+            mine[j] = range(I, I.lo, I.lo + d);
+            theirs[j] = range(I, plo[j], plo[j] + d);
+        }
         for (uint64_t t = 0; t < np; ++t) {
-            Span m = Piece(mine, pe, t);
-            Span th = Piece(theirs, pe, t);
-            b.Send(partner, Out(m.begin), m.len);
-            b.Recv(partner, Out(th.begin), th.len);
+            for (uint32_t j = 0; j < R; ++j) {
+                const uint32_t partner = inst[j].real[inst[j].v ^ d];
+                const Span mP = Piece(mine[j], pe, t);
+                const Span th = Piece(theirs[j], pe, t);
+                b.Send(partner, Out(mP.begin), mP.len);
+                b.Recv(partner, Out(th.begin), th.len);
+            }
             b.EndGroup();
         }
-        lo = std::min(lo, plo);
+        for (uint32_t j = 0; j < R; ++j) inst[j].lo = std::min(inst[j].lo, plo[j]);
     }
 }
 

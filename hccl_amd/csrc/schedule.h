@@ -44,6 +44,9 @@ int32_t SelectAlgo(int32_t opType, uint32_t nRanks, uint64_t bytes, bool special
 // The directed rings the ring schedules run for n ranks: arc-disjoint Hamiltonian cycles (rank lists).
 std::vector<std::vector<uint32_t>> RingTable(uint32_t n);
 
+// The RHD instances for a power-of-two n (empty otherwise): per instance, the real rank of every virtual rank.
+std::vector<std::vector<uint32_t>> RhdTable(uint32_t n);
+
 // Returns HCCL_E_PARA for an invalid combination, HCCL_SUCCESS otherwise.
 int BuildSchedule(const ScheduleParams& p, Schedule* out);
 

@@ -122,6 +122,11 @@ extern int32_t HcclAmdSelectAlgo(int32_t opType, uint32_t nRanks, uint64_t bytes
  * into cycles (may be NULL) and returns the number of rings (0 for nRanks == 0). */
 extern int32_t HcclAmdRingTable(uint32_t nRanks, uint32_t* cycles, uint32_t capacity);
 
+/* The concurrent instances HCCL_AMD_ALGO_RHD runs on a power-of-two nRanks (n-1 of them, one per XOR matching of
+ * the ranks): for each instance the real rank of every virtual rank, row-major (nRanks entries per instance), up to
+ * `capacity` instances. Returns the number of instances (0 when nRanks is not a power of two or exceeds 16). */
+extern int32_t HcclAmdRhdTable(uint32_t nRanks, uint32_t* realOfVirtual, uint32_t capacity);
+
 /* ---------------------------------------------------------------- communicator extensions */
 
 /* nRanks communicators on the current HIP device, joined by device-to-device copies. comms[r] is rank r.

@@ -216,6 +216,33 @@ def test_ring_uses_every_link_at_eight_ranks():
         assert len({o.peer for o in first if o.kind == 3}) == 7
 
 
+@pytest.mark.parametrize("n", [1, 2, 4, 8, 16])
+def test_rhd_instances_cover_every_link_once_per_step(n):
+    """Each RHD instance is a linear relabelling of the hypercube (virtual v -> real; XOR-compatible), and at every
+    step the n-1 instances' partner vectors are all the nonzero vectors: every link carries exactly one instance."""
+    t = H.rhd_table(n)
+    assert len(t) == max(1, n - 1)
+    m = n.bit_length() - 1
+    for real in t:
+        assert sorted(real) == list(range(n))
+        for a in range(n):
+            for b in range(n):
+                assert real[a ^ b] == real[a] ^ real[b]  # linear over GF(2)
+    for s in range(m):
+        d = n >> (s + 1)
+        vecs = sorted(real[d] for real in t)
+        assert vecs == (list(range(1, n)) if n > 1 else [0])
+    assert H.rhd_table(6) == [] and H.rhd_table(12) == []
+
+
+def test_rhd_uses_every_link_at_eight_ranks():
+    progs, used, _ = programs(AR, 4, 8, 1 << 16, O.FP32)
+    assert used == R.ALGO_RHD
+    for arr, nops in progs:
+        g0 = [o for o in arr[:nops] if o.kind in (2, 3) and o.group == 0]
+        assert len({o.peer for o in g0 if o.kind == 2}) == 7 and len({o.peer for o in g0 if o.kind == 3}) == 7
+
+
 def test_rhd_non_power_of_two_falls_back_to_ring():
     assert programs(AR, 4, 6, 1000, O.FP32)[1] == R.ALGO_RING
 
