@@ -101,12 +101,17 @@ def c1_sim_replay() -> dict:
             "us": round(med * 1e6, 1), "GiBps_per_rank_input": round((1 << 20) / med / GIB, 3), "cores": 1}
 
 
-def end_to_end_host(steps: int = 5) -> dict:
-    """Gradient buckets that start and end in host memory: pinned H2D of both operands, the reduce, D2H of the
-    result, all on one stream (BASELINE.json). Rate = 3 GiB of algorithmic bytes per step over the wall time."""
+def end_to_end_host(steps: int = 5, chunk: int = 64 << 20) -> dict:
+    """Gradient buckets that start and end in host memory (BASELINE.json): pinned H2D of both operands, the reduce,
+    D2H of the result. Two forms, both reported:
+      serial     one stream, whole buffers (H2D 2 GiB, reduce, D2H 1 GiB);
+      pipelined  chunks of `chunk` bytes per operand on three streams (H2D / reduce / D2H joined by events), so
+                 H2D of chunk i+1, the reduce of chunk i and D2H of chunk i-1 overlap and PCIe runs both directions.
+    Rate = 3 GiB of algorithmic bytes per step over the wall time of the step."""
     dev = torch.device("cuda", 0)
     h_src = torch.empty(C2_COUNT, dtype=torch.float32).pin_memory()
     h_dst = torch.empty(C2_COUNT, dtype=torch.float32).pin_memory()
+    h_out = torch.empty(C2_COUNT, dtype=torch.float32).pin_memory()
     h_src.uniform_(-1, 1)
     h_dst.uniform_(-1, 1)
     d_src = torch.empty(C2_COUNT, device=dev)
@@ -114,7 +119,7 @@ def end_to_end_host(steps: int = 5) -> dict:
     s = torch.cuda.current_stream()
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
 
-    def step(rec):
+    def serial(rec):
         if rec:
             evs[0].record(s)
         d_src.copy_(h_src, non_blocking=True)
@@ -124,25 +129,58 @@ def end_to_end_host(steps: int = 5) -> dict:
         H.local_reduce(d_dst, d_src, H.HcclReduceOp.SUM, s)
         if rec:
             evs[2].record(s)
-        h_dst.copy_(d_dst, non_blocking=True)
+        h_out.copy_(d_dst, non_blocking=True)
         if rec:
             evs[3].record(s)
 
-    step(False)
+    serial(False)
     torch.cuda.synchronize()
     parts = []
     t0 = time.perf_counter()
     for _ in range(steps):
-        step(True)
+        serial(True)
         torch.cuda.synchronize()
         parts.append([evs[i].elapsed_time(evs[i + 1]) for i in range(3)])
     wall = (time.perf_counter() - t0) / steps
     h2d, red, d2h = (float(np.median([p[i] for p in parts])) for i in range(3))
-    return {"GiBps": round(3 * C2_COUNT * 4 / wall / GIB, 2), "ms_per_step": round(wall * 1e3, 2),
-            "h2d_ms": round(h2d, 2), "reduce_ms": round(red, 3), "d2h_ms": round(d2h, 2),
-            "h2d_GBps": round(2 * C2_COUNT * 4 / (h2d / 1e3) / 1e9, 1),
-            "d2h_GBps": round(C2_COUNT * 4 / (d2h / 1e3) / 1e9, 1),
-            "note": "pinned host buffers, one stream, 2 GiB H2D + reduce + 1 GiB D2H per step (PCIe-bound)"}
+    ok_serial = bool(torch.equal(h_out[:: 1 << 16], (h_src + h_dst)[:: 1 << 16]))
+
+    up, mid, down = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    per = chunk // 4
+    nchunks = (C2_COUNT + per - 1) // per
+
+    def pipelined():
+        for i in range(nchunks):
+            sl = slice(i * per, min(C2_COUNT, (i + 1) * per))
+            with torch.cuda.stream(up):
+                d_src[sl].copy_(h_src[sl], non_blocking=True)
+                d_dst[sl].copy_(h_dst[sl], non_blocking=True)
+                e_up = torch.cuda.Event()
+                e_up.record(up)
+            mid.wait_event(e_up)
+            H.local_reduce(d_dst[sl], d_src[sl], H.HcclReduceOp.SUM, mid)
+            e_mid = torch.cuda.Event()
+            e_mid.record(mid)
+            down.wait_event(e_mid)
+            with torch.cuda.stream(down):
+                h_out[sl].copy_(d_dst[sl], non_blocking=True)
+        torch.cuda.synchronize()
+
+    h_out.zero_()
+    pipelined()
+    ok_pipe = bool(torch.equal(h_out[:: 1 << 16], (h_src + h_dst)[:: 1 << 16]))
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        pipelined()
+    wall_p = (time.perf_counter() - t0) / steps
+    return {"GiBps": round(3 * C2_COUNT * 4 / wall_p / GIB, 2), "ms_per_step": round(wall_p * 1e3, 2),
+            "form": f"pipelined: {chunk >> 20} MiB chunks, H2D / reduce / D2H on three streams",
+            "result_ok": ok_pipe,
+            "serial": {"GiBps": round(3 * C2_COUNT * 4 / wall / GIB, 2), "ms_per_step": round(wall * 1e3, 2),
+                       "h2d_ms": round(h2d, 2), "reduce_ms": round(red, 3), "d2h_ms": round(d2h, 2),
+                       "h2d_GBps": round(2 * C2_COUNT * 4 / (h2d / 1e3) / 1e9, 1),
+                       "d2h_GBps": round(C2_COUNT * 4 / (d2h / 1e3) / 1e9, 1), "result_ok": ok_serial},
+            "note": "pinned host buffers; 2 GiB H2D + reduce + 1 GiB D2H per step (PCIe-bound)"}
 
 
 def load_pmc_traffic(name: str):
@@ -332,9 +370,10 @@ def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
     return {"workload": "C5: AllReduce fp16 SUM, size sweep (RHD schedule and auto selection)", "points": rows}
 
 
-def bench_e2e_allreduce(comm, world, nbytes: int = 256 << 20, iters: int = 5) -> dict:
+def bench_e2e_allreduce(comm, world, nbytes: int = 256 << 20, iters: int = 5, chunk: int = 32 << 20) -> dict:
     """Gradient bucket that starts and ends in host memory (BASELINE.json): pinned H2D, HcclAllReduce fp32 SUM, D2H,
-    all on one stream; nbytes per rank. Rate = bucket bytes per rank / max-over-ranks time per step."""
+    nbytes per rank. serial = one stream, whole bucket; pipelined = chunks on three streams (H2D / AllReduce / D2H
+    joined by events). Rate = bucket bytes per rank / max-over-ranks time per step."""
     import torch.distributed as dist
 
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -342,25 +381,47 @@ def bench_e2e_allreduce(comm, world, nbytes: int = 256 << 20, iters: int = 5) ->
     h.uniform_(-1, 1)
     d = torch.empty(nbytes // 4, device=dev)
     s = torch.cuda.current_stream()
+    up, mid, down = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    per = chunk // 4
 
-    def step():
+    def serial():
         d.copy_(h, non_blocking=True)
         comm.all_reduce(d, d, H.HcclReduceOp.SUM, s)
         h.copy_(d, non_blocking=True)
 
-    step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        step()
-    torch.cuda.synchronize()
-    t = torch.tensor([(time.perf_counter() - t0) / iters], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    per = float(t[0])
-    return {"bytes_per_rank": nbytes, "ms_per_step": round(per * 1e3, 3), "GiBps_per_rank": round(nbytes / per / GIB, 2),
-            "algo": H.Algo(comm.last_algo).name,
-            "note": "pinned host bucket -> H2D -> in-place HcclAllReduce -> D2H on one stream (PCIe-bound)"}
+    def pipelined():
+        for i in range(0, d.numel(), per):
+            sl = slice(i, min(d.numel(), i + per))
+            with torch.cuda.stream(up):
+                d[sl].copy_(h[sl], non_blocking=True)
+                e_up = torch.cuda.Event()
+                e_up.record(up)
+            mid.wait_event(e_up)
+            comm.all_reduce(d[sl], d[sl], H.HcclReduceOp.SUM, mid)
+            e_mid = torch.cuda.Event()
+            e_mid.record(mid)
+            down.wait_event(e_mid)
+            with torch.cuda.stream(down):
+                h[sl].copy_(d[sl], non_blocking=True)
+        torch.cuda.synchronize()
+
+    out = {"bytes_per_rank": nbytes,
+           "note": "pinned host bucket -> H2D -> in-place HcclAllReduce -> D2H (PCIe-bound)"}
+    for name, fn in (("serial", serial), ("pipelined", pipelined)):
+        fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize()
+        t = torch.tensor([(time.perf_counter() - t0) / iters], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        per_step = float(t[0])
+        out[name] = {"ms_per_step": round(per_step * 1e3, 3), "GiBps_per_rank": round(nbytes / per_step / GIB, 2),
+                     "algo": H.Algo(comm.last_algo).name}
+    out["pipelined"]["chunk_bytes"] = chunk
+    return out
 
 
 def bench_c3_algos(comm, send, recv, world) -> dict:
