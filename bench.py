@@ -577,6 +577,9 @@ def main():
     import faulthandler
 
     faulthandler.dump_traceback_later(900, exit=False)  # diagnostics only: stacks to stderr if a run stalls
+    # a lost peer ends an IPC launch after this long (status bit 0, sticky per communicator) instead of 60 s, so a
+    # failing secondary row cannot stretch the driver's run
+    os.environ.setdefault("HCCL_AMD_IPC_TIMEOUT_MS", "10000")
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
