@@ -306,6 +306,20 @@ def test_default_selection_meshchunk(monkeypatch, op_type, n, count):
             c.destroy()
 
 
+def test_reference_st_largest_case_c3_selection(worlds):
+    """The reference ST's largest AllReduce (all_reduce_testcase.cc:288-296: 200 MiB + 1, across the CCL buffer) at
+    8 ranks and 260 MiB + 148 B per rank: the default selector takes MeshChunk (bytes * 8/64 > 32 MiB, the C3 branch),
+    the default HCCL_BUFFSIZE gives three executor loops, and every output bit follows order O6."""
+    n, count = 8, (260 << 20) // 4 + 37
+    comms = worlds(n)
+    xs = [np.random.default_rng(2000 + r).uniform(-1, 1, count).astype(np.float32) for r in range(n)]
+    used, outs = collective(comms, AR, 0, O.FP32, O.SUM, xs, count)
+    assert used == R.ALGO_MESHCHUNK
+    want = R.expected(AR, used, O.FP32, O.SUM, xs, count)
+    for r in range(n):
+        assert O.equal_bits(O.FP32, outs[r], want[r]), r
+
+
 def test_reference_sample_known_answer(worlds):
     """examples/02_collectives/01_allreduce: 8 ranks, x_r[i] = i, fp32 SUM -> [0 8 16 ... 56] on every rank;
     04_reduce_scatter: rank r gets 8r; 05_reduce: root 0 gets [0 8 ... 56], others untouched (zeros)."""
