@@ -249,6 +249,9 @@ def bench_local(args) -> dict:
             "kernel": "k_reduce2<EFp<float>, SUM>",
             "algorithmic_bytes_per_launch": bytes_step,
             "kernel_avg_us": round(kavg * 1e6, 2),
+            "kernel_median_us": round(float(np.median(per)) * 1e6, 2),
+            "kernel_p10_us": round(float(np.percentile(per, 10)) * 1e6, 2),
+            "kernel_p90_us": round(float(np.percentile(per, 90)) * 1e6, 2),
         },
     }
     if not args.no_e2e:
