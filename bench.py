@@ -347,7 +347,8 @@ def bench_c4(comm, send, recv, world) -> dict:
 
 def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
     """C5: AllReduce fp16 SUM, 1 KiB .. 4 GiB: latency at small sizes, busbw at large. Each size runs the RHD schedule
-    (the config's algorithm) and the auto selection (what the reference would run: one-shot / two-shot / MeshChunk)."""
+    (the config's algorithm), the auto selection (what the reference would run: one-shot / two-shot / MeshChunk) and,
+    up to 256 MiB, the one-sided IPC kernel (order O2, one launch per call: the latency end of the curve)."""
     s = torch.cuda.current_stream()
     rows = []
     nbytes = 1 << 10
@@ -358,14 +359,18 @@ def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
             b = recv.view(torch.float16)[: nbytes // 2]
             iters = 20 if nbytes <= (64 << 20) else 3
             row = {"bytes": nbytes}
-            for algo in (H.Algo.RHD, H.Algo.AUTO):
+            algos = (H.Algo.RHD, H.Algo.AUTO) + ((H.Algo.IPC_TWOSHOT,) if nbytes <= (256 << 20) else ())
+            for algo in algos:
                 comm.set_algo(algo)
                 t = _timed(lambda: comm.all_reduce(a, b, H.HcclReduceOp.SUM, s), iters)
-                key = "rhd" if algo == H.Algo.RHD else "auto"
+                key = {H.Algo.RHD: "rhd", H.Algo.AUTO: "auto", H.Algo.IPC_TWOSHOT: "ipc"}[algo]
                 row[f"{key}_us"] = round(t * 1e6, 1)
                 row[f"{key}_busbw_GBps"] = round(nbytes / t / 1e9 * f, 2)
                 if algo == H.Algo.AUTO:
                     row["auto_algo"] = H.Algo(comm.last_algo).name
+                if algo == H.Algo.IPC_TWOSHOT:
+                    row["ipc_ran"] = H.Algo(comm.last_algo).name
+                    row["ipc_barrier_timeouts"] = comm.ipc_status() & 1
             rows.append(row)
             nbytes *= 2
     finally:
