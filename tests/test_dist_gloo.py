@@ -108,7 +108,16 @@ FP32, FP16, INT32, SUM, MAX = 4, 3, 2, 0, 2
 def test_gloo_allreduce_reducescatter_reduce(world):
     cases = [
         (0, 1, 3001, FP32, SUM), (0, 2, 5003, FP32, SUM), (0, 3, 5003, FP32, SUM), (0, 4, 5003, FP32, SUM),
-        (0, 2, 2049, FP16, MAX), (1, 1, 1537, FP32, SUM), (1, 3, 1537, INT32, SUM),
+        (0, 5, 5003, FP32, SUM), (0, 6, 5003, FP32, SUM), (0, 8, 5003, FP32, SUM),
+        (0, 2, 2049, FP16, MAX), (1, 1, 1537, FP32, SUM), (1, 3, 1537, INT32, SUM), (1, 8, 1537, FP32, SUM),
         (2, 1, 4097, FP32, SUM), (2, 2, 4097, FP32, SUM),
     ]
     _launch(world, cases)
+
+
+def test_gloo_eight_ranks_every_link_schedules():
+    """World 8 (the driver's N = 8 shape): the 7-ring and 7-instance RHD schedules (every link in every step), MeshChunk
+    (C3 / C4 selection) and the two-shot, each rank generating its own program."""
+    cases = [(0, 3, 20011, FP32, SUM), (0, 4, 20011, FP32, SUM), (0, 8, 20011, FP32, SUM), (0, 2, 20011, FP32, SUM),
+             (1, 3, 2503, FP32, SUM), (1, 8, 2503, FP16, SUM)]
+    _launch(8, cases)
