@@ -81,6 +81,7 @@ class Algo(enum.IntEnum):
     ORDER_PRESERVED = 6
     IPC_TWOSHOT = 7
     MESH_CHUNK = 8
+    IPC = 9
 
 
 class OpType(enum.IntEnum):

@@ -75,11 +75,13 @@ struct Comm {
     ~Comm();
 };
 
-// One-sided AllReduce / ReduceScatter / Reduce (HCCL_AMD_ALGO_IPC_TWOSHOT), any buffer alignment, in the
-// reference's orders (O2 / O1 / two-shot O1). Returns HCCL_E_NOT_SUPPORT, on every rank alike, when the peer mappings
-// cannot be set up (the caller then runs the RCCL schedule of the same order).
-HcclResult RunIpcCollective(Comm& c, int32_t opType, const void* sendBuf, void* recvBuf, uint64_t count,
-                            HcclDataType dt, HcclReduceOp op, uint32_t root, hipStream_t stream);
+// One-sided AllReduce / ReduceScatter / Reduce over peer-mapped staging, any buffer alignment. `family` is the schedule
+// family whose order the folds follow: AllReduce one-shot (O1) / two-shot (O2) / MeshChunk (O6), ReduceScatter mesh
+// (O1) / MeshChunk (O6), Reduce one-shot (O1, root first) / two-shot (O1, owner first). Returns HCCL_E_NOT_SUPPORT,
+// on every rank alike, when the peer mappings cannot be set up (the caller then runs the RCCL schedule of the same
+// family).
+HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void* sendBuf, void* recvBuf,
+                            uint64_t count, HcclDataType dt, HcclReduceOp op, uint32_t root, hipStream_t stream);
 // Collective: every rank's IPC kernels have finished before any rank unmaps or frees (called by ~Comm).
 void IpcQuiesce(Comm& c);
 void IpcRelease(Comm& c);

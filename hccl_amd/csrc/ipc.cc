@@ -27,6 +27,14 @@ struct RawPtrs {
     uint32_t* flags;
 };
 
+// HCCL_AMD_IPC_L2_SCRUB=0 skips the scrub of fresh staging (diagnostics only: tests/test_gpu_collectives.py shows the
+// stale-line failure it prevents).
+bool ScrubEnabled()
+{
+    const char* e = std::getenv("HCCL_AMD_IPC_L2_SCRUB");
+    return e == nullptr || std::strcmp(e, "0") != 0;
+}
+
 HcclResult IpcSetup(Comm& c)
 {
     IpcState& s = c.ipc;
@@ -37,10 +45,13 @@ HcclResult IpcSetup(Comm& c)
     s.stgInBytes = kIpcStagingBytes;
     s.stgResBytes = kIpcStagingBytes;  // results of a whole round, in round coordinates
     const size_t flagBytes = size_t(s.blocks) * kIpcMaxRanks * sizeof(uint32_t);
+    // The fresh uncached pages may carry lines of a freed cached buffer in some XCD's L2: scrub the L2s before the
+    // flags are zeroed (ScrubL2), so that no stale line is ever read or written back over them.
     bool ok = hipExtMallocWithFlags(&s.stg, s.stgInBytes + s.stgResBytes, hipDeviceMallocUncached) == hipSuccess &&
               hipExtMallocWithFlags(reinterpret_cast<void**>(&s.flags), flagBytes, hipDeviceMallocUncached) ==
                   hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&s.status), kIpcStatusBytes) == hipSuccess &&
+              hipDeviceSynchronize() == hipSuccess && (!ScrubEnabled() || ScrubL2(c.reduceStream) == HCCL_SUCCESS) &&
               hipMemset(s.flags, 0, flagBytes) == hipSuccess && hipMemset(s.status, 0, kIpcStatusBytes) == hipSuccess &&
               hipDeviceSynchronize() == hipSuccess;
     if (!ok) HCCL_AMD_ERR("rank %u: IPC staging allocation failed", me);
@@ -148,16 +159,28 @@ void IpcRelease(Comm& c)
     s = IpcState{};
 }
 
-HcclResult RunIpcCollective(Comm& c, int32_t opType, const void* sendBuf, void* recvBuf, uint64_t count,
-                            HcclDataType dt, HcclReduceOp op, uint32_t root, hipStream_t stream)
+HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void* sendBuf, void* recvBuf,
+                            uint64_t count, HcclDataType dt, HcclReduceOp op, uint32_t root, hipStream_t stream)
 {
     const uint64_t es = DataTypeSize(dt);
     if (es == 0 || c.nRanks > kIpcMaxRanks) return HCCL_E_NOT_SUPPORT;
     IpcKind kind;
+    IpcOrder order;
     switch (opType) {
-        case HCCL_AMD_OP_ALLREDUCE: kind = kIpcAllReduce; break;
-        case HCCL_AMD_OP_REDUCE_SCATTER: kind = kIpcReduceScatter; break;
-        case HCCL_AMD_OP_REDUCE: kind = kIpcReduce; break;
+        case HCCL_AMD_OP_ALLREDUCE:
+            kind = family == HCCL_AMD_ALGO_MESH_ONESHOT ? kIpcAllReduceOneShot : kIpcAllReduce;
+            order = family == HCCL_AMD_ALGO_MESH_ONESHOT ? kIpcO1
+                  : family == HCCL_AMD_ALGO_MESH_CHUNK   ? kIpcO6
+                                                         : kIpcO2;
+            break;
+        case HCCL_AMD_OP_REDUCE_SCATTER:
+            kind = kIpcReduceScatter;
+            order = family == HCCL_AMD_ALGO_MESH_CHUNK ? kIpcO6 : kIpcO1;
+            break;
+        case HCCL_AMD_OP_REDUCE:
+            kind = family == HCCL_AMD_ALGO_MESH_ONESHOT ? kIpcReduceOneShot : kIpcReduce;
+            order = kIpcO1;
+            break;
         default: return HCCL_E_NOT_SUPPORT;
     }
     HCCL_CHK(IpcSetup(c));
@@ -173,31 +196,41 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, const void* sendBuf, void* 
     }
     a.n = n;
     a.kind = kind;
+    a.order = order;
+    a.subMode = opType == HCCL_AMD_OP_REDUCE_SCATTER ? kIpcSubRs4K : kIpcSubEven;
     a.root = root;
     a.timeoutTicks = IpcTimeoutTicks();  // a lost peer ends the kernel with status bit 0, never a hang
     a.status = s.status;
     const uint64_t slotCap = (s.stgInBytes / es / n) / V * V;
 
-    // One launch per executor loop [off, off + cnt) with the geometry the reference's template uses for it.
+    // One launch per executor loop [off, off + cnt) of the reference template whose order the fold follows: its
+    // slicing is per loop (schedule.cc RefLoopElems and the MeshChunk loops).
     struct Launch {
         uint64_t off, cnt;
     };
     std::vector<Launch> launches;
+    uint64_t loopElems = count;
     if (kind == kIpcReduce) {
         // ReduceSoleExecutor loops (reduce_sole_executor.cc:120-170): min(UB_MAX_DATA_SIZE, ccl / n) rounded down to
         // 128 B, each sliced by ReduceMesh1DTwoShot::CalcSlice on its own
-        const uint64_t loopBytes = std::min<uint64_t>(256ull << 20, c.cclBytes / n / 128 * 128);
-        const uint64_t per = std::max<uint64_t>(1, loopBytes / es);
-        for (uint64_t off = 0; off < count; off += per) launches.push_back({off, std::min(per, count - off)});
-    } else {
-        launches.push_back({0, count});
+        loopElems = std::max<uint64_t>(1, std::min<uint64_t>(256ull << 20, c.cclBytes / n / 128 * 128) / es);
+    } else if (order == kIpcO6 && opType == HCCL_AMD_OP_ALLREDUCE) {
+        // AllReduce MeshChunk: min(ccl, ccl / 2) rounded down to 128 B (scratch multiple 2)
+        loopElems = std::max<uint64_t>(1, std::min<uint64_t>(c.cclBytes, c.cclBytes / 2 / 128 * 128) / es);
+    } else if (order == kIpcO6) {
+        // ReduceScatter MeshChunk: min(ccl - 1 MiB, (ccl - 1 MiB) / (n-1)) rounded down to 128 B
+        const uint64_t tmp = c.cclBytes > (1ull << 20) ? c.cclBytes - (1ull << 20) : c.cclBytes;
+        loopElems = std::max<uint64_t>(1, std::min<uint64_t>(tmp, tmp / (n - 1) / 128 * 128) / es);
     }
+    for (uint64_t off = 0; off < count; off += loopElems) launches.push_back({off, std::min(loopElems, count - off)});
     auto geometry = [&](IpcArgs& g, uint64_t cnt) {
         if (kind == kIpcReduceScatter) {
-            // block c of the input (recvCount elements) is chunk c (reduce_scatter_op.cc:158-159)
+            // block c of the input (recvCount elements, stride recvCount) is chunk c (reduce_scatter_op.cc:158-159);
+            // a MeshChunk loop takes elements [off, off + cnt) of every block
             g.balanced = false;
-            g.total = uint64_t(n) * cnt;
-            g.chunkStride = g.chunkLen = cnt;
+            g.chunkStride = count;
+            g.chunkLen = cnt;
+            g.total = uint64_t(n - 1) * count + cnt;
             g.rem = 0;
         } else if (kind == kIpcReduce) {
             g.balanced = true;  // reduce_mesh_1D_two_shot.cc:108-131
@@ -205,6 +238,19 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, const void* sendBuf, void* 
             g.chunkLen = cnt / n;
             g.rem = cnt % n;
             g.chunkStride = 0;
+        } else if (kind == kIpcAllReduceOneShot || kind == kIpcReduceOneShot) {
+            // every rank holds (and, for the AllReduce, folds) the whole range
+            g.balanced = false;
+            g.total = cnt;
+            g.chunkStride = 0;
+            g.chunkLen = cnt;
+            g.rem = 0;
+        } else if (order == kIpcO6) {
+            // MeshChunk CalcSliceInfoVec (…mesh_chunk.cc:79-97): ceil(cnt / n), no 128-B alignment
+            g.balanced = false;
+            g.total = cnt;
+            g.chunkStride = g.chunkLen = (cnt + n - 1) / n;
+            g.rem = 0;
         } else {
             // ceil(count / n) rounded up to HCCL_MIN_SLICE_ALIGN = 128 B (order O2 does not depend on it)
             const uint64_t align = 128 / es;
@@ -228,7 +274,7 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, const void* sendBuf, void* 
         HIP_CHK(hipMemsetAsync(s.status + 1, 0, sizeof(uint32_t), stream));  // wait diagnostic of this call
         for (const Launch& l : launches) {
             a.in[c.rank] = at(sendBuf, l.off);
-            a.out[c.rank] = at(recvBuf, kind == kIpcReduceScatter ? 0 : l.off);
+            a.out[c.rank] = at(recvBuf, l.off);
             geometry(a, l.cnt);
             HCCL_CHK(LaunchIpcCollective(a, s.blocks, 0, dt, op, stream));
         }
@@ -259,7 +305,7 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, const void* sendBuf, void* 
         for (const Launch& l : launches) {
             for (uint32_t r = 0; r < n; ++r) {
                 a.in[r] = at(all[r].in, l.off);
-                a.out[r] = at(all[r].out, kind == kIpcReduceScatter ? 0 : l.off);
+                a.out[r] = at(all[r].out, l.off);
             }
             geometry(a, l.cnt);
             HCCL_CHK(LaunchIpcCollective(a, s.blocks, n, dt, op, stream));

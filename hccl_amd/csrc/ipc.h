@@ -12,9 +12,25 @@ namespace hccl_amd {
 constexpr int kIpcMaxRanks = 16;
 
 enum IpcKind : uint32_t {
-    kIpcAllReduce = 0,      // order O2 (acc = x_0, then x_1 .. x_{n-1}); every rank gets every chunk
-    kIpcReduceScatter = 1,  // order O1 per block owner (x_me first, then ascending); rank c gets block c
-    kIpcReduce = 2,         // order O1 with the chunk owner first (two-shot Reduce); only the root gets the result
+    kIpcAllReduce = 0,         // two-shot: owner c folds chunk c, every rank gets every chunk
+    kIpcReduceScatter = 1,     // owner c folds block c into its recvBuf
+    kIpcReduce = 2,            // two-shot Reduce: owner c folds chunk c, only the root gets the result
+    kIpcAllReduceOneShot = 3,  // every rank receives every peer's whole piece and folds all of it (no phase 2)
+    kIpcReduceOneShot = 4,     // the peers push their whole piece to the root, which folds it
+};
+
+// Operand order of a fold of chunk t.
+enum IpcOrder : uint32_t {
+    kIpcO2 = 0,  // x_0, x_1, .., x_{n-1}                          two-shot AllReduce
+    kIpcO1 = 1,  // x_t, then ascending q != t                      one-shot, mesh ReduceScatter, Reduce
+    kIpcO6 = 2,  // sub-slice j: x_t, then x_{t+o}, o = j+1..n-1, 1..j   MeshChunk AllReduce / ReduceScatter
+};
+
+// Sub-slices of a chunk for kIpcO6 (chunk coordinates): the MeshChunk AllReduce's even split (the first L % (n-1)
+// one longer) or the MeshChunk ReduceScatter's 4-KiB split (schedule.cc SubSlicesEven / SubSlicesRs).
+enum IpcSubMode : uint32_t {
+    kIpcSubEven = 0,
+    kIpcSubRs4K = 1,
 };
 
 // Kernel arguments. In rank mode (me >= 0) only in[me] / out[me] are used; stgIn / stgRes / flags hold every rank's
@@ -23,7 +39,8 @@ enum IpcKind : uint32_t {
 //
 // Geometry (elements): chunk c of the input starts at c * chunkStride and holds min(chunkLen, total - c*chunkStride)
 // elements (clamped at 0), or, balanced (the two-shot Reduce's split), starts at c*chunkLen + min(c, rem) and holds
-// chunkLen + (c < rem); rank c owns chunk c. Round k handles piece k of every chunk: chunk elements
+// chunkLen + (c < rem); rank c owns chunk c. The one-shot kinds use chunkStride = 0, chunkLen = total: every "chunk"
+// is the whole range and every rank owns it. Round k handles piece k of every chunk: chunk elements
 // [k*piece, (k+1)*piece). Block b always handles piece coordinates [b*blockElems, (b+1)*blockElems), so every round
 // of a launch touches the same slot and result addresses per block and the per-block barrier is sound.
 // Staging: owner c's slot q = stgIn[c] + q*piece; results of chunk c at stgRes[p] + c*piece.
@@ -36,7 +53,9 @@ struct IpcArgs {
     uint32_t n;
     int32_t me;
     uint32_t kind;  // IpcKind
-    uint32_t root;  // kIpcReduce
+    uint32_t order;    // IpcOrder
+    uint32_t subMode;  // IpcSubMode (kIpcO6 only)
+    uint32_t root;  // kIpcReduce, kIpcReduceOneShot
     uint64_t total;
     uint64_t chunkStride;
     uint64_t chunkLen;
@@ -53,6 +72,9 @@ struct IpcArgs {
 
 HcclResult LaunchIpcCollective(const IpcArgs& a, uint32_t blocks, uint32_t worldRanks, HcclDataType dt,
                               HcclReduceOp op, hipStream_t stream);
+
+// Evicts every line of every XCD's L2 (and writes back the dirty ones); synchronous on `stream`.
+HcclResult ScrubL2(hipStream_t stream);
 
 // Per-communicator state of the IPC path.
 struct IpcState {

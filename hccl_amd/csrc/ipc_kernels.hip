@@ -135,24 +135,61 @@ __device__ __forceinline__ void CopyRange(S* dst, const S* src, Range r, bool ve
     for (uint64_t e = max(vhi * V, r.lo) + threadIdx.x; e < r.hi; e += kIpcBlock) dst[e] = src[e];
 }
 
-// Fold of chunk `me` over the n operands in the kind's order, written to up to kIpcMaxRanks destinations.
-//   all-reduce (O2):            operand i = rank i
-//   reduce-scatter / reduce (O1): operand 0 = rank me (the owner), then the others ascending
+// Rank of operand i (0 .. n-1) of a fold of chunk t in the given order; j = the sub-slice (kIpcO6 only).
+__device__ __forceinline__ uint32_t OperandRank(uint32_t order, uint32_t n, uint32_t t, uint32_t j, uint32_t i)
+{
+    if (order == kIpcO2) return i;
+    if (i == 0) return t;
+    if (order == kIpcO1) return i <= t ? i - 1 : i;
+    uint32_t x = i + j;  // kIpcO6: step s = i - 1 brings nextNum = s + j + 1, plus one once it reaches n
+    if (x >= n) x += 1;
+    return (t + x) % n;
+}
+
+// First element (chunk coordinates) of sub-slice j of a chunk of L elements; SubStart(n-1) = L.
+template <typename S>
+__device__ __forceinline__ uint64_t SubStart(const IpcArgs& a, uint64_t L, uint32_t j)
+{
+    const uint32_t parts = a.n - 1;
+    if (j >= parts) return L;
+    if (a.subMode == kIpcSubRs4K && parts >= 2) {
+        const uint64_t al = L * sizeof(S) / parts / 4096 * 4096 / sizeof(S);
+        if (al != 0) return uint64_t(j) * al;
+    }
+    const uint64_t base = L / parts, big = L % parts;
+    return uint64_t(j) * base + min(uint64_t(j), big);
+}
+
+// Fold of the piece range r (piece coordinates) of chunk `me` over the n operands, operand i being rank
+// OperandRank(order, n, me, j, i), written to ndst destinations. own = this rank's operand, slots = its staging (slot
+// q at q * piece). vec: the chunk's operands are 16-B aligned at piece coordinate 0; r may start and end anywhere
+// (scalar head and tail around the vector body).
 template <class E, int OP, class Dst>
-__device__ __forceinline__ void FoldRange(const IpcArgs& a, uint32_t me, const typename E::S* own,
-                                          const typename E::S* slots, Dst dsts, uint32_t ndst, Range r, bool vec)
+__device__ __forceinline__ void FoldSeg(const IpcArgs& a, uint32_t me, uint32_t j, const typename E::S* own,
+                                        const typename E::S* slots, Dst dsts, uint32_t ndst, Range r, bool vec)
 {
     using S = typename E::S;
     constexpr uint64_t V = 16 / sizeof(S);
     const uint32_t n = a.n;
-    const bool o2 = a.kind == kIpcAllReduce;
     auto src = [&](uint32_t i) {
-        const uint32_t q = o2 ? i : (i == 0 ? me : (i <= me ? i - 1 : i));
+        const uint32_t q = OperandRank(a.order, n, me, j, i);
         return q == me ? own : slots + uint64_t(q) * a.piece;
     };
-    const uint64_t vlo = r.lo / V, vhi = vec ? max(vlo, r.hi / V) : vlo;
-    uint64_t v = vlo + threadIdx.x;
-    for (; v + (kIpcU - 1) * kIpcBlock < vhi; v += kIpcU * kIpcBlock) {
+    auto scalar = [&](uint64_t lo, uint64_t hi) {
+        for (uint64_t e = lo + threadIdx.x; e < hi; e += kIpcBlock) {
+            S acc = src(0)[e];
+            for (uint32_t i = 1; i < n; ++i) acc = E::template ap<OP>(src(i)[e], acc);
+            for (uint32_t d = 0; d < ndst; ++d) dsts(d)[e] = acc;
+        }
+    };
+    const uint64_t vb = (r.lo + V - 1) / V, ve = r.hi / V;
+    if (!vec || vb >= ve) {
+        scalar(r.lo, r.hi);
+        return;
+    }
+    scalar(r.lo, vb * V);
+    uint64_t v = vb + threadIdx.x;
+    for (; v + (kIpcU - 1) * kIpcBlock < ve; v += kIpcU * kIpcBlock) {
         u32x4 acc[kIpcU];
 #pragma unroll
         for (int u = 0; u < kIpcU; ++u) acc[u] = reinterpret_cast<const u32x4*>(src(0))[v + u * kIpcBlock];
@@ -168,15 +205,30 @@ __device__ __forceinline__ void FoldRange(const IpcArgs& a, uint32_t me, const t
             for (int u = 0; u < kIpcU; ++u) reinterpret_cast<u32x4*>(dsts(d))[v + u * kIpcBlock] = acc[u];
         }
     }
-    for (; v < vhi; v += kIpcBlock) {
+    for (; v < ve; v += kIpcBlock) {
         u32x4 acc = reinterpret_cast<const u32x4*>(src(0))[v];
         for (uint32_t i = 1; i < n; ++i) acc = combine<E, OP>(reinterpret_cast<const u32x4*>(src(i))[v], acc);
         for (uint32_t d = 0; d < ndst; ++d) reinterpret_cast<u32x4*>(dsts(d))[v] = acc;
     }
-    for (uint64_t e = max(vhi * V, r.lo) + threadIdx.x; e < r.hi; e += kIpcBlock) {
-        S acc = src(0)[e];
-        for (uint32_t i = 1; i < n; ++i) acc = E::template ap<OP>(src(i)[e], acc);
-        for (uint32_t d = 0; d < ndst; ++d) dsts(d)[e] = acc;
+    scalar(ve * V, r.hi);
+}
+
+// The block's window r of round k (piece coordinates, chunk offset kP) of chunk `me`: one FoldSeg, or, in order O6,
+// one per sub-slice the window meets.
+template <class E, int OP, class Dst>
+__device__ __forceinline__ void FoldRange(const IpcArgs& a, uint32_t me, uint64_t kP, const typename E::S* own,
+                                          const typename E::S* slots, Dst dsts, uint32_t ndst, Range r, bool vec)
+{
+    using S = typename E::S;
+    if (a.order != kIpcO6) {
+        FoldSeg<E, OP>(a, me, 0, own, slots, dsts, ndst, r, vec);
+        return;
+    }
+    const uint64_t L = ChunkElems(a, me);
+    for (uint32_t j = 0; j + 1 < a.n; ++j) {
+        const uint64_t sb = SubStart<S>(a, L, j), se = SubStart<S>(a, L, j + 1);
+        const uint64_t lo = max(r.lo, sb > kP ? sb - kP : 0), hi = min(r.hi, se > kP ? se - kP : 0);
+        if (lo < hi) FoldSeg<E, OP>(a, me, j, own, slots, dsts, ndst, Range{lo, hi}, vec);
     }
 }
 
@@ -188,26 +240,30 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
     const uint32_t me = a.me >= 0 ? static_cast<uint32_t>(a.me) : blockIdx.y;
     const S* in = static_cast<const S*>(a.in[me]);
     S* out = static_cast<S*>(a.out[me]);
+    const bool oneShot = a.kind == kIpcAllReduceOneShot || a.kind == kIpcReduceOneShot;
+    const bool reduceKind = a.kind == kIpcReduce || a.kind == kIpcReduceOneShot;
     // a communicator whose IPC barrier ever timed out stays failed (sticky bit): never wait on its peers again
     if ((__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 1u) != 0) return;
     uint32_t epoch = a.epochBase;
     for (uint32_t k = 0; k < a.rounds; ++k) {
         const uint64_t kP = uint64_t(k) * a.piece;
-        // phase 0: my piece of chunk c -> owner c's slot `me`
+        // phase 0: my piece of chunk c -> owner c's slot `me` (one-shot: my whole piece to every peer; to the root
+        // only for a one-shot Reduce)
         for (uint32_t c = 0; c < n; ++c) {
-            if (c == me) continue;
+            if (c == me || (a.kind == kIpcReduceOneShot && c != a.root)) continue;
             const Range r = BlockWindow(a, PieceLen(a, c, kP));
             S* slot = static_cast<S*>(a.stgIn[c]) + uint64_t(me) * a.piece;
             CopyRange<S>(slot, in + ChunkStart(a, c) + kP, r, ChunkVec<S>(a, c));
         }
         if (!Barrier(a, me, ++epoch)) return;
         // phase 1: fold my chunk's piece over the slots (my own operand straight from my input)
-        {
+        if (!(a.kind == kIpcReduceOneShot && me != a.root)) {
             const Range r = BlockWindow(a, PieceLen(a, me, kP));
             const S* own = in + ChunkStart(a, me) + kP;
             const S* slots = static_cast<const S*>(a.stgIn[me]);
-            // destination 0: my output (or, for a non-root Reduce rank, the root's result area); all-reduce also
-            // pushes to every peer's result area (destinations 1 .. n-1 = the peers in ascending order)
+            // destination 0: my output (or, for a non-root two-shot Reduce rank, the root's result area); the
+            // two-shot AllReduce also pushes to every peer's result area (destinations 1 .. n-1 = the peers in
+            // ascending order)
             S* first = a.kind == kIpcReduceScatter ? out + kP
                      : (a.kind == kIpcReduce && me != a.root)
                          ? static_cast<S*>(a.stgRes[a.root]) + uint64_t(me) * a.piece
@@ -217,11 +273,12 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
                 const uint32_t p = d - 1 < me ? d - 1 : d;
                 return static_cast<S*>(a.stgRes[p]) + uint64_t(me) * a.piece;
             };
-            FoldRange<E, OP>(a, me, own, slots, dst, a.kind == kIpcAllReduce ? n : 1u, r, ChunkVec<S>(a, me));
+            FoldRange<E, OP>(a, me, kP, own, slots, dst, a.kind == kIpcAllReduce ? n : 1u, r, ChunkVec<S>(a, me));
         }
         if (!Barrier(a, me, ++epoch)) return;
-        // phase 2: the other chunks' results from my own result area (all-reduce: every rank; reduce: the root)
-        if (a.kind == kIpcAllReduce || (a.kind == kIpcReduce && me == a.root)) {
+        // phase 2: the other chunks' results from my own result area (two-shot AllReduce: every rank; two-shot
+        // Reduce: the root)
+        if (!oneShot && (a.kind == kIpcAllReduce || (reduceKind && me == a.root))) {
             for (uint32_t c = 0; c < n; ++c) {
                 if (c == me) continue;
                 const Range r = BlockWindow(a, PieceLen(a, c, kP));
@@ -244,7 +301,45 @@ hipError_t LaunchIpcT(int op, const IpcArgs& a, dim3 grid, hipStream_t s)
     return hipGetLastError();
 }
 
+// L2 scrub for a fresh staging allocation. Its pages may have belonged to a freed cached (MTYPE RW) buffer whose lines
+// still sit in some XCD's L2; the uncached accesses of the protocol do not see through them reliably (observed: a
+// barrier flag read back from a stale line, phase 2 then copying the previous owner's bytes). Every block streams
+// its share of a buffer many times the L2 size through the normal cached path, which evicts every older line (dirty
+// ones are written back), and then writes back its XCD's L2 (system-scope release).
+__global__ __launch_bounds__(256) void k_l2_scrub(const u32x4* p, uint64_t nvec, uint32_t* sink)
+{
+    u32x4 acc = {0, 0, 0, 0};
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < nvec; i += uint64_t(gridDim.x) * 256) acc ^= p[i];
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u && threadIdx.x == 0) sink[0] = 1;  // keeps the loads
+    __threadfence_system();
+}
+
 }  // namespace
+
+HcclResult ScrubL2(hipStream_t stream)
+{
+    constexpr uint64_t kBytes = 512ull << 20;  // 64 MiB per XCD: 16 x its 4 MiB L2
+    void* buf = nullptr;
+    uint32_t* sink = nullptr;
+    HIP_CHK(hipMalloc(&buf, kBytes + 256));
+    sink = reinterpret_cast<uint32_t*>(static_cast<char*>(buf) + kBytes);
+    int cus = 256;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+        cus = 256;
+    }
+    hipLaunchKernelGGL(k_l2_scrub, dim3(uint32_t(cus) * 4), dim3(256), 0, stream, static_cast<const u32x4*>(buf),
+                       kBytes / 16, sink);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    (void)hipFree(buf);
+    if (e != hipSuccess) {
+        HCCL_AMD_ERR("L2 scrub failed: %s", hipGetErrorString(e));
+        return HCCL_E_RUNTIME;
+    }
+    return HCCL_SUCCESS;
+}
 
 HcclResult LaunchIpcCollective(const IpcArgs& a, uint32_t blocks, uint32_t worldRanks, HcclDataType dt,
                               HcclReduceOp op, hipStream_t stream)

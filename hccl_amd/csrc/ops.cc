@@ -83,18 +83,22 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     if (p.algo == HCCL_AMD_ALGO_AUTO && NeedStrictOrder(opType, dt, op, c.nRanks)) {
         p.algo = HCCL_AMD_ALGO_ORDER_PRESERVED;
     }
-    if (p.algo == HCCL_AMD_ALGO_IPC_TWOSHOT) {
-        if (opType != HCCL_AMD_OP_ALLGATHER) {
-            HcclResult r = RunIpcCollective(c, opType, sendBuf, recvBuf, count, dt, op, root, stream);
-            if (r != HCCL_E_NOT_SUPPORT) {
-                c.lastAlgo = HCCL_AMD_ALGO_IPC_TWOSHOT;
-                return r;
-            }
+    if ((p.algo == HCCL_AMD_ALGO_IPC_TWOSHOT || p.algo == HCCL_AMD_ALGO_IPC) && opType != HCCL_AMD_OP_ALLGATHER) {
+        // the order family of the one-sided kernel: IPC_TWOSHOT fixes AllReduce two-shot (O2), mesh ReduceScatter
+        // and two-shot Reduce; IPC takes whatever the auto selector takes, so its bits are the auto path's
+        const uint64_t bytes = count * es;
+        const int32_t family =
+            p.algo == HCCL_AMD_ALGO_IPC
+                ? SelectAlgo(opType, c.nRanks, bytes, IsSpecialForSelector(dt, op))
+                : (opType == HCCL_AMD_OP_REDUCE_SCATTER ? HCCL_AMD_ALGO_MESH_ONESHOT : HCCL_AMD_ALGO_MESH_TWOSHOT);
+        HcclResult r = RunIpcCollective(c, opType, family, sendBuf, recvBuf, count, dt, op, root, stream);
+        if (r != HCCL_E_NOT_SUPPORT) {
+            c.lastAlgo = p.algo;
+            return r;
         }
-        // the RCCL schedule with the same order: AllReduce / Reduce two-shot (O2 / owner-first O1), ReduceScatter
-        // mesh (O1); AllGather has no IPC form
-        p.algo = opType == HCCL_AMD_OP_REDUCE_SCATTER || opType == HCCL_AMD_OP_ALLGATHER ? HCCL_AMD_ALGO_MESH_ONESHOT
-                                                                                          : HCCL_AMD_ALGO_MESH_TWOSHOT;
+        p.algo = family;  // the RCCL schedule with the same order
+    } else if (p.algo == HCCL_AMD_ALGO_IPC_TWOSHOT || p.algo == HCCL_AMD_ALGO_IPC) {
+        p.algo = HCCL_AMD_ALGO_MESH_ONESHOT;  // AllGather has no IPC form
     }
     p.nRanks = c.nRanks;
     p.rank = c.rank;
@@ -289,7 +293,7 @@ HcclResult HcclAmdCommSetAlgo(HcclComm comm, int32_t algo)
 {
     Comm* c = AsComm(comm);
     if (c == nullptr) return HCCL_E_PTR;
-    if (algo < HCCL_AMD_ALGO_AUTO || algo > HCCL_AMD_ALGO_MESH_CHUNK) return HCCL_E_PARA;
+    if (algo < HCCL_AMD_ALGO_AUTO || algo > HCCL_AMD_ALGO_IPC) return HCCL_E_PARA;
     c->algoOverride = algo;
     return HCCL_SUCCESS;
 }

@@ -1256,6 +1256,7 @@ int BuildSchedule(const ScheduleParams& p, Schedule* out)
     // The one-sided IPC collectives run as one kernel per executor loop, not as IR; their IR twins (same orders, same
     // bits) are the two-shot AllReduce / Reduce and the mesh ReduceScatter, which also run when the IPC path cannot.
     if (algo == HCCL_AMD_ALGO_IPC_TWOSHOT) algo = HCCL_AMD_ALGO_MESH_TWOSHOT;
+    if (algo == HCCL_AMD_ALGO_IPC) algo = SelectAlgo(p.opType, p.nRanks, bytes, p.special);
     if (p.nRanks == 1) {
         // SingleRankProc (op_common.cc:3042-3098): a copy when the buffers differ.
         b.Copy(Out(0), In(0), p.count);

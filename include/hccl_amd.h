@@ -101,8 +101,10 @@ typedef enum {
     HCCL_AMD_ALGO_NHR = 5,          /* AllReduce: the reference's NHR template, order O5 (any rank count) */
     HCCL_AMD_ALGO_ORDER_PRESERVED = 6, /* AllReduce / ReduceScatter: HCCL_DETERMINISTIC=STRICT tree, order O4 */
     HCCL_AMD_ALGO_IPC_TWOSHOT = 7,     /* AllReduce: one kernel over peer-mapped staging (AIV GM_IN model), O2 */
-    HCCL_AMD_ALGO_MESH_CHUNK = 8       /* AllReduce / ReduceScatter: the reference's MeshChunk templates, order O6
+    HCCL_AMD_ALGO_MESH_CHUNK = 8,      /* AllReduce / ReduceScatter: the reference's MeshChunk templates, order O6
                                           (owner first, then the peers in a per-sub-slice rotated order) */
+    HCCL_AMD_ALGO_IPC = 9              /* the one-sided kernel in the order family the auto selector picks (one-shot
+                                          O1 / two-shot O2 / MeshChunk O6 ...): the auto path's bits over IPC */
 } HcclAmdAlgo;
 
 /* Build rank `rank`'s schedule. If ops == NULL only *numOps is written. scratchElems receives the number of

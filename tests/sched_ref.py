@@ -425,6 +425,7 @@ def reduce_scatter_meshchunk(dtype, op, xs, rc, ccl=None):
 
 
 ALGO_ONESHOT, ALGO_TWOSHOT, ALGO_RING, ALGO_RHD, ALGO_NHR, ALGO_TREE, ALGO_IPC, ALGO_MESHCHUNK = 1, 2, 3, 4, 5, 6, 7, 8
+ALGO_IPC_AUTO = 9
 
 
 def expected(op_type, algo, dtype, op, xs, count, root=0):

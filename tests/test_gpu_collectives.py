@@ -174,6 +174,92 @@ def test_ownership_orders_follow_executor_loops(monkeypatch, op_type, algo, n, c
             c.destroy()
 
 
+@pytest.mark.parametrize("op_type,n,count,buffsize", [
+    (AR, 4, 4099, None),                    # one-shot O1
+    (AR, 8, (9 << 20) // 4 + 3, None),      # two-shot O2 (8 MiB < bytes <= 256 MiB at n = 8)
+    (AR, 2, (17 << 20) // 4 + 5, "4"),      # MeshChunk O6, loops of 2 MiB
+    (AR, 3, (40 << 20) // 4 + 1, None),     # MeshChunk at n = 3: one loop, chunks not 16-B aligned
+    (RS, 4, 1001, None),                    # mesh O1
+    (RS, 4, (5 << 20) // 4 + 7, "4"),       # MeshChunk O6 with 4-KiB sub-slices, loops of 1 MiB
+    (RS, 8, (3 << 20) // 4 + 3, None),      # MeshChunk at n = 8, one loop
+    (RED, 4, 1003, None),                   # one-shot Reduce, root first
+    (RED, 3, (9 << 20) // 4 + 1, None),     # two-shot Reduce
+])
+def test_ipc_follows_auto_family(monkeypatch, op_type, n, count, buffsize):
+    """HCCL_AMD_ALGO_IPC runs the one-sided kernel in the order family the auto selector picks, so it gives the auto
+    path's bits: compared with the closed form of that family and with the auto (RCCL-schedule) run itself."""
+    if buffsize is not None:
+        monkeypatch.setenv("HCCL_BUFFSIZE", buffsize)
+    comms = H.loopback_world(n)
+    try:
+        root = n - 1
+        in_count = count * n if op_type == RS else count
+        xs = [O.random_operands(O.FP32, in_count, seed=520 + r, edge=False) for r in range(n)]
+        family = H.select_algo(op_type, n, count * 4, False)
+        used, outs = collective(comms, op_type, 9, O.FP32, O.SUM, xs, count, root=root)
+        assert used == 9
+        assert ipc_status(comms[0]) & 1 == 0
+        used_auto, outs_auto = collective(comms, op_type, 0, O.FP32, O.SUM, xs, count, root=root)
+        assert used_auto == family
+        want = R.expected(op_type, family, O.FP32, O.SUM, xs, count, root=root)
+        for r in range(n):
+            if op_type == RED and r != root:
+                assert not outs[r].any(), "non-root recvBuf written"
+                continue
+            bad = np.nonzero(outs[r].view(np.uint32) != want[r].view(np.uint32))[0]
+            if len(bad):
+                e = int(bad[0])
+                per_rank = [int(np.count_nonzero(outs[q].view(np.uint32) != want[q].view(np.uint32))) for q in range(n)]
+                prefix = np.cumsum(np.array([x[e] for x in xs], np.float64)).tolist()
+                raise AssertionError(f"rank {r}: {len(bad)} bad, per rank {per_rank}, first {bad[:4].tolist()} "
+                                     f"last {bad[-2:].tolist()}; at {e}: got {outs[r][e]!r} want {want[r][e]!r} "
+                                     f"operands {[float(x[e]) for x in xs]} prefix sums {prefix}")
+            assert O.equal_bits(O.FP32, outs[r], outs_auto[r]), r
+    finally:
+        torch.cuda.synchronize()
+        for c in comms:
+            c.destroy()
+
+
+def _stale_line_bait(mib=9):
+    """What preceded the observed failure: a world whose executor staging (cached, MTYPE RW) received raw operands,
+    destroyed right away, so that its pages go back to the driver with lines still in the L2s. The next uncached IPC
+    staging allocation may take those pages."""
+    n, count = 4, (mib << 20) // 4 + 3
+    comms = H.loopback_world(n)
+    try:
+        xs = [O.random_operands(O.FP32, count, seed=540 + r, edge=False) for r in range(n)]
+        collective(comms, AR, 2, O.FP32, O.SUM, xs, count)
+    finally:
+        torch.cuda.synchronize()
+        for c in comms:
+            c.destroy()
+
+
+def test_ipc_staging_survives_recycled_cached_pages():
+    """Fresh uncached IPC staging right after a destroyed world released its cached staging. Context: in the suite
+    order (bootstrap, IPC, executor-loop and auto-family tests) an 8-rank two-shot IPC AllReduce returned a few hundred
+    to a few thousand elements with one stale operand in the owner's fold, on every rank alike, in 4 of 5 runs without
+    the L2 scrub of IpcSetup and in none of 4 with it. This test repeats the destroy-then-create pattern; it did not
+    reproduce the failure by itself, so it is a guard, not the proof."""
+    n, count = 8, (9 << 20) // 4 + 3
+    xs = [O.random_operands(O.FP32, count, seed=530 + r, edge=False) for r in range(n)]
+    want = R.expected(AR, R.ALGO_TWOSHOT, O.FP32, O.SUM, xs, count)
+    for it in range(3):
+        _stale_line_bait()
+        comms = H.loopback_world(n)
+        try:
+            used, outs = collective(comms, AR, 7, O.FP32, O.SUM, xs, count)
+            assert used == 7 and ipc_status(comms[0]) & 1 == 0
+            for r in range(n):
+                bad = np.nonzero(outs[r].view(np.uint32) != want[r].view(np.uint32))[0]
+                assert len(bad) == 0, (it, r, len(bad), bad[:4].tolist())
+        finally:
+            torch.cuda.synchronize()
+            for c in comms:
+                c.destroy()
+
+
 @pytest.mark.parametrize("shift", [(1, 1), (0, 3), (2, 0)])
 def test_ipc_unaligned_buffers(worlds, shift):
     """Buffers not 16-B aligned still run the IPC kernel (element-wise accesses to the user buffers; the path choice
@@ -243,8 +329,8 @@ def test_fp32_sum(worlds, op_type, algo, n, count, streams, monkeypatch):
 @pytest.mark.parametrize("dtype", [O.INT8, O.INT16, O.INT32, O.INT64, O.UINT64, O.FP16, O.BFP16, O.FP64],
                          ids=lambda v: O.DTYPE_NAMES[v])
 @pytest.mark.parametrize("op", O.OPS, ids=lambda v: O.OP_NAMES[v])
-@pytest.mark.parametrize("op_type,algo", [(AR, 1), (AR, 2), (AR, 3), (AR, 5), (AR, 7), (AR, 8), (RS, 1), (RS, 5),
-                                          (RS, 7), (RS, 8), (RED, 2), (RED, 5), (RED, 7)])
+@pytest.mark.parametrize("op_type,algo", [(AR, 1), (AR, 2), (AR, 3), (AR, 5), (AR, 7), (AR, 8), (AR, 9), (RS, 1),
+                                          (RS, 5), (RS, 7), (RS, 8), (RS, 9), (RED, 2), (RED, 5), (RED, 7), (RED, 9)])
 def test_dtypes_ops(worlds, op_type, algo, dtype, op):
     n, count, root = 4, 40961, 2
     comms = worlds(n)

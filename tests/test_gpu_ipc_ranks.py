@@ -26,8 +26,13 @@ CASES = [
     (RS, O.FP32, O.SUM, 3), (RS, O.FP32, O.SUM, 50001), (RS, O.BFP16, O.MAX, 20003), (RS, O.FP32, O.SUM, (17 << 20) + 5),
     (RED, O.FP32, O.SUM, 5), (RED, O.FP16, O.SUM, 60001), (RED, O.FP32, O.MIN, (36 << 20) + 7),
     (AR, O.FP32, O.SUM, 250001),
+    # HCCL_AMD_ALGO_IPC (9): the order family the auto selector picks, so the auto path's bits over IPC:
+    # one-shot O1 AllReduce / Reduce, MeshChunk O6 (AllReduce above 16 MiB at n = 2, ReduceScatter above 4 MiB at
+    # n = 4 and 1 MiB at n = 2), two-shot O2 AllReduce at n = 4
+    (AR, O.FP32, O.SUM, 5001, 9), (AR, O.FP32, O.SUM, (20 << 20) // 4 + 3, 9), (RS, O.FP32, O.SUM, (5 << 20) // 4 + 1, 9),
+    (RED, O.FP16, O.SUM, 3001, 9), (AR, O.BFP16, O.MAX, 70001, 9),
 ]
-UNALIGNED_CASE = len(CASES) - 1
+UNALIGNED_CASE = CASES.index((AR, O.FP32, O.SUM, 250001))
 ROOT = 1
 
 
@@ -67,7 +72,10 @@ def _rank_main(rank, n, port, q):
         comm = H.comm_init_host_exchange(n, rank, all_gather)
         stream = torch.cuda.Stream()
         results = []
-        for i, (kind, dtype, op, count) in enumerate(CASES):
+        for i, case in enumerate(CASES):
+            kind, dtype, op, count = case[:4]
+            forced = case[4] if len(case) > 4 else None
+            comm.set_algo(forced if forced is not None else R.ALGO_IPC)
             progress.write(f"case {i} {CASES[i]} start\n")
             send = to_device(dtype, _inputs(dtype, _in_count(kind, count, n), n, i)[rank])
             recv = torch.zeros(count, dtype=send.dtype, device=send.device)
@@ -87,7 +95,12 @@ def _rank_main(rank, n, port, q):
             ok = True
             if not (kind == RED and rank != ROOT % n):
                 xs = _inputs(dtype, _in_count(kind, count, n), n, i)
-                want = R.expected(kind, R.ALGO_IPC, dtype, op, xs, count, root=ROOT % n)[rank]
+                fam = R.ALGO_IPC
+                if forced == 9:
+                    special = dtype in (O.INT64, O.UINT64, O.FP64) or op == O.PROD
+                    nbytes = count * O.NP_STORAGE[dtype]().itemsize
+                    fam = H.select_algo(kind, n, nbytes, special)
+                want = R.expected(kind, fam, dtype, op, xs, count, root=ROOT % n)[rank]
                 ok = O.equal_bits(dtype, got, want)
             progress.write(f"case {i} done status {status} algo {comm.last_algo} ok {ok}\n")
             results.append((i, status, comm.last_algo, ok))
@@ -129,7 +142,7 @@ def test_ipc_collectives_rank_mode(n):
         assert len(got[r][1]) == len(CASES), f"rank {r} stopped after case {len(got[r][1]) - 1}"
         for i, status, algo, _ok in got[r][1]:
             assert status & 1 == 0, f"rank {r} case {CASES[i]}: barrier timeout (status {status:#x})"
-            assert algo == R.ALGO_IPC
+            assert algo == (CASES[i][4] if len(CASES[i]) > 4 else R.ALGO_IPC)
     for r in range(n):
         for i, status, algo, ok in got[r][1]:
             assert ok, f"rank {r} case {CASES[i]} differs from the reference order"

@@ -13,13 +13,20 @@ import pytest
 STG_BYTES = 128 << 20  # kIpcStagingBytes (slot area and result area each)
 BLOCKS = 128           # kIpcBlocks
 AR, RS, RED = 0, 1, 2
+AR1, RED1, ARMC = 3, 4, 5  # one-shot AllReduce, one-shot Reduce, MeshChunk AllReduce (order O6, unaligned ceil)
 
 
 def geometry(kind, n, count, es):
     """RunIpcCollective for one launch: (chunks [(start, len)] in input coordinates, piece, block elems, rounds).
-    AllReduce: ceil(count/n) rounded to 128 B; ReduceScatter: the blocks; Reduce: the balanced two-shot split."""
+    AllReduce: ceil(count/n) rounded to 128 B; ReduceScatter: the blocks; Reduce: the balanced two-shot split;
+    one-shot kinds: every chunk is the whole range; MeshChunk AllReduce: ceil(count/n) without alignment."""
     v = 16 // es
-    if kind == RS:
+    if kind in (AR1, RED1):
+        chunks = [(0, count) for _ in range(n)]
+    elif kind == ARMC:
+        cs = -(-count // n)
+        chunks = [(min(count, c * cs), max(0, min(count, c * cs + cs) - min(count, c * cs))) for c in range(n)]
+    elif kind == RS:
         chunks = [(c * count, count) for c in range(n)]
     elif kind == RED:
         base, rem = divmod(count, n)
@@ -46,6 +53,102 @@ def touched(lo, hi, v, vec=True):
     vhi = max(vlo, hi // v) if vec else vlo
     t0 = max(vhi * v, lo)
     return [(vlo * v, vhi * v), (t0, max(t0, hi))]
+
+
+def sub_starts(length, n, es, rs4k):
+    """Sub-slice starts of a chunk for order O6 (ipc_kernels.hip SubStart), plus the end."""
+    parts = n - 1
+    if rs4k and parts >= 2:
+        al = length * es // parts // 4096 * 4096 // es
+        if al:
+            return [j * al for j in range(parts)] + [length]
+    base, big = divmod(length, parts)
+    return [j * base + min(j, big) for j in range(parts)] + [length]
+
+
+def fold_touched(lo, hi, v, vec):
+    """FoldSeg's accesses for [lo, hi): scalar head up to a vector boundary, the vector body, the scalar tail."""
+    vb, ve = -(-lo // v), hi // v
+    if not vec or vb >= ve:
+        return [(lo, hi)]
+    return [(lo, vb * v), (vb * v, ve * v), (ve * v, hi)]
+
+
+def fold_segments(kind, n, es, chunk_len, kp, lo, hi, o6):
+    """FoldRange: the window, or its pieces per O6 sub-slice (piece coordinates)."""
+    if not o6 or n < 2:
+        return [(lo, hi)]
+    st = sub_starts(chunk_len, n, es, kind == RS)
+    out = []
+    for j in range(n - 1):
+        a0 = max(lo, st[j] - kp if st[j] > kp else 0)
+        a1 = min(hi, st[j + 1] - kp if st[j + 1] > kp else 0)
+        if a0 < a1:
+            out.append((a0, a1))
+    return out
+
+
+def check_general(kind, n, count, es, vec, root=0, o6=False):
+    """The generalised kernel: one-shot kinds push the whole piece (Reduce: to the root only) and fold it without a
+    phase 2; O6 folds a window per sub-slice with scalar head and tail around the vector body."""
+    v = 16 // es
+    chunks, piece, block, rounds = geometry(kind, n, count, es)
+    total = n * count if kind == RS else count
+    for me in range(n):
+        cover1 = np.zeros(total, np.int32)
+        pushed = np.zeros((n, total), np.int32)  # pushed[c]: elements delivered to owner c by me
+        for k in range(rounds):
+            kp = k * piece
+            for b in range(BLOCKS):
+                for c in range(n):
+                    start, cl = chunks[c]
+                    plen = 0 if kp >= cl else min(piece, cl - kp)
+                    lo = min(plen, b * block)
+                    hi = min(plen, lo + block)
+                    cvec = vec and start % v == 0
+                    if c != me and not (kind == RED1 and c != root):
+                        for a0, a1 in touched(lo, hi, v, cvec):
+                            if a1 > a0:
+                                assert me * piece + a1 <= n * piece
+                                pushed[c][start + kp + a0:start + kp + a1] += 1
+                    if c == me and not (kind == RED1 and me != root):
+                        for s0, s1 in fold_segments(kind, n, es, cl, kp, lo, hi, o6):
+                            for a0, a1 in fold_touched(s0, s1, v, cvec):
+                                if a1 <= a0:
+                                    continue
+                                assert lo <= a0 and a1 <= hi
+                                for q in range(n):
+                                    assert q * piece + a1 <= n * piece
+                                g0, g1 = start + kp + a0, start + kp + a1
+                                assert 0 <= g0 and g1 <= total
+                                cover1[g0:g1] += 1
+        for c in range(n):
+            start, cl = chunks[c]
+            seg = slice(start, start + cl)
+            if c == me:
+                if not (kind == RED1 and me != root):
+                    assert np.all(cover1[seg] == 1), (kind, me, c)
+            elif not (kind == RED1 and c != root):
+                assert np.all(pushed[c][seg] == 1), (kind, me, c)
+
+
+@pytest.mark.parametrize("kind", [AR1, RED1])
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("es", [1, 2, 4, 8])
+@pytest.mark.parametrize("count", [1, 5, 33, 4099, 100003])
+def test_ipc_one_shot_in_bounds_and_exact_cover(kind, n, es, count):
+    check_general(kind, n, count, es, vec=True, root=n - 1)
+    check_general(kind, n, count, es, vec=False, root=0)
+
+
+@pytest.mark.parametrize("kind", [ARMC, RS])
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
+@pytest.mark.parametrize("es", [1, 2, 4, 8])
+@pytest.mark.parametrize("count", [1, 7, 33, 4099, 70001, 300007])
+def test_ipc_o6_sub_slices_in_bounds_and_exact_cover(kind, n, es, count):
+    """Order O6 folds a block's window per sub-slice; sub-slice edges fall anywhere (scalar head/tail)."""
+    check_general(kind, n, count, es, vec=True, o6=True)
+    check_general(kind, n, count, es, vec=False, o6=True)
 
 
 def check(kind, n, count, es, vec, root=0):
