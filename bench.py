@@ -327,7 +327,8 @@ def bench_c4(comm, send, recv, world) -> dict:
            "rs_ms": round(t_rs * 1e3, 3), "ag_ms": round(t_ag * 1e3, 3),
            "rs_busbw_GBps": round(nbytes / t_rs / 1e9 * f, 2), "ag_busbw_GBps": round(nbytes / t_ag / 1e9 * f, 2),
            "rs_ag_busbw_GBps": round(2 * nbytes / (t_rs + t_ag) / 1e9 * f, 2)}
-    # the mesh ReduceScatter (order O1) and the one-sided IPC kernel with the same order: same bits
+    # the mesh ReduceScatter (order O1) and the one-sided IPC kernel with the same order: same bits; then the IPC
+    # kernel in the auto family (MeshChunk O6 here), which must match the auto ReduceScatter
     try:
         comm.set_algo(H.Algo.MESH_ONESHOT)
         t_mesh = _timed(lambda: comm.reduce_scatter(x, shard, H.HcclReduceOp.SUM, s), 3, warmup=1)
@@ -340,6 +341,15 @@ def bench_c4(comm, send, recv, world) -> dict:
         out["rs_ipc_ran"] = H.Algo(comm.last_algo).name
         out["rs_ipc_matches_mesh"] = bool(torch.equal(ref, shard.view(torch.int16)[:: 1 << 10]))
         out["rs_ipc_barrier_timeouts"] = comm.ipc_status() & 1
+        comm.set_algo(H.Algo.AUTO)
+        comm.reduce_scatter(x, shard, H.HcclReduceOp.SUM, s)
+        ref_auto = shard.view(torch.int16)[:: 1 << 10].clone()
+        comm.set_algo(H.Algo.IPC)
+        t_ipc9 = _timed(lambda: comm.reduce_scatter(x, shard, H.HcclReduceOp.SUM, s), 5)
+        out["rs_ipc_auto_family_ms"] = round(t_ipc9 * 1e3, 3)
+        out["rs_ipc_auto_family_busbw_GBps"] = round(nbytes / t_ipc9 / 1e9 * f, 2)
+        out["rs_ipc_auto_family_ran"] = H.Algo(comm.last_algo).name
+        out["rs_ipc_auto_family_matches_auto"] = bool(torch.equal(ref_auto, shard.view(torch.int16)[:: 1 << 10]))
     finally:
         comm.set_algo(H.Algo.AUTO)
     return out
@@ -348,7 +358,7 @@ def bench_c4(comm, send, recv, world) -> dict:
 def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
     """C5: AllReduce fp16 SUM, 1 KiB .. 4 GiB: latency at small sizes, busbw at large. Each size runs the RHD schedule
     (the config's algorithm), the auto selection (what the reference would run: one-shot / two-shot / MeshChunk) and,
-    up to 256 MiB, the one-sided IPC kernel (order O2, one launch per call: the latency end of the curve)."""
+    up to 256 MiB, the one-sided IPC kernel in the same order family (one launch per call: the latency end)."""
     s = torch.cuda.current_stream()
     rows = []
     nbytes = 1 << 10
@@ -359,16 +369,16 @@ def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
             b = recv.view(torch.float16)[: nbytes // 2]
             iters = 20 if nbytes <= (64 << 20) else 3
             row = {"bytes": nbytes}
-            algos = (H.Algo.RHD, H.Algo.AUTO) + ((H.Algo.IPC_TWOSHOT,) if nbytes <= (256 << 20) else ())
+            algos = (H.Algo.RHD, H.Algo.AUTO) + ((H.Algo.IPC,) if nbytes <= (256 << 20) else ())
             for algo in algos:
                 comm.set_algo(algo)
                 t = _timed(lambda: comm.all_reduce(a, b, H.HcclReduceOp.SUM, s), iters)
-                key = {H.Algo.RHD: "rhd", H.Algo.AUTO: "auto", H.Algo.IPC_TWOSHOT: "ipc"}[algo]
+                key = {H.Algo.RHD: "rhd", H.Algo.AUTO: "auto", H.Algo.IPC: "ipc"}[algo]
                 row[f"{key}_us"] = round(t * 1e6, 1)
                 row[f"{key}_busbw_GBps"] = round(nbytes / t / 1e9 * f, 2)
                 if algo == H.Algo.AUTO:
                     row["auto_algo"] = H.Algo(comm.last_algo).name
-                if algo == H.Algo.IPC_TWOSHOT:
+                if algo == H.Algo.IPC:
                     row["ipc_ran"] = H.Algo(comm.last_algo).name
                     row["ipc_barrier_timeouts"] = comm.ipc_status() & 1
             rows.append(row)
@@ -433,32 +443,30 @@ def bench_e2e_allreduce(comm, world, nbytes: int = 256 << 20, iters: int = 5, ch
 
 
 def bench_c3_algos(comm, send, recv, world) -> dict:
-    """C3 shape (fp32 SUM, 4 GiB per rank) under every AllReduce schedule, 3 timed iterations each."""
+    """C3 shape (fp32 SUM, 4 GiB per rank) under every AllReduce schedule, 3 timed iterations each. Pairs that compute
+    the same order are compared bit for bit on a sample of the output: IPC_TWOSHOT vs MESH_TWOSHOT (O2) and IPC (the
+    auto family over the one-sided kernel) vs MESH_CHUNK (O6, the auto choice at this size)."""
     import torch.distributed as dist
 
     s = torch.cuda.current_stream()
     out = {}
-    ref = None
+    digests = {}
+    twin = {H.Algo.IPC_TWOSHOT: H.Algo.MESH_TWOSHOT, H.Algo.IPC: H.Algo.MESH_CHUNK}
     try:
-        for algo in (H.Algo.MESH_TWOSHOT, H.Algo.IPC_TWOSHOT, H.Algo.MESH_CHUNK, H.Algo.RING, H.Algo.RHD,
-                     H.Algo.NHR, H.Algo.MESH_ONESHOT):
+        for algo in (H.Algo.MESH_CHUNK, H.Algo.IPC, H.Algo.MESH_TWOSHOT, H.Algo.IPC_TWOSHOT, H.Algo.RING,
+                     H.Algo.RHD, H.Algo.NHR, H.Algo.MESH_ONESHOT):
             comm.set_algo(algo)
             t = _timed(lambda: comm.all_reduce(send, recv, H.HcclReduceOp.SUM, s), 3, warmup=1)
-            row = {"ms": round(t * 1e3, 3), "busbw_GBps": round(C3_BYTES / t / 1e9 * 2 * (world - 1) / world, 2)}
-            if algo in (H.Algo.MESH_TWOSHOT, H.Algo.IPC_TWOSHOT):
-                # both compute order O2: the outputs must be identical bit for bit
-                digest = recv.view(torch.int32)[:: 1 << 12].clone()
-                if ref is None:
-                    ref = digest
-                else:
-                    same = torch.tensor([1 if torch.equal(ref, digest) else 0], dtype=torch.int32)
-                    dist.all_reduce(same, op=dist.ReduceOp.MIN)
-                    row["matches_rccl_two_shot"] = bool(same.item())
-                if algo == H.Algo.IPC_TWOSHOT:
-                    st = comm.ipc_status()
-                    row["barrier_timeouts"] = st & 1
-                    row["longest_wait_polls_log2"] = (st >> 8) & 0xFF
-                    row["ran"] = H.Algo(comm.last_algo).name  # MESH_TWOSHOT if the IPC set-up fell back
+            row = {"ms": round(t * 1e3, 3), "busbw_GBps": round(C3_BYTES / t / 1e9 * 2 * (world - 1) / world, 2),
+                   "ran": H.Algo(comm.last_algo).name}  # an IPC row reads MESH_* if the IPC set-up fell back
+            digests[algo] = recv.view(torch.int32)[:: 1 << 12].clone()
+            if algo in twin:
+                same = torch.tensor([1 if torch.equal(digests[twin[algo]], digests[algo]) else 0], dtype=torch.int32)
+                dist.all_reduce(same, op=dist.ReduceOp.MIN)
+                row[f"matches_{twin[algo].name.lower()}"] = bool(same.item())
+                st = comm.ipc_status()
+                row["barrier_timeouts"] = st & 1
+                row["longest_wait_polls_log2"] = (st >> 8) & 0xFF
             out[algo.name] = row
     finally:
         comm.set_algo(H.Algo.AUTO)
