@@ -40,6 +40,62 @@ bool Conflicts(const std::vector<Range>& a, const std::vector<Range>& b)
     return false;
 }
 
+// Length of the run of REDUCE records starting at ops[i] that can share one batched launch: same operand count
+// (>= 2), at most kMaxBatchSegs, and no record's output overlapping another record's output or inputs (the batch
+// runs them concurrently). The records of one schedule step qualify: a MeshChunk piece's O6 sub-slices, the folds of
+// the R rings or of the RHD instances.
+size_t BatchRun(const std::vector<HcclAmdIrOp>& ops, size_t i, uint64_t es, void* const bufs[3])
+{
+    const HcclAmdIrOp& o = ops[i];
+    if (o.kind != HCCL_AMD_IR_REDUCE || o.nsrc < 2) return 1;
+    auto addr = [&](int32_t buf, uint64_t off) { return reinterpret_cast<uintptr_t>(bufs[buf]) + off * es; };
+    std::vector<Range> outs, ins;
+    size_t k = i;
+    for (; k < ops.size() && k - i < kMaxBatchSegs; ++k) {
+        const HcclAmdIrOp& q = ops[k];
+        if (q.kind != HCCL_AMD_IR_REDUCE || q.nsrc != o.nsrc) break;
+        const uintptr_t d = addr(q.dstBuf, q.dstOff);
+        const Range dr{d, d + q.count * es, true};
+        std::vector<Range> qin;
+        for (int j = 0; j < q.nsrc; ++j) {
+            const uintptr_t a = addr(q.srcBuf[j], q.srcOff[j]);
+            qin.push_back({a, a + q.count * es, false});
+        }
+        bool clash = false;
+        for (const Range& r : outs) clash = clash || (dr.lo < r.hi && r.lo < dr.hi);
+        for (const Range& r : ins) clash = clash || (dr.lo < r.hi && r.lo < dr.hi);
+        for (const Range& r : qin) {
+            for (const Range& w : outs) clash = clash || (r.lo < w.hi && w.lo < r.hi);
+        }
+        if (clash) break;
+        outs.push_back(dr);
+        ins.insert(ins.end(), qin.begin(), qin.end());
+    }
+    return std::max<size_t>(1, k - i);
+}
+
+// Launches REDUCE records ops[i, i+m) (one batch, or a single fold when m == 1).
+HcclResult LaunchFolds(const std::vector<HcclAmdIrOp>& ops, size_t i, size_t m, uint64_t es, void* const bufs[3],
+                       HcclDataType dt, HcclReduceOp op, hipStream_t stream)
+{
+    auto addr = [&](int32_t buf, uint64_t off) { return reinterpret_cast<uintptr_t>(bufs[buf]) + off * es; };
+    if (m == 1) {
+        const HcclAmdIrOp& o = ops[i];
+        const void* srcs[HCCL_AMD_IR_MAX_SRC];
+        for (int j = 0; j < o.nsrc; ++j) srcs[j] = reinterpret_cast<const void*>(addr(o.srcBuf[j], o.srcOff[j]));
+        return LaunchReduceN(reinterpret_cast<void*>(addr(o.dstBuf, o.dstOff)), srcs, static_cast<uint32_t>(o.nsrc),
+                             o.count, dt, op, stream);
+    }
+    FoldSeg segs[kMaxBatchSegs];
+    for (size_t g = 0; g < m; ++g) {
+        const HcclAmdIrOp& o = ops[i + g];
+        segs[g].out = reinterpret_cast<void*>(addr(o.dstBuf, o.dstOff));
+        for (int j = 0; j < o.nsrc; ++j) segs[g].srcs[j] = reinterpret_cast<const void*>(addr(o.srcBuf[j], o.srcOff[j]));
+        segs[g].count = o.count;
+    }
+    return LaunchReduceNBatch(segs, static_cast<uint32_t>(m), static_cast<uint32_t>(ops[i].nsrc), dt, op, stream);
+}
+
 }  // namespace
 
 // Small collectives have one pipeline piece, so the two-stream split cannot overlap anything: every unit goes on
@@ -74,9 +130,10 @@ static HcclResult ExecuteSingleStream(Comm& c, const std::vector<HcclAmdIrOp>& o
             const void* src = reinterpret_cast<const void*>(addr(o.srcBuf[0], o.srcOff[0]));
             if (src != dst) HIP_CHK(hipMemcpyAsync(dst, src, o.count * es, hipMemcpyDeviceToDevice, user));
         } else if (o.kind == HCCL_AMD_IR_REDUCE) {
-            const void* srcs[HCCL_AMD_IR_MAX_SRC];
-            for (int j = 0; j < o.nsrc; ++j) srcs[j] = reinterpret_cast<const void*>(addr(o.srcBuf[j], o.srcOff[j]));
-            HCCL_CHK(LaunchReduceN(dst, srcs, static_cast<uint32_t>(o.nsrc), o.count, dt, op, user));
+            const size_t m = BatchRun(ops, i, es, bufs);
+            HCCL_CHK(LaunchFolds(ops, i, m, es, bufs, dt, op, user));
+            i += m;
+            continue;
         } else {
             return HCCL_E_INTERNAL;
         }
@@ -114,6 +171,8 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
     while (i < ops.size()) {
         Unit u;
         p2p.clear();
+        const size_t firstIdx = i;
+        size_t batch = 1;
         const HcclAmdIrOp& first = ops[i];
         const bool isComm = first.kind == HCCL_AMD_IR_SEND || first.kind == HCCL_AMD_IR_RECV;
         u.stream = isComm ? 0 : 1;
@@ -135,15 +194,18 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
                 ++i;
             }
         } else {
-            const HcclAmdIrOp& o = first;
-            const uint64_t bytes = o.count * es;
-            uintptr_t d = addr(o.dstBuf, o.dstOff);
-            u.ranges.push_back({d, d + bytes, true});
-            for (int j = 0; j < o.nsrc; ++j) {
-                uintptr_t s = addr(o.srcBuf[j], o.srcOff[j]);
-                u.ranges.push_back({s, s + bytes, false});
+            batch = BatchRun(ops, i, es, bufs);
+            for (size_t g = 0; g < batch; ++g) {
+                const HcclAmdIrOp& o = ops[i + g];
+                const uint64_t bytes = o.count * es;
+                uintptr_t d = addr(o.dstBuf, o.dstOff);
+                u.ranges.push_back({d, d + bytes, true});
+                for (int j = 0; j < o.nsrc; ++j) {
+                    uintptr_t s = addr(o.srcBuf[j], o.srcOff[j]);
+                    u.ranges.push_back({s, s + bytes, false});
+                }
             }
-            ++i;
+            i += batch;
         }
 
         // cross-stream hazards: wait for the latest conflicting unit on the other stream
@@ -169,11 +231,7 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
                     HIP_CHK(hipMemcpyAsync(dst, src, o.count * es, hipMemcpyDeviceToDevice, streams[x]));
                 }
             } else if (o.kind == HCCL_AMD_IR_REDUCE) {
-                const void* srcs[HCCL_AMD_IR_MAX_SRC];
-                for (int j = 0; j < o.nsrc; ++j) {
-                    srcs[j] = reinterpret_cast<const void*>(addr(o.srcBuf[j], o.srcOff[j]));
-                }
-                HCCL_CHK(LaunchReduceN(dst, srcs, static_cast<uint32_t>(o.nsrc), o.count, dt, op, streams[x]));
+                HCCL_CHK(LaunchFolds(ops, firstIdx, batch, es, bufs, dt, op, streams[x]));
             } else {
                 return HCCL_E_INTERNAL;
             }

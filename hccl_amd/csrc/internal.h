@@ -30,6 +30,19 @@ HcclResult LaunchReduceN(void* out, const void* const* srcs, uint32_t n, uint64_
                          HcclReduceOp op, hipStream_t stream);
 HcclResult SetReduceLaunch(uint32_t blocksPerCu, uint32_t unroll, uint32_t cachePolicy);
 
+// Several independent ordered folds with the same operand count in ONE launch (blockIdx.y = segment): the executor
+// batches the consecutive REDUCE records of a schedule step (a MeshChunk piece's O6 sub-slices, the R rings' or RHD
+// instances' folds). Segments must not overlap each other's outputs. Falls back to one launch per segment when a
+// segment's pointers do not share a 16-B phase.
+constexpr uint32_t kMaxBatchSegs = 8;
+struct FoldSeg {
+    void* out;
+    const void* srcs[HCCL_AMD_IR_MAX_SRC];
+    uint64_t count;
+};
+HcclResult LaunchReduceNBatch(const FoldSeg* segs, uint32_t nseg, uint32_t nsrc, HcclDataType dt, HcclReduceOp op,
+                              hipStream_t stream);
+
 // ---- logging
 bool DebugEnabled();
 

@@ -17,6 +17,7 @@
 // denormals are preserved (checked in the code object: .amdhsa_float_denorm_mode_32 = 3).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstring>
 #include <mutex>
@@ -114,15 +115,16 @@ struct SrcPack {
     const void* p[HCCL_AMD_IR_MAX_SRC];
 };
 
+// One ordered fold over `nvec` 16-B vectors (plus scalar edges), worked by `nblocks` workgroups, this one `bid`.
 template <class E, int OP, int U, int NT>
-__global__ __launch_bounds__(kBlock) void k_reduceN(typename E::S* out, SrcPack srcs, int nsrc, uint64_t nvec,
-                                                      Edges edges)
+__device__ __forceinline__ void ReduceNBody(typename E::S* out, const SrcPack& srcs, int nsrc, uint64_t nvec,
+                                            Edges edges, uint32_t bid, uint32_t nblocks)
 {
     using S = typename E::S;
     constexpr uint64_t kTile = uint64_t(kBlock) * U;
     u32x4* vout = reinterpret_cast<u32x4*>(out + edges.head);
     const uint64_t fullTiles = nvec / kTile;
-    for (uint64_t t = blockIdx.x; t < fullTiles; t += gridDim.x) {
+    for (uint64_t t = bid; t < fullTiles; t += nblocks) {
         const uint64_t base = t * kTile + threadIdx.x;
         u32x4 acc[U];
         const u32x4* p0 = reinterpret_cast<const u32x4*>(static_cast<const S*>(srcs.p[0]) + edges.head);
@@ -147,8 +149,8 @@ __global__ __launch_bounds__(kBlock) void k_reduceN(typename E::S* out, SrcPack 
             st<NT>(vout + base + u * kBlock, acc[u]);
         }
     }
-    for (uint64_t i = fullTiles * kTile + uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < nvec;
-         i += uint64_t(gridDim.x) * kBlock) {
+    for (uint64_t i = fullTiles * kTile + uint64_t(bid) * kBlock + threadIdx.x; i < nvec;
+         i += uint64_t(nblocks) * kBlock) {
         u32x4 acc = ld<NT>(reinterpret_cast<const u32x4*>(static_cast<const S*>(srcs.p[0]) + edges.head) + i);
         for (int j = 1; j < nsrc; ++j) {
             acc = combine<E, OP>(ld<NT>(reinterpret_cast<const u32x4*>(static_cast<const S*>(srcs.p[j]) + edges.head) + i),
@@ -156,7 +158,7 @@ __global__ __launch_bounds__(kBlock) void k_reduceN(typename E::S* out, SrcPack 
         }
         st<NT>(vout + i, acc);
     }
-    if (blockIdx.x == 0) {
+    if (bid == 0) {
         uint32_t tid = threadIdx.x;
         uint64_t i;
         bool act = false;
@@ -175,6 +177,30 @@ __global__ __launch_bounds__(kBlock) void k_reduceN(typename E::S* out, SrcPack 
             out[i] = acc;
         }
     }
+}
+
+template <class E, int OP, int U, int NT>
+__global__ __launch_bounds__(kBlock) void k_reduceN(typename E::S* out, SrcPack srcs, int nsrc, uint64_t nvec,
+                                                      Edges edges)
+{
+    ReduceNBody<E, OP, U, NT>(out, srcs, nsrc, nvec, edges, blockIdx.x, gridDim.x);
+}
+
+// A batch of independent folds: segment blockIdx.y, worked by the gridDim.x workgroups of its row.
+struct BatchPack {
+    void* out[kMaxBatchSegs];
+    SrcPack srcs[kMaxBatchSegs];
+    uint64_t nvec[kMaxBatchSegs];
+    Edges edges[kMaxBatchSegs];
+    int nsrc;
+};
+
+template <class E, int OP, int U, int NT>
+__global__ __launch_bounds__(kBlock) void k_reduceN_batch(BatchPack pk)
+{
+    const uint32_t g = blockIdx.y;
+    ReduceNBody<E, OP, U, NT>(static_cast<typename E::S*>(pk.out[g]), pk.srcs[g], pk.nsrc, pk.nvec[g], pk.edges[g],
+                              blockIdx.x, gridDim.x);
 }
 
 template <class E, int OP>
@@ -491,6 +517,92 @@ HcclResult LaunchReduceN(void* out, const void* const* srcs, uint32_t n, uint64_
     }
     if (e != hipSuccess) {
         HCCL_AMD_ERR("reduceN launch failed: %s", hipGetErrorString(e));
+        return HCCL_E_RUNTIME;
+    }
+    return HCCL_SUCCESS;
+}
+
+namespace {
+
+template <class E, int OP>
+hipError_t RunBatch(const BatchPack& pk, uint32_t nseg, uint64_t maxVec, hipStream_t stream)
+{
+    // fill the chip once across the batch: the per-CU budget of the n-ary default, split over the segments
+    const LaunchCfg cfg = kDefaultN;
+    const uint64_t cap = std::max<uint64_t>(1, uint64_t(CuCount()) * cfg.blocksPerCu / nseg);
+    const uint64_t need = std::max<uint64_t>(1, (maxVec + kBlock * cfg.unroll - 1) / (kBlock * cfg.unroll));
+    const uint32_t gx = static_cast<uint32_t>(std::min(cap, need));
+    hipLaunchKernelGGL((k_reduceN_batch<E, OP, kDefaultN.unroll, kDefaultN.nt>), dim3(gx, nseg), dim3(kBlock), 0,
+                       stream, pk);
+    return hipGetLastError();
+}
+
+template <class E>
+hipError_t DispatchBatch(int op, const BatchPack& pk, uint32_t nseg, uint64_t maxVec, hipStream_t s)
+{
+    switch (op) {
+        case R_SUM: return RunBatch<E, R_SUM>(pk, nseg, maxVec, s);
+        case R_PROD: return RunBatch<E, R_PROD>(pk, nseg, maxVec, s);
+        case R_MAX: return RunBatch<E, R_MAX>(pk, nseg, maxVec, s);
+        default: return RunBatch<E, R_MIN>(pk, nseg, maxVec, s);
+    }
+}
+
+}  // namespace
+
+HcclResult LaunchReduceNBatch(const FoldSeg* segs, uint32_t nseg, uint32_t nsrc, HcclDataType dt, HcclReduceOp op,
+                              hipStream_t stream)
+{
+    if (!ValidOp(op) || nsrc < 2 || nsrc > HCCL_AMD_IR_MAX_SRC || nseg > kMaxBatchSegs) return HCCL_E_PARA;
+    const uint32_t es = DataTypeSize(dt);
+    if (es == 0) return HCCL_E_NOT_SUPPORT;
+    BatchPack pk{};
+    pk.nsrc = int(nsrc);
+    uint32_t nb = 0;
+    uint64_t maxVec = 0;
+    for (uint32_t g = 0; g < nseg; ++g) {
+        const FoldSeg& f = segs[g];
+        if (f.count == 0) continue;
+        const void* ptrs[HCCL_AMD_IR_MAX_SRC + 1];
+        ptrs[0] = f.out;
+        for (uint32_t j = 0; j < nsrc; ++j) ptrs[j + 1] = f.srcs[j];
+        Edges edges{};
+        uint64_t nvec = 0;
+        bool ok = false;
+        switch (es) {
+            case 1: ok = SplitAligned<uint8_t>(ptrs, int(nsrc) + 1, f.count, &edges, &nvec); break;
+            case 2: ok = SplitAligned<uint16_t>(ptrs, int(nsrc) + 1, f.count, &edges, &nvec); break;
+            case 4: ok = SplitAligned<uint32_t>(ptrs, int(nsrc) + 1, f.count, &edges, &nvec); break;
+            default: ok = SplitAligned<uint64_t>(ptrs, int(nsrc) + 1, f.count, &edges, &nvec); break;
+        }
+        // a segment whose pointers do not share a 16-B phase runs on its own (scalar kernel)
+        if (!ok) {
+            HCCL_CHK(LaunchReduceN(f.out, f.srcs, nsrc, f.count, dt, op, stream));
+            continue;
+        }
+        pk.out[nb] = f.out;
+        for (uint32_t j = 0; j < nsrc; ++j) pk.srcs[nb].p[j] = f.srcs[j];
+        pk.nvec[nb] = nvec;
+        pk.edges[nb] = edges;
+        maxVec = std::max(maxVec, nvec);
+        ++nb;
+    }
+    if (nb == 0) return HCCL_SUCCESS;
+    hipError_t e;
+    switch (dt) {
+        case HCCL_DATA_TYPE_INT8: e = DispatchBatch<EI8>(op, pk, nb, maxVec, stream); break;
+        case HCCL_DATA_TYPE_INT16: e = DispatchBatch<EI16>(op, pk, nb, maxVec, stream); break;
+        case HCCL_DATA_TYPE_INT32: e = DispatchBatch<EI32>(op, pk, nb, maxVec, stream); break;
+        case HCCL_DATA_TYPE_INT64: e = DispatchBatch<EI64>(op, pk, nb, maxVec, stream); break;
+        case HCCL_DATA_TYPE_UINT64: e = DispatchBatch<EU64>(op, pk, nb, maxVec, stream); break;
+        case HCCL_DATA_TYPE_FP16: e = DispatchBatch<EF16>(op, pk, nb, maxVec, stream); break;
+        case HCCL_DATA_TYPE_BFP16: e = DispatchBatch<EBF16>(op, pk, nb, maxVec, stream); break;
+        case HCCL_DATA_TYPE_FP32: e = DispatchBatch<EF32>(op, pk, nb, maxVec, stream); break;
+        case HCCL_DATA_TYPE_FP64: e = DispatchBatch<EF64>(op, pk, nb, maxVec, stream); break;
+        default: return HCCL_E_NOT_SUPPORT;
+    }
+    if (e != hipSuccess) {
+        HCCL_AMD_ERR("batched reduce launch failed: %s", hipGetErrorString(e));
         return HCCL_E_RUNTIME;
     }
     return HCCL_SUCCESS;
