@@ -349,6 +349,7 @@ class HostExchangeTransport : public Transport {
 public:
     HostExchangeTransport(HcclAmdHostAllGatherFn fn, void* ctx) : fn_(fn), ctx_(ctx) {}
     const char* Name() const override { return "host-exchange"; }
+    bool HasSendRecv() const override { return false; }
     HcclResult Group(const std::vector<P2pOp>&, hipStream_t) override
     {
         HCCL_AMD_ERR("host-exchange communicator has no send/recv path (only the IPC AllReduce)");

@@ -36,6 +36,8 @@ public:
     virtual HcclResult AllGatherHost(const void* mine, size_t bytes, void* all) = 0;
     // True when every rank lives in this process on this device (loopback world).
     virtual bool SharedDevice() const { return false; }
+    // False for a bootstrap-only transport: the communicator's only data path is the one-sided IPC kernel.
+    virtual bool HasSendRecv() const { return true; }
 };
 
 std::unique_ptr<Transport> MakeRcclTransport(void* uniqueId, uint32_t nRanks, uint32_t rank, HcclResult* err);

@@ -80,6 +80,11 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     ScheduleParams p;
     p.opType = opType;
     p.algo = c.algoOverride;
+    // an IPC-only communicator (bootstrap transport without send/recv) runs every reducing op on the IPC kernel in
+    // the auto family, whatever schedule family was asked for
+    if (!c.transport->HasSendRecv() && opType != HCCL_AMD_OP_ALLGATHER && p.algo != HCCL_AMD_ALGO_IPC_TWOSHOT) {
+        p.algo = HCCL_AMD_ALGO_IPC;
+    }
     if (p.algo == HCCL_AMD_ALGO_AUTO && NeedStrictOrder(opType, dt, op, c.nRanks)) {
         p.algo = HCCL_AMD_ALGO_ORDER_PRESERVED;
     }
