@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "internal.h"
 
@@ -103,6 +104,18 @@ template <class E, int OP>
 __device__ __forceinline__ u32x4 combine(u32x4 s, u32x4 d)
 {
     using S = typename E::S;
+    if constexpr (std::is_same<E, EInt<int8_t, uint32_t>>::value && OP == R_SUM) {
+        // int8 SUM, four lanes per dword without unpacking: add the low 7 bits of every byte (no carry can cross a
+        // byte), then put back each byte's top bit as the XOR of the operands' top bits and that carry. Two's
+        // complement wrap per byte, the same bits as the per-element rule.
+        u32x4 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t a = s[i], b = d[i];
+            r[i] = ((a & 0x7F7F7F7Fu) + (b & 0x7F7F7F7Fu)) ^ ((a ^ b) & 0x80808080u);
+        }
+        return r;
+    }
     constexpr int N = 16 / sizeof(S);
     S a[N];
     S b[N];

@@ -1,6 +1,7 @@
 """Roofline table of the shipped reduce kernels on one MI355X (default launch configuration):
   1. every dtype x op of k_reduce2 at 1 GiB per operand (3 streams), HBM GB/s and fraction of 8 TB/s;
-  2. the ordered n-ary fold k_reduceN at n = 2..16 over 256 MiB per input ((n+1) streams);
+  2. the ordered n-ary fold k_reduceN at n = 2..16 over 1 GiB per input ((n+1) streams; 1 GiB keeps the working
+     set far above the 256 MiB Infinity Cache, whose hits made 256 MiB inputs read box-dependently fast);
   3. the fp32 SUM local reduce from 1 KiB to 1 GiB per operand (launch latency to bandwidth).
 Median of interleaved rounds; algorithmic bytes only. One JSON line per measurement."""
 import json
@@ -43,11 +44,11 @@ def main():
                               "us": round(t * 1e6, 1), "GBps": round(3 * GIB / t / 1e9, 1),
                               "frac_8TBps": round(3 * GIB / t / 8e12, 4)}), flush=True)
     # 2. n-ary fold
-    per = 256 << 20
+    per = 1 << 30
     bufs = [torch.empty(per // 4, dtype=torch.float32, device="cuda").uniform_() for _ in range(16)]
     out = torch.empty_like(bufs[0])
     for n in (2, 3, 4, 8, 16):
-        ts = sorted(timeit(lambda: H.local_reduce_n(out, bufs[:n]), 10) for _ in range(3))
+        ts = sorted(timeit(lambda: H.local_reduce_n(out, bufs[:n]), 5) for _ in range(3))
         t = ts[1]
         nbytes = (n + 1) * per
         print(json.dumps({"table": "reduce_n", "n": n, "bytes": nbytes, "us": round(t * 1e6, 1),
