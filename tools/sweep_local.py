@@ -20,10 +20,14 @@ def main():
     src = torch.rand(N, device="cuda") * 2 - 1
     dst = torch.rand(N, device="cuda") * 2 - 1
     out = torch.empty_like(src)
-    # cache policy: 1 plain, 2 nt loads, 3 nt stores, 4 nt both, 5 nt both + contiguous per-workgroup tile runs
-    variants = [(b, u, pol, mode) for b, u, pol in itertools.product([1, 2, 3, 4], [1, 2, 4], [1, 2, 3, 4, 5])
-                for mode in ("inplace",)]
-    variants += [(b, u, 4, "outofplace") for b, u in itertools.product([1, 2, 3, 4], [1, 2])]
+    # cache policy: 1 plain, 2 nt loads, 3 nt stores, 4 nt both, 5 nt both + contiguous per-workgroup tile runs.
+    # SWEEP_QUICK=1: the four best launch shapes only.
+    if os.environ.get("SWEEP_QUICK") == "1":
+        variants = [(b, u, 4, mode) for b, u in ((2, 1), (1, 2), (2, 2), (1, 1)) for mode in ("inplace", "outofplace")]
+    else:
+        variants = [(b, u, pol, mode) for b, u, pol in itertools.product([1, 2, 3, 4], [1, 2, 4], [1, 2, 3, 4, 5])
+                    for mode in ("inplace",)]
+        variants += [(b, u, 4, "outofplace") for b, u in itertools.product([1, 2, 3, 4], [1, 2])]
     res = {v: [] for v in variants}
     s = torch.cuda.current_stream()
     for _ in range(ROUNDS):
