@@ -457,27 +457,33 @@ def bench_c3_algos(comm, send, recv, world) -> dict:
     digests = {}
     twin = {H.Algo.IPC_TWOSHOT: H.Algo.MESH_TWOSHOT, H.Algo.IPC: H.Algo.MESH_CHUNK}
     try:
-        for algo in (H.Algo.MESH_CHUNK, H.Algo.IPC, H.Algo.MESH_TWOSHOT, H.Algo.IPC_TWOSHOT, H.Algo.RING,
-                     H.Algo.RHD, H.Algo.NHR, H.Algo.MESH_ONESHOT):
+        # (schedule, IPC workgroups per launch; 0 = default 128)
+        for algo, blocks in ((H.Algo.MESH_CHUNK, 0), (H.Algo.IPC, 0), (H.Algo.IPC, 256), (H.Algo.MESH_TWOSHOT, 0),
+                             (H.Algo.IPC_TWOSHOT, 0), (H.Algo.RING, 0), (H.Algo.RHD, 0), (H.Algo.NHR, 0),
+                             (H.Algo.MESH_ONESHOT, 0)):
+            name = algo.name if blocks == 0 else f"{algo.name}_{blocks}_BLOCKS"
             comm.set_algo(algo)
+            comm.set_ipc_blocks(blocks)
             try:
                 t = _timed(lambda: comm.all_reduce(send, recv, H.HcclReduceOp.SUM, s), 3, warmup=1)
             except H.HcclError as e:  # one schedule failing never hides the others
-                out[algo.name] = {"error": str(e)}
+                out[name] = {"error": str(e)}
                 continue
             row = {"ms": round(t * 1e3, 3), "busbw_GBps": round(C3_BYTES / t / 1e9 * 2 * (world - 1) / world, 2),
                    "ran": H.Algo(comm.last_algo).name}  # an IPC row reads MESH_* if the IPC set-up fell back
-            digests[algo] = recv.view(torch.int32)[:: 1 << 12].clone()
+            digests.setdefault(algo, recv.view(torch.int32)[:: 1 << 12].clone())
+            digest = recv.view(torch.int32)[:: 1 << 12].clone()
             if algo in twin and twin[algo] in digests:
-                same = torch.tensor([1 if torch.equal(digests[twin[algo]], digests[algo]) else 0], dtype=torch.int32)
+                same = torch.tensor([1 if torch.equal(digests[twin[algo]], digest) else 0], dtype=torch.int32)
                 dist.all_reduce(same, op=dist.ReduceOp.MIN)
                 row[f"matches_{twin[algo].name.lower()}"] = bool(same.item())
                 st = comm.ipc_status()
                 row["barrier_timeouts"] = st & 1
                 row["longest_wait_polls_log2"] = (st >> 8) & 0xFF
-            out[algo.name] = row
+            out[name] = row
     finally:
         comm.set_algo(H.Algo.AUTO)
+        comm.set_ipc_blocks(0)
     return out
 
 

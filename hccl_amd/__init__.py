@@ -157,6 +157,9 @@ class Comm:
     def set_piece_bytes(self, nbytes: int) -> None:
         check("HcclAmdCommSetPieceBytes", lib.HcclAmdCommSetPieceBytes(self.handle, nbytes))
 
+    def set_ipc_blocks(self, blocks: int) -> None:
+        check("HcclAmdCommSetIpcBlocks", lib.HcclAmdCommSetIpcBlocks(self.handle, blocks))
+
     @property
     def last_algo(self) -> int:
         return lib.HcclAmdCommLastAlgo(self.handle)

@@ -157,6 +157,7 @@ SIGNATURES = {
     "HcclAmdCommInitLoopback": (_res, [_u32, ctypes.POINTER(_vp)]),
     "HcclAmdCommSetAlgo": (_res, [_vp, _i32]),
     "HcclAmdCommSetPieceBytes": (_res, [_vp, _u64]),
+    "HcclAmdCommSetIpcBlocks": (_res, [_vp, _u32]),
     "HcclAmdCommLastAlgo": (_i32, [_vp]),
     "HcclAmdCommIpcStatus": (_res, [_vp, ctypes.POINTER(_u32)]),
     "HcclAmdCommInitHostExchange": (_res, [_u32, _u32, _vp, _vp, ctypes.POINTER(_vp)]),

@@ -44,7 +44,7 @@ HcclResult IpcSetup(Comm& c)
     s.blocks = kIpcBlocks;
     s.stgInBytes = kIpcStagingBytes;
     s.stgResBytes = kIpcStagingBytes;  // results of a whole round, in round coordinates
-    const size_t flagBytes = size_t(s.blocks) * kIpcMaxRanks * sizeof(uint32_t);
+    const size_t flagBytes = size_t(kIpcMaxBlocks) * kIpcMaxRanks * sizeof(uint32_t);
     // The fresh uncached pages may carry lines of a freed cached buffer in some XCD's L2: scrub the L2s before the
     // flags are zeroed (ScrubL2), so that no stale line is ever read or written back over them.
     bool ok = hipExtMallocWithFlags(&s.stg, s.stgInBytes + s.stgResBytes, hipDeviceMallocUncached) == hipSuccess &&
@@ -186,6 +186,10 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
     HCCL_CHK(IpcSetup(c));
     IpcState& s = c.ipc;
     const uint32_t n = c.nRanks;
+    // workgroups per rank (equal on every rank: block b pairs with block b of each peer). A loopback world runs every
+    // rank's blocks in one launch on one GPU, so it keeps the default to stay co-resident.
+    s.blocks = c.ipcBlocks != 0 ? c.ipcBlocks : kIpcBlocks;
+    if (c.transport->SharedDevice()) s.blocks = std::min(s.blocks, kIpcBlocks);
     const uint64_t V = 16 / es;
 
     IpcArgs a{};

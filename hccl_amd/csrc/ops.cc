@@ -303,6 +303,15 @@ HcclResult HcclAmdCommSetAlgo(HcclComm comm, int32_t algo)
     return HCCL_SUCCESS;
 }
 
+HcclResult HcclAmdCommSetIpcBlocks(HcclComm comm, uint32_t blocks)
+{
+    Comm* c = AsComm(comm);
+    if (c == nullptr) return HCCL_E_PTR;
+    if (blocks > kIpcMaxBlocks) return HCCL_E_PARA;
+    c->ipcBlocks = blocks;
+    return HCCL_SUCCESS;
+}
+
 HcclResult HcclAmdCommSetPieceBytes(HcclComm comm, uint64_t pieceBytes)
 {
     Comm* c = AsComm(comm);

@@ -31,6 +31,9 @@ CASES = [
     # n = 4 and 1 MiB at n = 2), two-shot O2 AllReduce at n = 4
     (AR, O.FP32, O.SUM, 5001, 9), (AR, O.FP32, O.SUM, (20 << 20) // 4 + 3, 9), (RS, O.FP32, O.SUM, (5 << 20) // 4 + 1, 9),
     (RED, O.FP16, O.SUM, 3001, 9), (AR, O.BFP16, O.MAX, 70001, 9),
+    # HcclAmdCommSetIpcBlocks: 256 and 64 workgroups per launch instead of 128 (different windows per block)
+    (AR, O.FP32, O.SUM, (20 << 20) // 4 + 3, 9, 256), (AR, O.FP32, O.SUM, 40961, 7, 64),
+    (RS, O.FP32, O.SUM, 70001, 7, 256),
 ]
 UNALIGNED_CASE = CASES.index((AR, O.FP32, O.SUM, 250001))
 ROOT = 1
@@ -76,6 +79,7 @@ def _rank_main(rank, n, port, q):
             kind, dtype, op, count = case[:4]
             forced = case[4] if len(case) > 4 else None
             comm.set_algo(forced if forced is not None else R.ALGO_IPC)
+            comm.set_ipc_blocks(case[5] if len(case) > 5 else 0)
             progress.write(f"case {i} {CASES[i]} start\n")
             send = to_device(dtype, _inputs(dtype, _in_count(kind, count, n), n, i)[rank])
             recv = torch.zeros(count, dtype=send.dtype, device=send.device)
