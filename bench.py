@@ -34,6 +34,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH
 C2_COUNT = 1 << 28      # 268,435,456 fp32 = 1 GiB per buffer
 C3_BYTES = 4 << 30      # 4 GiB per rank
 GIB = float(1 << 30)
+XGMI_LINK_GBPS = 76.8  # one xGMI link, one direction: the brief's 153 GB/s per link counts both directions
 
 
 def log(*a):
@@ -549,6 +550,7 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     per_step = elapsed / args.steps
     algbw = C3_BYTES / per_step / 1e9
     busbw = algbw * 2 * (world - 1) / world
+    xgmi_peak = min(world - 1, 7) * XGMI_LINK_GBPS
     value = world * C3_BYTES * args.steps / elapsed / GIB
     algo = comm.last_algo
     extra = {}
@@ -593,11 +595,12 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
         "roofline": {
             "bound": "xgmi",
             "achieved": round(busbw, 2),
-            "peak": 7 * 153.6 / 2,
+            "peak": round(xgmi_peak, 1),
             "unit": "GB/s",
-            "frac": round(busbw / (7 * 153.6 / 2), 4),
+            "frac": round(busbw / xgmi_peak, 4),
             "traffic": None,
-            "note": "busbw = algbw*2(n-1)/n against 7 xGMI links x 76.8 GB/s per direction",
+            "note": f"busbw = algbw*2(n-1)/n against the {world - 1} direct xGMI links a rank has to its peers "
+                    "x 76.8 GB/s per direction (fully connected node: one link per peer)",
         },
     }
     return res if rank == 0 else None
