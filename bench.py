@@ -597,7 +597,7 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
             "achieved": round(busbw, 2),
             "peak": round(xgmi_peak, 1),
             "unit": "GB/s",
-            "frac": round(busbw / xgmi_peak, 4),
+            "frac": None if harness else round(busbw / xgmi_peak, 4),  # one shared GPU has no xGMI in the path
             "traffic": None,
             "note": f"busbw = algbw*2(n-1)/n against the {world - 1} direct xGMI links a rank has to its peers "
                     "x 76.8 GB/s per direction (fully connected node: one link per peer)",
