@@ -71,7 +71,7 @@ struct Comm {
     size_t nextEvent = 0;
 
     IpcState ipc;  // one-sided AllReduce path, set up on first use (collectively)
-    uint32_t ipcBlocks = 0;  // workgroups per IPC launch, 0 = kIpcBlocks (HcclAmdCommSetIpcBlocks)
+    uint32_t ipcBlocks = 0;  // workgroups per IPC launch, 0 = DefaultIpcBlocks(bytes) (HcclAmdCommSetIpcBlocks)
 
     HcclResult Init(int dev);
     HcclResult NextEvent(hipEvent_t* e);

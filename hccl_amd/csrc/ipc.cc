@@ -159,6 +159,20 @@ void IpcRelease(Comm& c)
     s = IpcState{};
 }
 
+// Default workgroups per launch by the bytes of one rank's input. Every block runs its own cross-rank barrier (a
+// system-scope release, one flag store per peer, a poll), so small calls pay per block: 16 blocks run a 1 KiB
+// AllReduce in 11 us where 128 take 25 us and 256 take 42 us; large calls want the whole chip (1 GiB: 256 blocks
+// 10 % ahead of 128). Rank-mode sweep on one GPU, n = 2 and 4 (tools/sweep_ipc_blocks.py,
+// profiles/r01_sweep_ipc_blocks.jsonl); the best count agreed between n = 2 and 4 at every size.
+uint32_t DefaultIpcBlocks(uint64_t bytes)
+{
+    if (bytes <= (512ull << 10)) return 16;
+    if (bytes <= (2ull << 20)) return 32;
+    if (bytes <= (32ull << 20)) return 64;
+    if (bytes <= (64ull << 20)) return 128;
+    return kIpcMaxBlocks;
+}
+
 HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void* sendBuf, void* recvBuf,
                             uint64_t count, HcclDataType dt, HcclReduceOp op, uint32_t root, hipStream_t stream)
 {
@@ -186,9 +200,11 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
     HCCL_CHK(IpcSetup(c));
     IpcState& s = c.ipc;
     const uint32_t n = c.nRanks;
-    // workgroups per rank (equal on every rank: block b pairs with block b of each peer). A loopback world runs every
-    // rank's blocks in one launch on one GPU, so it keeps the default to stay co-resident.
-    s.blocks = c.ipcBlocks != 0 ? c.ipcBlocks : kIpcBlocks;
+    // workgroups per rank (equal on every rank: block b pairs with block b of each peer, and the default is a function
+    // of the call's arguments alone). A loopback world runs every rank's blocks in one launch on one GPU, so it keeps
+    // at most kIpcBlocks per rank to stay co-resident.
+    const uint64_t callBytes = (opType == HCCL_AMD_OP_REDUCE_SCATTER ? uint64_t(c.nRanks) : 1u) * count * es;
+    s.blocks = c.ipcBlocks != 0 ? c.ipcBlocks : DefaultIpcBlocks(callBytes);
     if (c.transport->SharedDevice()) s.blocks = std::min(s.blocks, kIpcBlocks);
     const uint64_t V = 16 / es;
 

@@ -92,8 +92,9 @@ struct IpcState {
     uint32_t blocks = 0;
 };
 
-constexpr uint32_t kIpcBlocks = 128;     // default workgroups per rank and launch
+constexpr uint32_t kIpcBlocks = 128;     // workgroups per rank and launch in a loopback world (cap)
 constexpr uint32_t kIpcMaxBlocks = 256;  // flags are sized for this many (HcclAmdCommSetIpcBlocks)
+uint32_t DefaultIpcBlocks(uint64_t bytes);  // workgroups per launch when the communicator sets none (ipc.cc)
 constexpr size_t kIpcStatusBytes = 16;  // status words, reset as one 16-B block per call
 constexpr uint64_t kIpcStagingBytes = 128ull << 20;  // slot area per rank; the result area is as large
 
