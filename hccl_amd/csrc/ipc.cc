@@ -44,10 +44,12 @@ HcclResult IpcSetup(Comm& c)
     s.blocks = kIpcBlocks;
     s.stgInBytes = kIpcStagingBytes;
     s.stgResBytes = kIpcStagingBytes;  // results of a whole round, in round coordinates
+    s.stgAltBytes = kIpcStagingBytes;  // slots of the single-barrier kinds, two areas used alternately
     const size_t flagBytes = size_t(kIpcMaxBlocks) * kIpcMaxRanks * sizeof(uint32_t);
     // The fresh uncached pages may carry lines of a freed cached buffer in some XCD's L2: scrub the L2s before the
     // flags are zeroed (ScrubL2), so that no stale line is ever read or written back over them.
-    bool ok = hipExtMallocWithFlags(&s.stg, s.stgInBytes + s.stgResBytes, hipDeviceMallocUncached) == hipSuccess &&
+    bool ok = hipExtMallocWithFlags(&s.stg, s.stgInBytes + s.stgResBytes + 2 * s.stgAltBytes,
+                                    hipDeviceMallocUncached) == hipSuccess &&
               hipExtMallocWithFlags(reinterpret_cast<void**>(&s.flags), flagBytes, hipDeviceMallocUncached) ==
                   hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&s.status), kIpcStatusBytes) == hipSuccess &&
@@ -221,7 +223,11 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
     a.root = root;
     a.timeoutTicks = IpcTimeoutTicks();  // a lost peer ends the kernel with status bit 0, never a hang
     a.status = s.status;
-    const uint64_t slotCap = (s.stgInBytes / es / n) / V * V;
+    a.callSeq = ++s.callSeq;  // equal on every rank of a loopback world (each runs this once per call)
+    a.altOff = s.stgInBytes + s.stgResBytes;
+    a.altBytes = s.stgAltBytes;
+    const bool single = SingleBarrierKind(kind);
+    const uint64_t slotCap = ((single ? s.stgAltBytes : s.stgInBytes) / es / n) / V * V;
 
     // One launch per executor loop [off, off + cnt) of the reference template whose order the fold follows: its
     // slicing is per loop (schedule.cc RefLoopElems and the MeshChunk loops).
@@ -284,14 +290,13 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
         g.blockElems = ((g.piece + s.blocks - 1) / s.blocks + V - 1) / V * V;
         g.rounds = static_cast<uint32_t>((widest + g.piece - 1) / g.piece);
         g.epochBase = s.epoch;
-        s.epoch += 2 * g.rounds;
+        s.epoch += (single ? 1 : 2) * g.rounds;
     };
     auto at = [es](const void* p, uint64_t off) { return static_cast<char*>(const_cast<void*>(p)) + off * es; };
 
     if (!c.transport->SharedDevice()) {
         a.me = static_cast<int32_t>(c.rank);
         a.aligned = Aligned16(sendBuf, recvBuf);
-        HIP_CHK(hipMemsetAsync(s.status + 1, 0, sizeof(uint32_t), stream));  // wait diagnostic of this call
         for (const Launch& l : launches) {
             a.in[c.rank] = at(sendBuf, l.off);
             a.out[c.rank] = at(recvBuf, l.off);
@@ -321,7 +326,6 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
             a.aligned = a.aligned && Aligned16(all[r].in, all[r].out);
             HIP_CHK(hipStreamWaitEvent(stream, all[r].ready, 0));
         }
-        HIP_CHK(hipMemsetAsync(s.status + 1, 0, sizeof(uint32_t), stream));
         for (const Launch& l : launches) {
             for (uint32_t r = 0; r < n; ++r) {
                 a.in[r] = at(all[r].in, l.off);
@@ -350,10 +354,11 @@ extern "C" HcclResult HcclAmdCommIpcStatus(HcclComm comm, uint32_t* status)
     *status = 0;
     if (!c->ipc.ready) return HCCL_SUCCESS;
     HIP_CHK(hipSetDevice(c->device));
-    uint32_t w[2] = {0, 0};
+    uint32_t w[4] = {0, 0, 0, 0};
     HIP_CHK(hipMemcpy(w, c->ipc.status, sizeof w, hipMemcpyDeviceToHost));
+    const uint32_t wait = w[3] == c->ipc.callSeq ? w[2] : 0;  // an older tag: no block of the last call waited
     uint32_t lg = 0;
-    while (lg < 32 && (uint64_t(1) << lg) <= w[1]) ++lg;  // bit length of the longest wait
+    while (lg < 32 && (uint64_t(1) << lg) <= wait) ++lg;  // bit length of the longest wait
     *status = (w[0] & 0xFFu) | (lg << 8);
     return HCCL_SUCCESS;
 }

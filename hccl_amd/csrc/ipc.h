@@ -33,6 +33,14 @@ enum IpcSubMode : uint32_t {
     kIpcSubRs4K = 1,
 };
 
+// Kinds whose fold reads only slots and writes only the rank's own output (no result push, no phase 2). They need
+// one barrier per round: their slots alternate between two areas that no other kind touches, so the next round's
+// stores never meet this round's fold (k_ipc_collective). The others keep two (results must be complete before phase 2).
+__host__ __device__ constexpr bool SingleBarrierKind(uint32_t kind)
+{
+    return kind == kIpcReduceScatter || kind == kIpcAllReduceOneShot || kind == kIpcReduceOneShot;
+}
+
 // Kernel arguments. In rank mode (me >= 0) only in[me] / out[me] are used; stgIn / stgRes / flags hold every rank's
 // mapping (own allocation at [me], peers opened through hipIpcOpenMemHandle). In world mode (me < 0) every table is
 // full and blockIdx.y is the rank.
@@ -43,7 +51,9 @@ enum IpcSubMode : uint32_t {
 // is the whole range and every rank owns it. Round k handles piece k of every chunk: chunk elements
 // [k*piece, (k+1)*piece). Block b always handles piece coordinates [b*blockElems, (b+1)*blockElems), so every round
 // of a launch touches the same slot and result addresses per block and the per-block barrier is sound.
-// Staging: owner c's slot q = stgIn[c] + q*piece; results of chunk c at stgRes[p] + c*piece.
+// Staging: owner c's slot q = stgIn[c] + q*piece; results of chunk c at stgRes[p] + c*piece. The single-barrier kinds
+// (SingleBarrierKind) put their slots in one of two alternate areas instead, at stgIn[c] + altOff + (e & 1)*altBytes
+// for the round whose barrier has epoch e (see k_ipc_collective).
 struct IpcArgs {
     const void* in[kIpcMaxRanks];
     void* out[kIpcMaxRanks];
@@ -65,8 +75,12 @@ struct IpcArgs {
     uint64_t blockElems;
     uint32_t rounds;
     uint32_t epochBase;
+    uint64_t altOff;    // byte offset of the alternate slot areas from stgIn[c] (same layout on every rank)
+    uint64_t altBytes;  // bytes of one alternate area
     uint64_t timeoutTicks;  // per barrier wait, in s_memrealtime ticks (100 MHz)
-    uint32_t* status;  // [0] bit 0: a barrier timed out (sticky per communicator); [1]: longest wait, in polls
+    uint32_t* status;  // [0] bit 0: a barrier timed out (sticky per communicator); [2..3]: (callSeq << 32) | longest
+                       // wait of that call, in polls (64-bit max)
+    uint32_t callSeq;  // this call's sequence number on the communicator
     bool aligned;      // every in[] / out[] is 16-B aligned (chunks whose start is not are still element-wise)
 };
 
@@ -80,14 +94,16 @@ HcclResult ScrubL2(hipStream_t stream);
 struct IpcState {
     bool ready = false;
     bool unavailable = false;      // set-up failed on some rank: every later call reports NOT_SUPPORT
-    void* stg = nullptr;           // own staging: [in area: stgInBytes][result area: stgResBytes], uncached
+    void* stg = nullptr;           // own staging, uncached: [in area][result area][alternate area 0][area 1]
     uint32_t* flags = nullptr;     // own flags, uncached, zeroed
-    uint32_t* status = nullptr;    // device words: [0] bit 0 = barrier timeout, [1] = longest barrier wait (polls)
+    uint32_t* status = nullptr;    // device words: [0] bit 0 = barrier timeout, [2..3] = tagged longest wait (IpcArgs)
+    uint32_t callSeq = 0;          // IPC calls issued on the communicator (tags the wait diagnostic)
     void* peerStg[kIpcMaxRanks] = {};
     uint32_t* peerFlags[kIpcMaxRanks] = {};
     bool opened[kIpcMaxRanks] = {};
     uint64_t stgInBytes = 0;
     uint64_t stgResBytes = 0;
+    uint64_t stgAltBytes = 0;      // each of the two alternate slot areas of the single-barrier kinds
     uint32_t epoch = 0;
     uint32_t blocks = 0;
 };
@@ -95,7 +111,8 @@ struct IpcState {
 constexpr uint32_t kIpcBlocks = 128;     // workgroups per rank and launch in a loopback world (cap)
 constexpr uint32_t kIpcMaxBlocks = 256;  // flags are sized for this many (HcclAmdCommSetIpcBlocks)
 uint32_t DefaultIpcBlocks(uint64_t bytes);  // workgroups per launch when the communicator sets none (ipc.cc)
-constexpr size_t kIpcStatusBytes = 16;  // status words, reset as one 16-B block per call
-constexpr uint64_t kIpcStagingBytes = 128ull << 20;  // slot area per rank; the result area is as large
+constexpr size_t kIpcStatusBytes = 16;  // status words (IpcArgs::status)
+constexpr uint64_t kIpcStagingBytes = 128ull << 20;  // slot area per rank; the result area is as large, and so is
+                                                     // each alternate slot area
 
 }  // namespace hccl_amd

@@ -17,7 +17,9 @@
 //     phase 2  every rank copies the other chunks from its own result area
 // Two barriers per round suffice: a peer's next-round phase-0 stores into my staging come after it passed barrier 2
 // (so after my phase-1 reads), and its next phase-1 stores into my result area come after barrier 1 of the next
-// round (so after my phase-2 reads); the same holds across calls (kernels of a stream run in order).
+// round (so after my phase-2 reads); the same holds across calls (kernels of a stream run in order). The kinds with
+// no result push and no phase 2 (ReduceScatter, one-shot) keep only the first barrier and alternate their slots
+// between two areas of their own instead (k_ipc_collective; model-checked by tests/test_ipc_protocol.py).
 // Every round of one launch has the same geometry (the host launches a shorter last round separately), so block b
 // of every rank touches the same slot and result addresses in every round and only waits for block b of its peers;
 // nothing in a GPU waits for another block of the same GPU. Every storing wave drains (s_waitcnt vmcnt(0)) before the
@@ -41,40 +43,59 @@ namespace {
 constexpr int kIpcBlock = 256;
 constexpr int kIpcU = 4;
 
-// Returns false when a barrier of this launch timed out (status bit 0): the caller then stops at once, so a rank
-// never stores into a peer it has lost track of.
-__device__ __forceinline__ bool Barrier(const IpcArgs& a, uint32_t me, uint32_t epoch)
+// Returns false when this block's wait was cut short: its own timeout, or a timeout another block of this rank already
+// set (status bit 0). The caller then stops at once, so a rank never stores into a peer it has lost track of. The
+// longest wait (in polls) stays in the lane's `waitMax` and is published once per launch (PublishWait), off the
+// barrier's critical path.
+__device__ __forceinline__ bool Barrier(const IpcArgs& a, uint32_t me, uint32_t epoch, uint32_t& waitMax)
 {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its stores have left the CU
     __syncthreads();
+    __shared__ uint32_t failed;
     const uint32_t t = threadIdx.x;
     if (t < a.n) {
+        if (t == 0) failed = 0;  // every thread read the previous barrier's value before the __syncthreads above
         __threadfence_system();
         uint32_t* remote = a.flags[t] + blockIdx.x * a.n + me;
         __hip_atomic_store(remote, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         uint32_t* mine = a.flags[me] + blockIdx.x * a.n + t;
         uint32_t polls = 0;
+        bool cut = false;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz constant clock
         while (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
             ++polls;
             if ((polls & 63u) == 0) {
                 // a timeout anywhere (this or another block of this rank) ends the wait at once
-                if ((__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 1u) != 0) break;
+                if ((__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 1u) != 0) {
+                    cut = true;
+                    break;
+                }
                 if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeoutTicks) {
                     __hip_atomic_fetch_or(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    cut = true;
                     break;
                 }
             }
             __builtin_amdgcn_s_sleep(2);
         }
-        if (polls != 0) __hip_atomic_fetch_max(a.status + 1, polls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        waitMax = max(waitMax, polls);
+        if (cut) failed = 1;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate has completed before the barrier opens
     }
-    __shared__ uint32_t failed;
-    if (t == 0) failed = __hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 1u;
     __syncthreads();
     return failed == 0;
+}
+
+// Longest barrier wait of this call: one 64-bit max per lane and launch into status words 2..3, tagged with the
+// call's sequence number in the high half, so a new call needs no reset (HcclAmdCommIpcStatus keeps only its own tag).
+__device__ __forceinline__ void PublishWait(const IpcArgs& a, uint32_t waitMax)
+{
+    if (threadIdx.x < a.n && waitMax != 0) {
+        __hip_atomic_fetch_max(reinterpret_cast<unsigned long long*>(a.status + 2),
+                               (static_cast<unsigned long long>(a.callSeq) << 32) | waitMax, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 struct Range {
@@ -244,7 +265,25 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
     const bool reduceKind = a.kind == kIpcReduce || a.kind == kIpcReduceOneShot;
     // a communicator whose IPC barrier ever timed out stays failed (sticky bit): never wait on its peers again
     if ((__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 1u) != 0) return;
+    // Slots: the two-barrier kinds use stgIn. The single-barrier kinds alternate between two areas by the parity of
+    // the round's barrier epoch e, and fold after the barrier with no second one, so rank i may store round k+2
+    // (parity of k) while a peer still folds round k. That is safe because block b of rank i passed barrier k+1
+    // first, and:
+    //   * rounds k, k+1, k+2 in one launch: every peer's block b signalled k+1 after its fold of round k, and block b
+    //     of every rank touches only its own window of the area in every round of a launch;
+    //   * k+1 in the launch of k, k+2 in a later one: rank i's launch of k ended only after all its blocks passed
+    //     k+1 (the block count is the same on every rank), so every block of every peer had folded round k;
+    //   * k+1 in a later launch than k: the peer's block b signalled k+1 from that later launch, which its stream
+    //     started only after the launch with round k had ended.
+    // No two-barrier kind touches these areas, so a peer still in phase 2 of an earlier call is never disturbed, and a
+    // later two-shot call never stores over a fold that runs after the last barrier.
+    const bool single = SingleBarrierKind(a.kind);
+    auto slotArea = [&](uint32_t c, uint32_t e) -> char* {
+        char* base = static_cast<char*>(a.stgIn[c]);
+        return single ? base + a.altOff + (e & 1u) * a.altBytes : base;
+    };
     uint32_t epoch = a.epochBase;
+    uint32_t waitMax = 0;
     for (uint32_t k = 0; k < a.rounds; ++k) {
         const uint64_t kP = uint64_t(k) * a.piece;
         // phase 0: my piece of chunk c -> owner c's slot `me` (one-shot: my whole piece to every peer; to the root
@@ -252,15 +291,15 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
         for (uint32_t c = 0; c < n; ++c) {
             if (c == me || (a.kind == kIpcReduceOneShot && c != a.root)) continue;
             const Range r = BlockWindow(a, PieceLen(a, c, kP));
-            S* slot = static_cast<S*>(a.stgIn[c]) + uint64_t(me) * a.piece;
+            S* slot = reinterpret_cast<S*>(slotArea(c, epoch + 1)) + uint64_t(me) * a.piece;
             CopyRange<S>(slot, in + ChunkStart(a, c) + kP, r, ChunkVec<S>(a, c));
         }
-        if (!Barrier(a, me, ++epoch)) return;
+        if (!Barrier(a, me, ++epoch, waitMax)) break;
         // phase 1: fold my chunk's piece over the slots (my own operand straight from my input)
         if (!(a.kind == kIpcReduceOneShot && me != a.root)) {
             const Range r = BlockWindow(a, PieceLen(a, me, kP));
             const S* own = in + ChunkStart(a, me) + kP;
-            const S* slots = static_cast<const S*>(a.stgIn[me]);
+            const S* slots = reinterpret_cast<const S*>(slotArea(me, epoch));
             // destination 0: my output (or, for a non-root two-shot Reduce rank, the root's result area); the
             // two-shot AllReduce also pushes to every peer's result area (destinations 1 .. n-1 = the peers in
             // ascending order)
@@ -275,7 +314,7 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
             };
             FoldRange<E, OP>(a, me, kP, own, slots, dst, a.kind == kIpcAllReduce ? n : 1u, r, ChunkVec<S>(a, me));
         }
-        if (!Barrier(a, me, ++epoch)) return;
+        if (!single && !Barrier(a, me, ++epoch, waitMax)) break;
         // phase 2: the other chunks' results from my own result area (two-shot AllReduce: every rank; two-shot
         // Reduce: the root)
         if (!oneShot && (a.kind == kIpcAllReduce || (reduceKind && me == a.root))) {
@@ -287,6 +326,7 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
             }
         }
     }
+    PublishWait(a, waitMax);
 }
 
 template <class E>

@@ -225,6 +225,10 @@ def test_ipc_lost_peer_times_out_and_sticks():
         assert got[r][1]["first_ok"] and got[r][1]["first_status"] & 1 == 0
     r0 = got[0][1]
     assert r0["lost_status"] & 1 == 1
+    # bits 8+: bit length of the call's longest wait in polls (~100 ns each): a 1.5 s wait is millions of polls
+    assert (r0["lost_status"] >> 8) >= 16, hex(r0["lost_status"])
     assert 1.0 < r0["lost_s"] < 15.0, r0
     assert r0["after_status"] & 1 == 1
+    # the next call returns before any barrier, so it has no wait of its own (the diagnostic is per call)
+    assert (r0["after_status"] >> 8) == 0, hex(r0["after_status"])
     assert r0["after_s"] < 1.0, r0
