@@ -199,6 +199,14 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
             break;
         default: return HCCL_E_NOT_SUPPORT;
     }
+    // The barrier epochs and the block count live on the host and advance per call, so a captured launch replayed
+    // from a graph would meet flags that already passed its epochs and run without waiting. A capturing stream
+    // takes the RCCL schedule of the same family instead (NOT_SUPPORT here; same bits). Every rank of a
+    // collective is captured alike, so they all decide the same way, before the collective set-up.
+    hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &capture) != hipSuccess || capture != hipStreamCaptureStatusNone) {
+        return HCCL_E_NOT_SUPPORT;
+    }
     HCCL_CHK(IpcSetup(c));
     IpcState& s = c.ipc;
     const uint32_t n = c.nRanks;

@@ -101,7 +101,9 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
             c.lastAlgo = p.algo;
             return r;
         }
-        p.algo = family;  // the RCCL schedule with the same order
+        // no peer mappings, or a capturing stream: the RCCL schedule with the same order, if there is RCCL
+        if (!c.transport->HasSendRecv()) return HCCL_E_NOT_SUPPORT;
+        p.algo = family;
     } else if (p.algo == HCCL_AMD_ALGO_IPC_TWOSHOT || p.algo == HCCL_AMD_ALGO_IPC) {
         p.algo = HCCL_AMD_ALGO_MESH_ONESHOT;  // AllGather has no IPC form
     }

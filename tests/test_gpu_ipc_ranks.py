@@ -110,6 +110,22 @@ def _rank_main(rank, n, port, q):
             results.append((i, status, comm.last_algo, ok))
             if max(all_gather(status & 1)) != 0:  # every rank stops together after a barrier timeout anywhere
                 break
+        # a capturing stream never takes the IPC kernel (host-side epochs would not advance on replay); with no
+        # RCCL behind this communicator the call reports NOT_SUPPORT and captures nothing
+        x = torch.ones(4096, device="cuda")
+        y = torch.zeros_like(x)
+        graph = torch.cuda.CUDAGraph()
+        capture_code = None
+        torch.cuda.synchronize()
+        try:
+            with torch.cuda.graph(graph):
+                try:
+                    comm.all_reduce(x, y, O.SUM, stream=torch.cuda.current_stream())
+                except H.HcclError as e:
+                    capture_code = e.code
+        except Exception as e:  # noqa: BLE001
+            capture_code = f"capture failed: {e}"
+        results.append(("capture", capture_code))
         dist.barrier()
         comm.destroy()  # collective: no rank unmaps while a peer's kernel may still store into it
         progress.write("destroyed\n")
@@ -142,6 +158,9 @@ def test_ipc_collectives_rank_mode(n):
                 p.kill()
     for r in range(n):
         assert got[r][0] == "ok", f"rank {r}:\n{got[r][0]}"
+    for r in range(n):
+        assert got[r][1][-1] == ("capture", 5), got[r][1][-1]  # HCCL_E_NOT_SUPPORT
+        got[r] = (got[r][0], got[r][1][:-1])
     for r in range(n):
         assert len(got[r][1]) == len(CASES), f"rank {r} stopped after case {len(got[r][1]) - 1}"
         for i, status, algo, _ok in got[r][1]:
