@@ -351,6 +351,24 @@ def bench_c4(comm, send, recv, world) -> dict:
         out["rs_ipc_auto_family_busbw_GBps"] = round(nbytes / t_ipc9 / 1e9 * f, 2)
         out["rs_ipc_auto_family_ran"] = H.Algo(comm.last_algo).name
         out["rs_ipc_auto_family_matches_auto"] = bool(torch.equal(ref_auto, shard.view(torch.int16)[:: 1 << 10]))
+    except H.HcclError as e:
+        out["rs_rows_error"] = str(e)
+    finally:
+        comm.set_algo(H.Algo.AUTO)
+    # the AllGather half on the IPC kernel (one launch per call, data movement only) beside the RCCL mesh above
+    try:
+        comm.set_algo(H.Algo.AUTO)
+        comm.all_gather(shard, full, s)
+        ref_ag = full.view(torch.int16)[:: 1 << 10].clone()
+        comm.set_algo(H.Algo.IPC)
+        t_ag_ipc = _timed(lambda: comm.all_gather(shard, full, s), 5)
+        out["ag_ipc_ms"] = round(t_ag_ipc * 1e3, 3)
+        out["ag_ipc_busbw_GBps"] = round(nbytes / t_ag_ipc / 1e9 * f, 2)
+        out["ag_ipc_ran"] = H.Algo(comm.last_algo).name
+        out["ag_ipc_matches_auto"] = bool(torch.equal(ref_ag, full.view(torch.int16)[:: 1 << 10]))
+        out["ag_ipc_barrier_timeouts"] = comm.ipc_status() & 1
+    except H.HcclError as e:
+        out["ag_ipc_error"] = str(e)
     finally:
         comm.set_algo(H.Algo.AUTO)
     return out

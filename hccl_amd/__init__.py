@@ -40,6 +40,12 @@ TORCH_TO_HCCL = {
     torch.bfloat16: HcclDataType.BFP16,
     torch.float32: HcclDataType.FP32,
     torch.float64: HcclDataType.FP64,
+    # movable but not reducible (the reduce entries answer HCCL_E_NOT_SUPPORT, as CheckDataType does)
+    torch.uint8: HcclDataType.UINT8,
+    torch.uint16: HcclDataType.UINT16,
+    torch.uint32: HcclDataType.UINT32,
+    torch.float8_e4m3fn: HcclDataType.FP8E4M3,
+    torch.float8_e5m2: HcclDataType.FP8E5M2,
 }
 
 

@@ -178,8 +178,20 @@ uint32_t DefaultIpcBlocks(uint64_t bytes)
 HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void* sendBuf, void* recvBuf,
                             uint64_t count, HcclDataType dt, HcclReduceOp op, uint32_t root, hipStream_t stream)
 {
-    const uint64_t es = DataTypeSize(dt);
+    uint64_t es = DataTypeSize(dt);
     if (es == 0 || c.nRanks > kIpcMaxRanks) return HCCL_E_NOT_SUPPORT;
+    if (opType == HCCL_AMD_OP_ALLGATHER) {
+        // pure data movement: any dtype runs as the integer type of its size (16-B types as pairs of 8-B words)
+        op = HCCL_REDUCE_SUM;
+        switch (es) {
+            case 1: dt = HCCL_DATA_TYPE_INT8; break;
+            case 2: dt = HCCL_DATA_TYPE_INT16; break;
+            case 4: dt = HCCL_DATA_TYPE_INT32; break;
+            case 8: dt = HCCL_DATA_TYPE_INT64; break;
+            case 16: dt = HCCL_DATA_TYPE_INT64; count *= 2; es = 8; break;
+            default: return HCCL_E_NOT_SUPPORT;
+        }
+    }
     IpcKind kind;
     IpcOrder order;
     switch (opType) {
@@ -195,6 +207,10 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
             break;
         case HCCL_AMD_OP_REDUCE:
             kind = family == HCCL_AMD_ALGO_MESH_ONESHOT ? kIpcReduceOneShot : kIpcReduce;
+            order = kIpcO1;
+            break;
+        case HCCL_AMD_OP_ALLGATHER:
+            kind = kIpcAllGather;  // data movement only: no order
             order = kIpcO1;
             break;
         default: return HCCL_E_NOT_SUPPORT;
@@ -213,7 +229,8 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
     // workgroups per rank (equal on every rank: block b pairs with block b of each peer, and the default is a function
     // of the call's arguments alone). A loopback world runs every rank's blocks in one launch on one GPU, so it keeps
     // at most kIpcBlocks per rank to stay co-resident.
-    const uint64_t callBytes = (opType == HCCL_AMD_OP_REDUCE_SCATTER ? uint64_t(c.nRanks) : 1u) * count * es;
+    const bool nBlocks = opType == HCCL_AMD_OP_REDUCE_SCATTER || opType == HCCL_AMD_OP_ALLGATHER;
+    const uint64_t callBytes = (nBlocks ? uint64_t(c.nRanks) : 1u) * count * es;  // RS input / AG output
     s.blocks = c.ipcBlocks != 0 ? c.ipcBlocks : DefaultIpcBlocks(callBytes);
     if (c.transport->SharedDevice()) s.blocks = std::min(s.blocks, kIpcBlocks);
     const uint64_t V = 16 / es;
@@ -232,6 +249,7 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
     a.timeoutTicks = IpcTimeoutTicks();  // a lost peer ends the kernel with status bit 0, never a hang
     a.status = s.status;
     a.callSeq = ++s.callSeq;  // equal on every rank of a loopback world (each runs this once per call)
+    a.outStride = count;
     a.altOff = s.stgInBytes + s.stgResBytes;
     a.altBytes = s.stgAltBytes;
     const bool single = SingleBarrierKind(kind);
@@ -272,8 +290,8 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
             g.chunkLen = cnt / n;
             g.rem = cnt % n;
             g.chunkStride = 0;
-        } else if (kind == kIpcAllReduceOneShot || kind == kIpcReduceOneShot) {
-            // every rank holds (and, for the AllReduce, folds) the whole range
+        } else if (kind == kIpcAllReduceOneShot || kind == kIpcReduceOneShot || kind == kIpcAllGather) {
+            // every rank holds (and, for the AllReduce, folds) the whole range; AllGather: its whole input
             g.balanced = false;
             g.total = cnt;
             g.chunkStride = 0;

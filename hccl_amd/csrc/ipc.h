@@ -17,6 +17,7 @@ enum IpcKind : uint32_t {
     kIpcReduce = 2,            // two-shot Reduce: owner c folds chunk c, only the root gets the result
     kIpcAllReduceOneShot = 3,  // every rank receives every peer's whole piece and folds all of it (no phase 2)
     kIpcReduceOneShot = 4,     // the peers push their whole piece to the root, which folds it
+    kIpcAllGather = 5,         // every rank pushes its whole piece to every peer; each copies the n pieces out
 };
 
 // Operand order of a fold of chunk t.
@@ -38,7 +39,8 @@ enum IpcSubMode : uint32_t {
 // stores never meet this round's fold (k_ipc_collective). The others keep two (results must be complete before phase 2).
 __host__ __device__ constexpr bool SingleBarrierKind(uint32_t kind)
 {
-    return kind == kIpcReduceScatter || kind == kIpcAllReduceOneShot || kind == kIpcReduceOneShot;
+    return kind == kIpcReduceScatter || kind == kIpcAllReduceOneShot || kind == kIpcReduceOneShot ||
+           kind == kIpcAllGather;
 }
 
 // Kernel arguments. In rank mode (me >= 0) only in[me] / out[me] are used; stgIn / stgRes / flags hold every rank's
@@ -75,6 +77,7 @@ struct IpcArgs {
     uint64_t blockElems;
     uint32_t rounds;
     uint32_t epochBase;
+    uint64_t outStride;  // kIpcAllGather: elements between consecutive ranks' blocks of the output (sendCount)
     uint64_t altOff;    // byte offset of the alternate slot areas from stgIn[c] (same layout on every rank)
     uint64_t altBytes;  // bytes of one alternate area
     uint64_t timeoutTicks;  // per barrier wait, in s_memrealtime ticks (100 MHz)

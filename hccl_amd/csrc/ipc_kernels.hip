@@ -295,8 +295,18 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
             CopyRange<S>(slot, in + ChunkStart(a, c) + kP, r, ChunkVec<S>(a, c));
         }
         if (!Barrier(a, me, ++epoch, waitMax)) break;
-        // phase 1: fold my chunk's piece over the slots (my own operand straight from my input)
-        if (!(a.kind == kIpcReduceOneShot && me != a.root)) {
+        if (a.kind == kIpcAllGather) {
+            // phase 1 of an AllGather: rank q's piece, from my slot q (mine from my input), to output block q
+            const Range r = BlockWindow(a, PieceLen(a, me, kP));
+            const S* slots = reinterpret_cast<const S*>(slotArea(me, epoch));
+            constexpr uint64_t V = 16 / sizeof(S);
+            for (uint32_t q = 0; q < n; ++q) {
+                const S* src = q == me ? in + kP : slots + uint64_t(q) * a.piece;
+                S* dst = out + uint64_t(q) * a.outStride + kP;
+                if (src != dst) CopyRange<S>(dst, src, r, a.aligned && (uint64_t(q) * a.outStride) % V == 0);
+            }
+        } else if (!(a.kind == kIpcReduceOneShot && me != a.root)) {
+            // phase 1: fold my chunk's piece over the slots (my own operand straight from my input)
             const Range r = BlockWindow(a, PieceLen(a, me, kP));
             const S* own = in + ChunkStart(a, me) + kP;
             const S* slots = reinterpret_cast<const S*>(slotArea(me, epoch));

@@ -82,15 +82,14 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     p.algo = c.algoOverride;
     // an IPC-only communicator (bootstrap transport without send/recv) runs every reducing op on the IPC kernel in
     // the auto family, whatever schedule family was asked for
-    if (!c.transport->HasSendRecv() && opType != HCCL_AMD_OP_ALLGATHER && p.algo != HCCL_AMD_ALGO_IPC_TWOSHOT) {
-        p.algo = HCCL_AMD_ALGO_IPC;
-    }
+    if (!c.transport->HasSendRecv() && p.algo != HCCL_AMD_ALGO_IPC_TWOSHOT) p.algo = HCCL_AMD_ALGO_IPC;
     if (p.algo == HCCL_AMD_ALGO_AUTO && NeedStrictOrder(opType, dt, op, c.nRanks)) {
         p.algo = HCCL_AMD_ALGO_ORDER_PRESERVED;
     }
-    if ((p.algo == HCCL_AMD_ALGO_IPC_TWOSHOT || p.algo == HCCL_AMD_ALGO_IPC) && opType != HCCL_AMD_OP_ALLGATHER) {
+    if (p.algo == HCCL_AMD_ALGO_IPC_TWOSHOT || p.algo == HCCL_AMD_ALGO_IPC) {
         // the order family of the one-sided kernel: IPC_TWOSHOT fixes AllReduce two-shot (O2), mesh ReduceScatter
         // and two-shot Reduce; IPC takes whatever the auto selector takes, so its bits are the auto path's
+        // (AllGather moves data only: the family does not matter)
         const uint64_t bytes = count * es;
         const int32_t family =
             p.algo == HCCL_AMD_ALGO_IPC
@@ -103,9 +102,7 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
         }
         // no peer mappings, or a capturing stream: the RCCL schedule with the same order, if there is RCCL
         if (!c.transport->HasSendRecv()) return HCCL_E_NOT_SUPPORT;
-        p.algo = family;
-    } else if (p.algo == HCCL_AMD_ALGO_IPC_TWOSHOT || p.algo == HCCL_AMD_ALGO_IPC) {
-        p.algo = HCCL_AMD_ALGO_MESH_ONESHOT;  // AllGather has no IPC form
+        p.algo = opType == HCCL_AMD_OP_ALLGATHER ? HCCL_AMD_ALGO_MESH_ONESHOT : family;
     }
     p.nRanks = c.nRanks;
     p.rank = c.rank;

@@ -260,6 +260,45 @@ def test_ipc_staging_survives_recycled_cached_pages():
                 c.destroy()
 
 
+@pytest.mark.parametrize("dtype", [torch.uint8, torch.float16, torch.float32, torch.float64, torch.int64],
+                         ids=str)
+@pytest.mark.parametrize("n,count", [(2, 1), (3, 5), (4, 4099), (8, 100003), (2, (36 << 20) + 11)])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_ipc_allgather(worlds, dtype, n, count, inplace):
+    """AllGather on the IPC kernel (pure data movement: any dtype, including the non-reducible uint8): rank r's
+    input lands in block r of every output (all_gather_op.cc semantics), across several staging rounds, in place
+    (sendBuf = recvBuf + r * count) or not."""
+    if count > (1 << 20) and dtype != torch.float32:
+        pytest.skip("multi-round case runs once, in fp32")
+    comms = worlds(n)
+    g = torch.Generator(device="cuda").manual_seed(900 + n)
+    full = torch.randint(0, 256, (n * count * dtype.itemsize,), device="cuda", dtype=torch.uint8,
+                         generator=g).view(dtype)
+    recvs = [torch.zeros(n * count, dtype=dtype, device="cuda") for _ in range(n)]
+    sends = []
+    for r in range(n):
+        if inplace:
+            recvs[r][r * count:(r + 1) * count] = full[r * count:(r + 1) * count]
+            sends.append(recvs[r][r * count:(r + 1) * count])
+        else:
+            sends.append(full[r * count:(r + 1) * count].clone())
+    streams = [torch.cuda.Stream() for _ in range(n)]
+    for c in comms:
+        c.set_algo(H.Algo.IPC)
+    torch.cuda.synchronize()
+    try:
+        run_ranks(n, lambda r: comms[r].all_gather(sends[r], recvs[r], streams[r]))
+        torch.cuda.synchronize()
+        assert comms[0].last_algo == H.Algo.IPC
+        assert ipc_status(comms[0]) & 1 == 0
+        want = full.view(torch.uint8)
+        for r in range(n):
+            assert torch.equal(recvs[r].view(torch.uint8), want), r
+    finally:
+        for c in comms:
+            c.set_algo(0)
+
+
 @pytest.mark.parametrize("shift", [(1, 1), (0, 3), (2, 0)])
 def test_ipc_unaligned_buffers(worlds, shift):
     """Buffers not 16-B aligned still run the IPC kernel (element-wise accesses to the user buffers; the path choice

@@ -17,7 +17,7 @@ from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
-AR, RS, RED = 0, 1, 2
+AR, RS, RED, AG = 0, 1, 2, 3
 # (collective, dtype, op, count): ragged counts, every reduce dtype family, counts that need several pieces per chunk
 CASES = [
     (AR, O.FP32, O.SUM, 1), (AR, O.FP32, O.SUM, 4099), (AR, O.FP32, O.MAX, 100003), (AR, O.FP32, O.SUM, (36 << 20) + 11),
@@ -34,6 +34,9 @@ CASES = [
     # HcclAmdCommSetIpcBlocks: 256 and 64 workgroups per launch instead of 128 (different windows per block)
     (AR, O.FP32, O.SUM, (20 << 20) // 4 + 3, 9, 256), (AR, O.FP32, O.SUM, 40961, 7, 64),
     (RS, O.FP32, O.SUM, 70001, 7, 256),
+    # AllGather (data movement, one barrier per round): ragged, several rounds, and between reducing calls
+    (AG, O.FP16, O.SUM, 33333, 9), (AG, O.FP32, O.SUM, (20 << 20) + 3, 9), (AG, O.INT8, O.SUM, 5, 9),
+    (AR, O.FP32, O.SUM, 4099, 9),
 ]
 UNALIGNED_CASE = CASES.index((AR, O.FP32, O.SUM, 250001))
 ROOT = 1
@@ -82,7 +85,7 @@ def _rank_main(rank, n, port, q):
             comm.set_ipc_blocks(case[5] if len(case) > 5 else 0)
             progress.write(f"case {i} {CASES[i]} start\n")
             send = to_device(dtype, _inputs(dtype, _in_count(kind, count, n), n, i)[rank])
-            recv = torch.zeros(count, dtype=send.dtype, device=send.device)
+            recv = torch.zeros(count * n if kind == AG else count, dtype=send.dtype, device=send.device)
             if i == UNALIGNED_CASE and rank == n - 1:  # one rank with unaligned buffers: still the IPC path
                 send = torch.cat([send[:1], send])[1:]
                 recv = torch.empty(count + 1, dtype=send.dtype, device=send.device)[1:]
@@ -91,13 +94,18 @@ def _rank_main(rank, n, port, q):
                 comm.all_reduce(send, recv, op, stream=stream)
             elif kind == RS:
                 comm.reduce_scatter(send, recv, op, stream=stream)
+            elif kind == AG:
+                comm.all_gather(send, recv, stream=stream)
             else:
                 comm.reduce(send, recv, ROOT % n, op, stream=stream)
             stream.synchronize()
             status = comm.ipc_status()
             got = to_host(dtype, recv)
             ok = True
-            if not (kind == RED and rank != ROOT % n):
+            if kind == AG:
+                want = np.concatenate(_inputs(dtype, count, n, i))
+                ok = O.equal_bits(dtype, got, want)
+            elif not (kind == RED and rank != ROOT % n):
                 xs = _inputs(dtype, _in_count(kind, count, n), n, i)
                 fam = R.ALGO_IPC
                 if forced == 9:

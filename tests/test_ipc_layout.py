@@ -151,6 +151,62 @@ def test_ipc_o6_sub_slices_in_bounds_and_exact_cover(kind, n, es, count):
     check_general(kind, n, count, es, vec=False, o6=True)
 
 
+def check_allgather(n, count, es, vec, blocks):
+    """kIpcAllGather: the one-shot geometry (every rank pushes its whole piece to every peer's slot `me`), then each
+    rank copies slot q (its own piece from its input) to output block q at q * count. Every output element is written
+    exactly once per rank, inside [0, n * count), and every slot access stays inside the owner's n slots."""
+    v = 16 // es
+    slot_cap = (STG_BYTES // es // n) // v * v
+    piece = max(v, min(slot_cap, -(-count // v) * v))
+    block = -(-(-(-piece // blocks)) // v) * v
+    rounds = -(-count // piece)
+    for me in range(n):
+        out_cover = np.zeros(n * count, np.int32)
+        pushed = np.zeros(count, np.int32)
+        for k in range(rounds):
+            kp = k * piece
+            plen = 0 if kp >= count else min(piece, count - kp)
+            for b in range(blocks):
+                lo = min(plen, b * block)
+                hi = min(plen, lo + block)
+                for a0, a1 in touched(lo, hi, v, vec):
+                    if a1 > a0:
+                        assert me * piece + a1 <= n * piece
+                        pushed[kp + a0:kp + a1] += 1  # once per peer: counted for one of them
+                for q in range(n):
+                    for a0, a1 in touched(lo, hi, v, vec and (q * count) % v == 0):
+                        if a1 <= a0:
+                            continue
+                        assert q * piece + a1 <= n * piece
+                        g0, g1 = q * count + kp + a0, q * count + kp + a1
+                        assert 0 <= g0 and g1 <= n * count
+                        out_cover[g0:g1] += 1
+        assert np.all(pushed == 1), me
+        assert np.all(out_cover == 1), me
+
+
+def default_blocks(nbytes):
+    """ipc.cc DefaultIpcBlocks: workgroups per launch by the call's bytes."""
+    for limit, b in ((512 << 10, 16), (2 << 20, 32), (32 << 20, 64), (64 << 20, 128)):
+        if nbytes <= limit:
+            return b
+    return 256
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("es", [1, 2, 4, 8])
+@pytest.mark.parametrize("count", [1, 5, 33, 4099, 100003])
+def test_ipc_allgather_in_bounds_and_exact_cover(n, es, count):
+    for blocks in sorted({default_blocks(n * count * es), 1, 256}):
+        check_allgather(n, count, es, vec=True, blocks=blocks)
+        check_allgather(n, count, es, vec=False, blocks=blocks)
+
+
+def test_ipc_allgather_multi_round():
+    n, count = 2, (36 << 20) + 11  # fp32: 3 rounds of 16 Mi elements
+    check_allgather(n, count, 4, vec=True, blocks=default_blocks(n * count * 4))
+
+
 def check(kind, n, count, es, vec, root=0):
     v = 16 // es
     chunks, piece, block, rounds = geometry(kind, n, count, es)
