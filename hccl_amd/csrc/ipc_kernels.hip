@@ -287,9 +287,11 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
     for (uint32_t k = 0; k < a.rounds; ++k) {
         const uint64_t kP = uint64_t(k) * a.piece;
         // phase 0: my piece of chunk c -> owner c's slot `me` (one-shot: my whole piece to every peer; to the root
-        // only for a one-shot Reduce)
-        for (uint32_t c = 0; c < n; ++c) {
-            if (c == me || (a.kind == kIpcReduceOneShot && c != a.root)) continue;
+        // only for a one-shot Reduce). Each block starts at a different peer (offset rotated by blockIdx.x), so at any
+        // moment the blocks of a rank spread their stores over all n-1 xGMI links instead of all feeding one peer.
+        for (uint32_t i = 0; i + 1 < n; ++i) {
+            const uint32_t c = (me + 1 + (i + blockIdx.x) % (n - 1)) % n;
+            if (a.kind == kIpcReduceOneShot && c != a.root) continue;
             const Range r = BlockWindow(a, PieceLen(a, c, kP));
             S* slot = reinterpret_cast<S*>(slotArea(c, epoch + 1)) + uint64_t(me) * a.piece;
             CopyRange<S>(slot, in + ChunkStart(a, c) + kP, r, ChunkVec<S>(a, c));
