@@ -105,7 +105,6 @@ HcclResult IpcSetup(Comm& c)
             return HCCL_E_NOT_SUPPORT;
         }
     }
-    s.epoch = 0;
     s.ready = true;
     return HCCL_SUCCESS;
 }
@@ -215,12 +214,15 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
             break;
         default: return HCCL_E_NOT_SUPPORT;
     }
-    // The barrier epochs and the block count live on the host and advance per call, so a captured launch replayed
-    // from a graph would meet flags that already passed its epochs and run without waiting. A capturing stream
-    // takes the RCCL schedule of the same family instead (NOT_SUPPORT here; same bits). Every rank of a
-    // collective is captured alike, so they all decide the same way, before the collective set-up.
+    // Stream capture: the barrier epochs live on the device (status word kIpcEpochWord, advanced by the last block
+    // of every launch), so a captured launch replays correctly: each replay takes the next epochs, as a new call
+    // would. Two things cannot be captured: the collective set-up of the first call (allocation, host exchange,
+    // device synchronisation) and the loopback world, which exchanges events between host threads per call. Those
+    // report NOT_SUPPORT under capture; a communicator with RCCL then takes the RCCL schedule of the same family.
+    // Every rank of a collective is captured alike, so they all decide the same way.
     hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(stream, &capture) != hipSuccess || capture != hipStreamCaptureStatusNone) {
+    if (hipStreamIsCapturing(stream, &capture) != hipSuccess) return HCCL_E_NOT_SUPPORT;
+    if (capture != hipStreamCaptureStatusNone && (!c.ipc.ready || c.transport->SharedDevice())) {
         return HCCL_E_NOT_SUPPORT;
     }
     HCCL_CHK(IpcSetup(c));
@@ -315,8 +317,7 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
         g.piece = std::max<uint64_t>(V, std::min(slotCap, (widest + V - 1) / V * V));
         g.blockElems = ((g.piece + s.blocks - 1) / s.blocks + V - 1) / V * V;
         g.rounds = static_cast<uint32_t>((widest + g.piece - 1) / g.piece);
-        g.epochBase = s.epoch;
-        s.epoch += (single ? 1 : 2) * g.rounds;
+        g.epochSpan = (single ? 1 : 2) * g.rounds;
     };
     auto at = [es](const void* p, uint64_t off) { return static_cast<char*>(const_cast<void*>(p)) + off * es; };
 

@@ -76,13 +76,14 @@ struct IpcArgs {
     uint64_t piece;
     uint64_t blockElems;
     uint32_t rounds;
-    uint32_t epochBase;
+    uint32_t epochSpan;  // barriers per block in this launch: the device epoch counter advances by this much
     uint64_t outStride;  // kIpcAllGather: elements between consecutive ranks' blocks of the output (sendCount)
     uint64_t altOff;    // byte offset of the alternate slot areas from stgIn[c] (same layout on every rank)
     uint64_t altBytes;  // bytes of one alternate area
     uint64_t timeoutTicks;  // per barrier wait, in s_memrealtime ticks (100 MHz)
     uint32_t* status;  // [0] bit 0: a barrier timed out (sticky per communicator); [2..3]: (callSeq << 32) | longest
-                       // wait of that call, in polls (64-bit max)
+                       // wait of that call, in polls (64-bit max); [4]: epoch counter (barriers so far, per block);
+                       // [5]: blocks of the running launch that have finished (kIpcEpochWord, kIpcDoneWord)
     uint32_t callSeq;  // this call's sequence number on the communicator
     bool aligned;      // every in[] / out[] is 16-B aligned (chunks whose start is not are still element-wise)
 };
@@ -107,14 +108,15 @@ struct IpcState {
     uint64_t stgInBytes = 0;
     uint64_t stgResBytes = 0;
     uint64_t stgAltBytes = 0;      // each of the two alternate slot areas of the single-barrier kinds
-    uint32_t epoch = 0;
     uint32_t blocks = 0;
 };
 
 constexpr uint32_t kIpcBlocks = 128;     // workgroups per rank and launch in a loopback world (cap)
 constexpr uint32_t kIpcMaxBlocks = 256;  // flags are sized for this many (HcclAmdCommSetIpcBlocks)
 uint32_t DefaultIpcBlocks(uint64_t bytes);  // workgroups per launch when the communicator sets none (ipc.cc)
-constexpr size_t kIpcStatusBytes = 16;  // status words (IpcArgs::status)
+constexpr size_t kIpcStatusBytes = 32;  // status words (IpcArgs::status)
+constexpr int kIpcEpochWord = 4;
+constexpr int kIpcDoneWord = 5;
 constexpr uint64_t kIpcStagingBytes = 128ull << 20;  // slot area per rank; the result area is as large, and so is
                                                      // each alternate slot area
 

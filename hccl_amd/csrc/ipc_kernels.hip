@@ -98,6 +98,25 @@ __device__ __forceinline__ void PublishWait(const IpcArgs& a, uint32_t waitMax)
     }
 }
 
+// The last block of the launch to get here advances the epoch counter by the launch's barriers per block and resets
+// the finished-block count. Every block read the counter at its start, before counting itself here. A launch that
+// returns at once on a failed communicator (sticky bit) leaves the counter alone; no later launch waits on it.
+__device__ __forceinline__ void EndLaunch(const IpcArgs& a)
+{
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t total = gridDim.x * gridDim.y;
+        // relaxed: the count only needs the RMW order on its own word (this block's epoch load has returned before,
+        // since the kernel used it), and the next launch sees the new epoch through the end-of-kernel release
+        const uint32_t prev = __hip_atomic_fetch_add(a.status + kIpcDoneWord, 1u, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+        if (prev + 1 == total) {
+            __hip_atomic_store(a.status + kIpcDoneWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(a.status + kIpcEpochWord, a.epochSpan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 struct Range {
     uint64_t lo, hi;  // piece coordinates
 };
@@ -282,7 +301,10 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
         char* base = static_cast<char*>(a.stgIn[c]);
         return single ? base + a.altOff + (e & 1u) * a.altBytes : base;
     };
-    uint32_t epoch = a.epochBase;
+    // Epochs come from the device counter, read by every block before it signals anything; the last block of the
+    // launch to finish advances it (EndLaunch), so the next launch in stream order, a call or a graph replay alike,
+    // starts where this one ended. Every rank runs the same launch sequence, so the counters agree across ranks.
+    uint32_t epoch = __hip_atomic_load(a.status + kIpcEpochWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t waitMax = 0;
     for (uint32_t k = 0; k < a.rounds; ++k) {
         const uint64_t kP = uint64_t(k) * a.piece;
@@ -339,6 +361,7 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
         }
     }
     PublishWait(a, waitMax);
+    EndLaunch(a);
 }
 
 template <class E>

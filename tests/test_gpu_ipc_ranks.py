@@ -118,22 +118,46 @@ def _rank_main(rank, n, port, q):
             results.append((i, status, comm.last_algo, ok))
             if max(all_gather(status & 1)) != 0:  # every rank stops together after a barrier timeout anywhere
                 break
-        # a capturing stream never takes the IPC kernel (host-side epochs would not advance on replay); with no
-        # RCCL behind this communicator the call reports NOT_SUPPORT and captures nothing
-        x = torch.ones(4096, device="cuda")
-        y = torch.zeros_like(x)
+        # HIP graph: AllReduce (three sizes, so one-shot and two-shot), ReduceScatter and AllGather captured once,
+        # then replayed with fresh inputs. The barrier epochs live on the device, so each replay takes new ones as a
+        # new call would. Small integers in fp32: every order gives the same bits.
+        comm.set_algo(R.ALGO_IPC)
+        comm.set_ipc_blocks(0)
+        sizes = (1000, 300001, (3 << 20) + 5)
+        ar_in = [torch.zeros(c, device="cuda") for c in sizes]
+        ar_out = [torch.zeros(c, device="cuda") for c in sizes]
+        rs_len, ag_len = 70001, 50003
+        rs_in = torch.zeros(n * rs_len, device="cuda")
+        rs_out = torch.zeros(rs_len, device="cuda")
+        ag_in = torch.zeros(ag_len, device="cuda")
+        ag_out = torch.zeros(n * ag_len, device="cuda")
+        ramp = torch.arange(n * rs_len, device="cuda", dtype=torch.float32) % 97
         graph = torch.cuda.CUDAGraph()
-        capture_code = None
         torch.cuda.synchronize()
-        try:
-            with torch.cuda.graph(graph):
-                try:
-                    comm.all_reduce(x, y, O.SUM, stream=torch.cuda.current_stream())
-                except H.HcclError as e:
-                    capture_code = e.code
-        except Exception as e:  # noqa: BLE001
-            capture_code = f"capture failed: {e}"
-        results.append(("capture", capture_code))
+        with torch.cuda.graph(graph, stream=torch.cuda.Stream()):
+            cs = torch.cuda.current_stream()
+            for x, y in zip(ar_in, ar_out):
+                comm.all_reduce(x, y, O.SUM, stream=cs)
+            comm.reduce_scatter(rs_in, rs_out, O.SUM, stream=cs)
+            comm.all_gather(ag_in, ag_out, stream=cs)
+        graph_ok = []
+        for rep in range(4):
+            v = float((rank + 1) * (rep + 1))
+            for x in ar_in:
+                x.fill_(v)
+            rs_in.copy_(ramp + v)
+            ag_in.fill_(v)
+            torch.cuda.synchronize()
+            graph.replay()
+            torch.cuda.synchronize()
+            tot = float((rep + 1) * n * (n + 1) // 2)
+            ok = all(bool(torch.all(y == tot).item()) for y in ar_out)
+            ok = ok and bool(torch.all(rs_out == n * ramp[rank * rs_len:(rank + 1) * rs_len] + tot).item())
+            want = torch.cat([torch.full((ag_len,), float((q + 1) * (rep + 1)), device="cuda") for q in range(n)])
+            ok = ok and bool(torch.equal(ag_out, want))
+            graph_ok.append(ok)
+            progress.write(f"graph replay {rep} ok {ok}\n")
+        results.append(("graph", graph_ok, comm.ipc_status() & 1))
         dist.barrier()
         comm.destroy()  # collective: no rank unmaps while a peer's kernel may still store into it
         progress.write("destroyed\n")
@@ -167,7 +191,7 @@ def test_ipc_collectives_rank_mode(n):
     for r in range(n):
         assert got[r][0] == "ok", f"rank {r}:\n{got[r][0]}"
     for r in range(n):
-        assert got[r][1][-1] == ("capture", 5), got[r][1][-1]  # HCCL_E_NOT_SUPPORT
+        assert got[r][1][-1] == ("graph", [True] * 4, 0), got[r][1][-1]  # every replay right, no barrier timeout
         got[r] = (got[r][0], got[r][1][:-1])
     for r in range(n):
         assert len(got[r][1]) == len(CASES), f"rank {r} stopped after case {len(got[r][1]) - 1}"

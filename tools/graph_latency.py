@@ -1,0 +1,79 @@
+"""Per-call latency of the IPC AllReduce, eager vs captured in a HIP graph (K calls per graph, one replay), in rank
+mode on the one-GPU box (n processes share the GPU over the IPC-only communicator; not an xGMI measurement).
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29541 \\
+      tools/graph_latency.py > gpurun_out/graph_latency.jsonl
+"""
+import json
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import hccl_amd as H  # noqa: E402
+
+K = 100
+
+
+def main():
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    os.environ.setdefault("HCCL_AMD_IPC_TIMEOUT_MS", "10000")
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def all_gather(b):
+        out = [None] * world
+        dist.all_gather_object(out, b)
+        return out
+
+    comm = H.comm_init_host_exchange(world, rank, all_gather)
+    comm.set_algo(H.Algo.IPC)
+    s = torch.cuda.Stream()
+    for nbytes in (1 << 10, 64 << 10, 1 << 20):
+        x = torch.ones(nbytes // 2, dtype=torch.float16, device="cuda")
+        y = torch.empty_like(x)
+        for _ in range(10):
+            comm.all_reduce(x, y, H.HcclReduceOp.SUM, s)
+        torch.cuda.synchronize()
+        dist.barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(K):
+            comm.all_reduce(x, y, H.HcclReduceOp.SUM, s)
+        e1.record(s)
+        torch.cuda.synchronize()
+        eager = e0.elapsed_time(e1) / K
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=torch.cuda.Stream()):
+            cs = torch.cuda.current_stream()
+            for _ in range(K):
+                comm.all_reduce(x, y, H.HcclReduceOp.SUM, cs)
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        dist.barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        cur = torch.cuda.current_stream()
+        e0.record(cur)
+        for _ in range(5):
+            g.replay()
+        e1.record(cur)
+        torch.cuda.synchronize()
+        graph = e0.elapsed_time(e1) / (5 * K)
+        ok = bool(torch.all(y == world).item())
+        t = torch.tensor([eager, graph])
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if rank == 0:
+            print(json.dumps({"n": world, "bytes": nbytes, "eager_us": round(float(t[0]) * 1e3, 2),
+                              "graph_us": round(float(t[1]) * 1e3, 2), "ok": ok,
+                              "ipc_status_bit0": comm.ipc_status() & 1}), flush=True)
+        del g
+    torch.cuda.synchronize()
+    dist.barrier()
+    comm.destroy()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
