@@ -329,6 +329,34 @@ def _timed(fn, iters: int, warmup: int = 2) -> float:
     return float(t[0])
 
 
+def _graph_us(call, calls: int = 50, replays: int = 5) -> float:
+    """Per-call microseconds of `call(stream)` captured `calls` times in one HIP graph and replayed, max over ranks.
+    Every rank captures the same calls, so the replays' barriers pair up."""
+    import torch.distributed as dist
+
+    g = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, stream=torch.cuda.Stream()):
+        st = torch.cuda.current_stream()
+        for _ in range(calls):
+            call(st)
+    g.replay()
+    torch.cuda.synchronize()
+    dist.barrier()
+    cur = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(cur)
+    for _ in range(replays):
+        g.replay()
+    e1.record(cur)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = torch.tensor([e0.elapsed_time(e1) * 1e3 / (calls * replays)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    del g
+    return float(t[0])
+
+
 def bench_c4(comm, send, recv, world) -> dict:
     """C4: ZeRO-style gradient bucket, bf16, 2 GiB per rank: HcclReduceScatter (SUM) then HcclAllGather."""
     nbytes = 2 << 30
@@ -420,6 +448,17 @@ def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
                 if algo == H.Algo.IPC:
                     row["ipc_ran"] = H.Algo(comm.last_algo).name
                     row["ipc_barrier_timeouts"] = comm.ipc_status() & 1
+            if nbytes <= (1 << 20) and row.get("ipc_ran") == "IPC":
+                # the latency end replayed from a HIP graph (50 captured calls per replay; device-side epochs)
+                try:
+                    comm.set_algo(H.Algo.IPC)
+                    row["ipc_graph_us"] = round(_graph_us(lambda st: comm.all_reduce(a, b, H.HcclReduceOp.SUM, st)),
+                                                1)
+                    row["ipc_graph_barrier_timeouts"] = comm.ipc_status() & 1
+                except Exception as e:  # noqa: BLE001  (capture problems never end the sweep)
+                    row["ipc_graph_error"] = f"{type(e).__name__}: {e}"
+                finally:
+                    comm.set_algo(H.Algo.AUTO)
             rows.append(row)
             nbytes *= 2
     finally:
