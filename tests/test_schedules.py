@@ -303,6 +303,36 @@ def test_sends_and_recvs_pair_up():
                 assert sends == recvs, (op_type, algo, a, b)
 
 
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
+@pytest.mark.parametrize("op_type,algo", CASES + [(AR, 7), (RS, 7)])
+def test_every_output_holds_every_rank_once_at_its_offset(op_type, algo, n):
+    """The reference ST's semantics check (test/st/algorithm/utils/src/hccl_verifier/.../allreduce_semantics_checker.cc:
+    every output range is built from the INPUT of all rankSize ranks at the same offset), made numeric: rank r's
+    element i is i * 2^20 + 2^r in int64, so the SUM at i is n * i * 2^20 + 2^n - 1 exactly when each rank
+    contributes once and from offset i. A missing or repeated rank changes the low bits; a wrong offset the high ones.
+    AllGather: block q of every output is rank q's input."""
+    count, root = 10007, n // 2
+    progs, used, scratch = programs(op_type, algo, n, count, O.INT64, root=root, piece_bytes=4096)
+    in_count = count * n if op_type == RS else count
+    idx = np.arange(in_count, dtype=np.int64)
+    xs = [idx * (1 << 20) + (1 << r) for r in range(n)]
+    bufs = [[x.copy(), np.zeros(count * n if op_type == AG else count, np.int64), np.zeros(max(scratch, 1), np.int64)]
+            for x in xs]
+    assert O.replay(n, O.INT64, O.SUM, progs, bufs) == 0
+    full = (1 << n) - 1
+    for r in range(n):
+        out = bufs[r][1]
+        if op_type == AG:
+            assert np.array_equal(out, np.concatenate(xs)), r
+        elif op_type == RS:
+            g = np.arange(r * count, (r + 1) * count, dtype=np.int64)
+            assert np.array_equal(out, n * g * (1 << 20) + full), r
+        elif op_type == RED and r != root:
+            assert not out.any()
+        else:
+            assert np.array_equal(out, n * np.arange(count, dtype=np.int64) * (1 << 20) + full), (r, used)
+
+
 @pytest.mark.parametrize("inplace", [False, True])
 def test_groups_are_race_free(inplace):
     """The reference ST's memory-conflict check (test/st/algorithm/utils/src/hccl_verifier/mem_conflict_check/)
