@@ -239,7 +239,14 @@ std::atomic<uint32_t> g_order{0};
 // peaks with ~16 KiB of loads in flight per CU (2 workgroups x 256 lanes x 2 operands x 16 B) and nt loads+stores;
 // more bytes in flight lowers throughput.
 constexpr LaunchCfg kDefault2{2, 1, 3, 0};
-constexpr LaunchCfg kDefaultN{2, 2, 3, 0};
+// The n-ary fold's input loop is serial per wave (input j+1 is loaded after input j is folded), so its loads in flight
+// per CU are blocksPerCu x waves x U vectors, whatever n is. Two inputs behave like the 2-input kernel (U = 1 best);
+// from three inputs up, U = 4 keeps enough bytes in flight (tools/sweep_fold_launch.py, interleaved rounds, fp32 SUM,
+// 1 GiB per input: n = 2 498 vs 554 us at U = 2; n = 3 714 vs 745; n = 4 913 vs 927; n = 8 1709 vs 1787).
+constexpr LaunchCfg kDefaultN2{2, 1, 3, 0};
+constexpr LaunchCfg kDefaultN{2, 4, 3, 0};
+
+constexpr const LaunchCfg& DefaultFor(uint32_t nsrc) { return nsrc <= 2 ? kDefaultN2 : kDefaultN; }
 
 LaunchCfg CurrentCfg(const LaunchCfg& dflt)
 {
@@ -374,7 +381,7 @@ template <class E, int OP>
 hipError_t RunN(void* out, const void* const* srcs, uint32_t n, uint64_t count, hipStream_t stream)
 {
     using S = typename E::S;
-    LaunchCfg cfg = CurrentCfg(kDefaultN);
+    LaunchCfg cfg = CurrentCfg(DefaultFor(n));
     SrcPack pk{};
     const void* ptrs[HCCL_AMD_IR_MAX_SRC + 1];
     ptrs[0] = out;
@@ -402,6 +409,10 @@ hipError_t RunN(void* out, const void* const* srcs, uint32_t n, uint64_t count, 
             default: return hipErrorInvalidValue;
         }
     } else {
+        if (n <= 2) {
+            uint32_t grid = GridFor(nvec, kBlock * kDefaultN2.unroll, cfg);
+            return RunNVariant<E, OP, kDefaultN2.unroll, kDefaultN2.nt>(out, pk, int(n), nvec, edges, grid, stream);
+        }
         uint32_t grid = GridFor(nvec, kBlock * kDefaultN.unroll, cfg);
         return RunNVariant<E, OP, kDefaultN.unroll, kDefaultN.nt>(out, pk, int(n), nvec, edges, grid, stream);
     }
@@ -528,12 +539,17 @@ template <class E, int OP>
 hipError_t RunBatch(const BatchPack& pk, uint32_t nseg, uint64_t maxVec, hipStream_t stream)
 {
     // fill the chip once across the batch: the per-CU budget of the n-ary default, split over the segments
-    const LaunchCfg cfg = kDefaultN;
+    const LaunchCfg& cfg = DefaultFor(static_cast<uint32_t>(pk.nsrc));
     const uint64_t cap = std::max<uint64_t>(1, uint64_t(CuCount()) * cfg.blocksPerCu / nseg);
     const uint64_t need = std::max<uint64_t>(1, (maxVec + kBlock * cfg.unroll - 1) / (kBlock * cfg.unroll));
     const uint32_t gx = static_cast<uint32_t>(std::min(cap, need));
-    hipLaunchKernelGGL((k_reduceN_batch<E, OP, kDefaultN.unroll, kDefaultN.nt>), dim3(gx, nseg), dim3(kBlock), 0,
-                       stream, pk);
+    if (pk.nsrc <= 2) {
+        hipLaunchKernelGGL((k_reduceN_batch<E, OP, kDefaultN2.unroll, kDefaultN2.nt>), dim3(gx, nseg), dim3(kBlock),
+                           0, stream, pk);
+    } else {
+        hipLaunchKernelGGL((k_reduceN_batch<E, OP, kDefaultN.unroll, kDefaultN.nt>), dim3(gx, nseg), dim3(kBlock), 0,
+                           stream, pk);
+    }
     return hipGetLastError();
 }
 
