@@ -1,0 +1,127 @@
+"""Parity at BASELINE.json's full sizes (configs C3, C4, C5) on a loopback world of 8 ranks on the one GPU, through
+properties that do not need the CPU oracle to run at that size:
+  * C3, 4 GiB fp32 per rank, two-shot order O2 (ins_temp_all_reduce_mesh_1D_two_shot.cc:327-335) on random data:
+    bit-exact against the same left fold done by torch on the GPU (IEEE fp32 adds in the same order), on the RCCL-path
+    schedule and on the one-sided IPC kernel;
+  * C3 with the reference's own selection (MeshChunk at this size) on integer-valued fp32: exact sums, so every
+    element holds every rank exactly once;
+  * C4, 2 GiB bf16 per rank: ReduceScatter then AllGather of integer-valued bf16 equals the exact AllReduce;
+  * C5's largest point, 4 GiB fp16 per rank on the RHD schedule: integer-valued fp16, exact sums.
+The small-size tests pin the association order of every family bit for bit against the oracle; these pin that
+nothing changes at the sizes the benchmark runs.
+"""
+import threading
+
+import pytest
+import torch
+
+import hccl_amd as H
+
+pytestmark = pytest.mark.gpu
+
+N = 8
+
+
+@pytest.fixture(scope="module")
+def world():
+    comms = H.loopback_world(N)
+    yield comms
+    torch.cuda.synchronize()
+    for c in comms:
+        c.destroy()
+
+
+def run_all(comms, fn):
+    errs = []
+    streams = [torch.cuda.Stream() for _ in comms]
+
+    def body(r):
+        try:
+            fn(r, streams[r])
+        except Exception as e:  # noqa: BLE001
+            errs.append((r, e))
+
+    torch.cuda.synchronize()
+    th = [threading.Thread(target=body, args=(r,)) for r in range(len(comms))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=900)
+    torch.cuda.synchronize()
+    assert not errs, errs
+
+
+def pattern(count, r, dtype, mod):
+    """Small integers, exact in `dtype` and in every partial sum over 8 ranks: (i % mod) + r."""
+    return (torch.arange(count, device="cuda", dtype=torch.int64) % mod + r).to(dtype)
+
+
+@pytest.mark.parametrize("algo", [H.Algo.MESH_TWOSHOT, H.Algo.IPC_TWOSHOT])
+def test_c3_full_size_two_shot_bit_exact_random(world, algo):
+    count = (4 << 30) // 4
+    xs = []
+    for r in range(N):
+        g = torch.Generator(device="cuda").manual_seed(0xC3 + r)
+        xs.append(torch.rand(count, device="cuda", generator=g).mul_(2).sub_(1))
+    want = xs[0].clone()
+    for r in range(1, N):
+        want.add_(xs[r])  # acc = x_r + acc, r ascending (order O2)
+    outs = [torch.empty(count, device="cuda") for _ in range(N)]
+    for c in world:
+        c.set_algo(algo)
+    try:
+        run_all(world, lambda r, s: world[r].all_reduce(xs[r], outs[r], H.HcclReduceOp.SUM, s))
+        assert world[0].last_algo == algo
+        for r in range(N):
+            bad = torch.count_nonzero(outs[r].view(torch.int32) != want.view(torch.int32)).item()
+            assert bad == 0, (r, bad)
+    finally:
+        for c in world:
+            c.set_algo(H.Algo.AUTO)
+    del xs, outs, want
+
+
+def test_c3_full_size_reference_selection_exact(world):
+    count = (4 << 30) // 4
+    xs = [pattern(count, r, torch.float32, 251) for r in range(N)]
+    outs = [torch.empty(count, device="cuda") for _ in range(N)]
+    run_all(world, lambda r, s: world[r].all_reduce(xs[r], outs[r], H.HcclReduceOp.SUM, s))
+    assert world[0].last_algo == H.Algo.MESH_CHUNK  # bytes * 8 / n^2 > 32 MiB (all_reduce_auto_selector.cc)
+    want = pattern(count, 0, torch.float32, 251).mul_(N).add_(N * (N - 1) // 2)
+    for r in range(N):
+        assert torch.equal(outs[r], want), r
+    del xs, outs, want
+
+
+def test_c4_full_size_reduce_scatter_then_all_gather(world):
+    count = (2 << 30) // 2
+    shard = count // N
+    xs = [pattern(count, r, torch.bfloat16, 29) for r in range(N)]
+    shards = [torch.empty(shard, dtype=torch.bfloat16, device="cuda") for _ in range(N)]
+    fulls = [torch.empty(count, dtype=torch.bfloat16, device="cuda") for _ in range(N)]
+    run_all(world, lambda r, s: world[r].reduce_scatter(xs[r], shards[r], H.HcclReduceOp.SUM, s))
+    rs_algo = world[0].last_algo
+    run_all(world, lambda r, s: world[r].all_gather(shards[r], fulls[r], s))
+    want = pattern(count, 0, torch.float32, 29).mul_(N).add_(N * (N - 1) // 2).to(torch.bfloat16)
+    for r in range(N):
+        assert torch.equal(shards[r], want[r * shard:(r + 1) * shard]), (r, rs_algo)
+        assert torch.equal(fulls[r], want), r
+    del xs, shards, fulls, want
+
+
+def test_c5_largest_point_rhd_exact(world):
+    count = (4 << 30) // 2
+    xs = [pattern(count, r, torch.float16, 61) for r in range(N)]
+    outs = [torch.empty(count, dtype=torch.float16, device="cuda") for _ in range(N)]
+    for c in world:
+        c.set_algo(H.Algo.RHD)
+    try:
+        run_all(world, lambda r, s: world[r].all_reduce(xs[r], outs[r], H.HcclReduceOp.SUM, s))
+        assert world[0].last_algo == H.Algo.RHD
+        want = pattern(count, 0, torch.float32, 61).mul_(N).add_(N * (N - 1) // 2).to(torch.float16)
+        for r in range(N):
+            assert torch.equal(outs[r], want), r
+    finally:
+        for c in world:
+            c.set_algo(H.Algo.AUTO)
+    del xs, outs
