@@ -636,6 +636,17 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
                 extra[name] = fn()
             except Exception as e:  # noqa: BLE001  (a secondary config never hides the headline line)
                 extra[name] = {"error": f"{type(e).__name__}: {e}"}
+    # correctness of the measured path at the measured size: integer-valued inputs make every order exact, so the
+    # auto AllReduce must return exactly sum_r((i % 251) + r) on every rank (checked on the GPU, AND over ranks)
+    check = torch.arange(count, device=dev, dtype=torch.int64) % 251
+    send.copy_(check + rank)
+    comm.set_algo(H.Algo.AUTO)
+    comm.all_reduce(send, recv, H.HcclReduceOp.SUM, stream)
+    torch.cuda.synchronize()
+    ok = torch.tensor([1 if torch.equal(recv, (check * world + world * (world - 1) // 2).to(recv.dtype)) else 0])
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    result_ok = bool(ok.item())
+    del check
     comm.destroy()
     rccl_ref = None
     if not args.no_rccl_ref:
@@ -663,6 +674,7 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
         },
         "busbw_GBps": round(busbw, 2),
         "algbw_GBps": round(algbw, 2),
+        "result_ok": result_ok,
         "rccl_allreduce_reference": rccl_ref,
         "other_configs": extra,
         "roofline": {
