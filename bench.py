@@ -304,6 +304,32 @@ def rccl_allreduce_reference(send, recv, world, args):
         t = _timed(lambda: dist.all_gather_into_tensor(recv, shard, group=g), 3)
         out["allgather_ms"] = round(t * 1e3, 3)
         out["allgather_busbw_GBps"] = round(C3_BYTES / t / 1e9 * f, 2)
+        # B_link: RCCL send/recv of 1 GiB between ranks 0 and 1 over their one direct link, one way
+        # and both ways at once; the other ranks only take part in the barriers
+        rank = dist.get_rank()
+        nbytes = 1 << 30
+        a, b = send.view(torch.uint8)[:nbytes], recv.view(torch.uint8)[:nbytes]
+
+        def p2p(both):
+            ops = []
+            if rank == 0:
+                ops.append(dist.P2POp(dist.isend, a, 1, g))
+                if both:
+                    ops.append(dist.P2POp(dist.irecv, b, 1, g))
+            elif rank == 1:
+                ops.append(dist.P2POp(dist.irecv, b, 0, g))
+                if both:
+                    ops.append(dist.P2POp(dist.isend, a, 0, g))
+            for req in dist.batch_isend_irecv(ops) if ops else ():
+                req.wait()
+
+        try:
+            t = _timed(lambda: p2p(False), 3)
+            out["link_probe"] = {"pair": [0, 1], "bytes": nbytes, "one_way_GBps": round(nbytes / t / 1e9, 2)}
+            t = _timed(lambda: p2p(True), 3)
+            out["link_probe"]["both_ways_GBps_per_direction"] = round(nbytes / t / 1e9, 2)
+        except Exception as e:  # noqa: BLE001  (the probe never hides the rows above)
+            out["link_probe"] = {"error": f"{type(e).__name__}: {e}"}
         return out
     except Exception as e:  # noqa: BLE001
         return {"error": f"{type(e).__name__}: {e}"}
