@@ -55,7 +55,10 @@ __device__ __forceinline__ bool Barrier(const IpcArgs& a, uint32_t me, uint32_t 
     const uint32_t t = threadIdx.x;
     if (t < a.n) {
         if (t == 0) failed = 0;  // every thread read the previous barrier's value before the __syncthreads above
-        __threadfence_system();
+        // The system-scope release store below writes the L2 back first (buffer_wbl2 sc0 sc1). Every wave of the
+        // block has drained its stores (vmcnt(0)) before the workgroup barrier, so that write-back covers the
+        // whole block's data. A separate __threadfence_system() here only added a second write-back and an
+        // invalidate per barrier.
         uint32_t* remote = a.flags[t] + blockIdx.x * a.n + me;
         __hip_atomic_store(remote, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         uint32_t* mine = a.flags[me] + blockIdx.x * a.n + t;
