@@ -47,7 +47,21 @@ constexpr int kIpcU = 4;
 // set (status bit 0). The caller then stops at once, so a rank never stores into a peer it has lost track of. The
 // longest wait (in polls) stays in the lane's `waitMax` and is published once per launch (PublishWait), off the
 // barrier's critical path.
-__device__ __forceinline__ bool Barrier(const IpcArgs& a, uint32_t me, uint32_t epoch, uint32_t& waitMax)
+// The flag words lane t (< n) of block b uses in every barrier: the one it stores into on peer t, and the one peer t
+// stores into here. Computed once per launch (the pointer table is in kernel-argument memory, indexed per lane).
+struct FlagLane {
+    uint32_t* remote;
+    uint32_t* mine;
+};
+
+__device__ __forceinline__ FlagLane LaneFlags(const IpcArgs& a, uint32_t me)
+{
+    const uint32_t t = threadIdx.x;
+    if (t >= a.n) return {nullptr, nullptr};
+    return {a.flags[t] + blockIdx.x * a.n + me, a.flags[me] + blockIdx.x * a.n + t};
+}
+
+__device__ __forceinline__ bool Barrier(const IpcArgs& a, FlagLane fl, uint32_t epoch, uint32_t& waitMax)
 {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its stores have left the CU
     __syncthreads();
@@ -59,9 +73,8 @@ __device__ __forceinline__ bool Barrier(const IpcArgs& a, uint32_t me, uint32_t 
         // block has drained its stores (vmcnt(0)) before the workgroup barrier, so that write-back covers the
         // whole block's data. A separate __threadfence_system() here only added a second write-back and an
         // invalidate per barrier.
-        uint32_t* remote = a.flags[t] + blockIdx.x * a.n + me;
-        __hip_atomic_store(remote, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        uint32_t* mine = a.flags[me] + blockIdx.x * a.n + t;
+        __hip_atomic_store(fl.remote, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        uint32_t* mine = fl.mine;
         uint32_t polls = 0;
         bool cut = false;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz constant clock
@@ -101,22 +114,25 @@ __device__ __forceinline__ void PublishWait(const IpcArgs& a, uint32_t waitMax)
     }
 }
 
-// The last block of the launch to get here advances the epoch counter by the launch's barriers per block and resets
-// the finished-block count. Every block read the counter at its start, before counting itself here. A launch that
-// returns at once on a failed communicator (sticky bit) leaves the counter alone; no later launch waits on it.
-__device__ __forceinline__ void EndLaunch(const IpcArgs& a)
+// Epoch counter protocol. Every block reads the counter at its start, then counts itself in the arrival word
+// (kIpcDoneWord), in that order: the count is issued only once the read has returned. The block whose arrival
+// completes the grid advances the counter by the launch's barriers per block and resets the count (EndLaunch).
+// Every block read before it arrived, so no block of this launch can see the advanced value. The next launch in
+// stream order starts only after this one has ended, so it sees it. The arrival is a returning atomic issued at the
+// start, and its value is consumed only at the end, so its round trip overlaps the launch's work. A launch that
+// returns at once on a failed communicator (sticky bit) never arrives; no later launch waits on it.
+__device__ __forceinline__ uint32_t Arrive(const IpcArgs& a, uint32_t epoch)
 {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t total = gridDim.x * gridDim.y;
-        // relaxed: the count only needs the RMW order on its own word (this block's epoch load has returned before,
-        // since the kernel used it), and the next launch sees the new epoch through the end-of-kernel release
-        const uint32_t prev = __hip_atomic_fetch_add(a.status + kIpcDoneWord, 1u, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-        if (prev + 1 == total) {
-            __hip_atomic_store(a.status + kIpcDoneWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(a.status + kIpcEpochWord, a.epochSpan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+    if (threadIdx.x != 0) return 0;
+    asm volatile("" ::"v"(epoch) : "memory");  // the counter read has returned before the arrival is issued
+    return __hip_atomic_fetch_add(a.status + kIpcDoneWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void EndLaunch(const IpcArgs& a, uint32_t arrivedBefore)
+{
+    if (threadIdx.x == 0 && arrivedBefore + 1 == gridDim.x * gridDim.y) {
+        __hip_atomic_store(a.status + kIpcDoneWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(a.status + kIpcEpochWord, a.epochSpan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -304,10 +320,11 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
         char* base = static_cast<char*>(a.stgIn[c]);
         return single ? base + a.altOff + (e & 1u) * a.altBytes : base;
     };
-    // Epochs come from the device counter, read by every block before it signals anything; the last block of the
-    // launch to finish advances it (EndLaunch), so the next launch in stream order, a call or a graph replay alike,
-    // starts where this one ended. Every rank runs the same launch sequence, so the counters agree across ranks.
+    // Epochs come from the device counter (Arrive / EndLaunch), so the next launch in stream order, a call or a graph
+    // replay alike, starts where this one ended. Every rank runs the same launch sequence, so the counters agree.
     uint32_t epoch = __hip_atomic_load(a.status + kIpcEpochWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const FlagLane fl = LaneFlags(a, me);
+    const uint32_t arrivedBefore = Arrive(a, epoch);
     uint32_t waitMax = 0;
     for (uint32_t k = 0; k < a.rounds; ++k) {
         const uint64_t kP = uint64_t(k) * a.piece;
@@ -321,7 +338,7 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
             S* slot = reinterpret_cast<S*>(slotArea(c, epoch + 1)) + uint64_t(me) * a.piece;
             CopyRange<S>(slot, in + ChunkStart(a, c) + kP, r, ChunkVec<S>(a, c));
         }
-        if (!Barrier(a, me, ++epoch, waitMax)) break;
+        if (!Barrier(a, fl, ++epoch, waitMax)) break;
         if (a.kind == kIpcAllGather) {
             // phase 1 of an AllGather: rank q's piece, from my slot q (mine from my input), to output block q
             const Range r = BlockWindow(a, PieceLen(a, me, kP));
@@ -351,7 +368,7 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
             };
             FoldRange<E, OP>(a, me, kP, own, slots, dst, a.kind == kIpcAllReduce ? n : 1u, r, ChunkVec<S>(a, me));
         }
-        if (!single && !Barrier(a, me, ++epoch, waitMax)) break;
+        if (!single && !Barrier(a, fl, ++epoch, waitMax)) break;
         // phase 2: the other chunks' results from my own result area (two-shot AllReduce: every rank; two-shot
         // Reduce: the root)
         if (!oneShot && (a.kind == kIpcAllReduce || (reduceKind && me == a.root))) {
@@ -364,7 +381,7 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
         }
     }
     PublishWait(a, waitMax);
-    EndLaunch(a);
+    EndLaunch(a, arrivedBefore);
 }
 
 template <class E>
