@@ -271,6 +271,30 @@ def bench_local(args) -> dict:
             "kernel_p90_us": round(float(np.percentile(per, 90)) * 1e6, 2),
         },
     }
+    # the same stream shapes on PyTorch's own kernels, same buffers and stream: the vendor-library baseline for this
+    # op (torch.add, 2 reads + 1 write) and the 1 read + 1 write copy, as measured context for `frac`
+    try:
+        out = torch.empty_like(dst)
+
+        def rate(fn, nbytes, reps=10):
+            fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                fn()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            return round(nbytes / (e0.elapsed_time(e1) / 1e3 / reps) / 1e9, 1)
+
+        res["roofline"]["same_op_on_torch"] = {
+            "torch_add_GBps": rate(lambda: torch.add(src, dst, out=out), bytes_step),
+            "torch_copy_GBps": rate(lambda: out.copy_(src), 2 * C2_COUNT * 4),
+            "note": "torch.add(src, dst, out) over the same 2 x 1 GiB fp32 (3 GiB per call) and a 1 GiB copy",
+        }
+        del out
+    except Exception as e:  # noqa: BLE001
+        res["roofline"]["same_op_on_torch"] = {"error": f"{type(e).__name__}: {e}"}
     if not args.no_e2e:
         try:
             res["end_to_end_host_buffers"] = end_to_end_host()
