@@ -121,3 +121,34 @@ def test_headers_compile_as_plain_c(header, tmp_path):
     src.write_text(f'#include "{header}"\nint main(void) {{ return 0; }}\n')
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src), "-o",
                     str(tmp_path / "t")], check=True)
+
+
+def test_c_caller_links_and_gets_reference_codes(tmp_path):
+    """A plain C caller, written the way the reference's samples call HCCL (examples/02_collectives/01_allreduce/
+    main.cc), compiles against include/hccl.h, links libhccl_amd.so and gets the reference's entry-check codes
+    (no device work: every call returns before touching memory)."""
+    src = tmp_path / "caller.c"
+    src.write_text(r'''
+#include <stdio.h>
+#include "hccl.h"
+int main(void) {
+    void* p = (void*)0x1000;
+    int bad = 0;
+    bad |= HcclAllReduce(NULL, NULL, 0, HCCL_DATA_TYPE_FP32, HCCL_REDUCE_SUM, NULL, NULL) != HCCL_SUCCESS;
+    bad |= HcclAllReduce(p, p, 8, HCCL_DATA_TYPE_FP32, HCCL_REDUCE_SUM, p, NULL) != HCCL_E_PTR;
+    bad |= HcclReduceScatter(p, p, 8, HCCL_DATA_TYPE_BFP16, HCCL_REDUCE_SUM, NULL, p) != HCCL_E_PTR;
+    bad |= HcclReduce(p, p, 8, HCCL_DATA_TYPE_FP16, HCCL_REDUCE_MAX, 0, NULL, p) != HCCL_E_PTR;
+    bad |= HcclAllGather(p, p, 8, HCCL_DATA_TYPE_INT8, NULL, p) != HCCL_E_PTR;
+    bad |= HcclGetRootInfo(NULL) != HCCL_E_PTR;
+    uint32_t n = 0;
+    bad |= HcclGetRankSize(NULL, &n) != HCCL_E_PTR;
+    printf("%s\n", bad ? "FAIL" : "OK");
+    return bad;
+}
+''')
+    exe = tmp_path / "caller"
+    libdir = os.path.dirname(H.LIB_PATH)
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src), "-o",
+                    str(exe), "-L", libdir, "-lhccl_amd", f"-Wl,-rpath,{libdir}"], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.strip() == "OK", (out.stdout, out.stderr)
