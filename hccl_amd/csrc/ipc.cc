@@ -1,6 +1,6 @@
-// ipc.cc — host side of the one-sided AllReduce (ipc_kernels.hip): peer-mapped staging set-up and launch.
+// ipc.cc — host side of the one-sided collectives (ipc_kernels.hip): peer-mapped staging set-up and launch.
 //
-// Set-up (collective, on the first IPC AllReduce of a communicator): every rank allocates uncached staging and a
+// Set-up (collective, on the first IPC call of a communicator): every rank allocates uncached staging and a
 // flag array, exports them with hipIpcGetMemHandle, all-gathers the handles over the communicator (ncclAllGather)
 // and opens every peer's with hipIpcOpenMemHandle — the reference's channel set-up that hands each rank its peers'
 // CCL buffers (ChannelInfo.remoteCclMem, alg_param.h:434-448; AIV GM_IN[r], aiv_communication_base_v2.h:121-150).

@@ -1,4 +1,4 @@
-// ipc.h — one-sided AllReduce / ReduceScatter / Reduce over peer-mapped staging (host state + launch interface).
+// ipc.h — one-sided AllReduce / ReduceScatter / Reduce / AllGather over peer-mapped staging (host state + launch).
 #pragma once
 
 #include <hip/hip_runtime.h>

@@ -1,4 +1,5 @@
-// ipc_kernels.hip — one-sided AllReduce over peer-mapped staging buffers.
+// ipc_kernels.hip — one-sided AllReduce / ReduceScatter / Reduce / AllGather over peer-mapped staging buffers
+// (SURVEY.md §8f rank 3). The two-shot AllReduce is described first; the other kinds are variations of it (IpcKind).
 //
 // The reference's AIV engine runs AllReduce as ONE kernel whose blocks write into every peer's CCL buffer
 // (GM_IN[r]) and synchronise with per-block flags (aiv_all_reduce_mesh_1d_twoshot.h:20-217,
