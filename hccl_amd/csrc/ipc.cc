@@ -214,8 +214,8 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
             break;
         default: return HCCL_E_NOT_SUPPORT;
     }
-    // Stream capture: the barrier epochs live on the device (status word kIpcEpochWord, advanced by the last block
-    // of every launch), so a captured launch replays correctly: each replay takes the next epochs, as a new call
+    // Stream capture: the barrier epochs live on the device (status word kIpcEpochWord, advanced once per launch by
+    // the block that completes its arrival count), so a captured launch replays correctly: each replay takes the next epochs, as a new call
     // would. Two things cannot be captured: the collective set-up of the first call (allocation, host exchange,
     // device synchronisation) and the loopback world, which exchanges events between host threads per call. Those
     // report NOT_SUPPORT under capture; a communicator with RCCL then takes the RCCL schedule of the same family.
@@ -231,8 +231,8 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
     // workgroups per rank (equal on every rank: block b pairs with block b of each peer, and the default is a function
     // of the call's arguments alone). A loopback world runs every rank's blocks in one launch on one GPU, so it keeps
     // at most kIpcBlocks per rank to stay co-resident.
-    const bool nBlocks = opType == HCCL_AMD_OP_REDUCE_SCATTER || opType == HCCL_AMD_OP_ALLGATHER;
-    const uint64_t callBytes = (nBlocks ? uint64_t(c.nRanks) : 1u) * count * es;  // RS input / AG output
+    const bool blockLayout = opType == HCCL_AMD_OP_REDUCE_SCATTER || opType == HCCL_AMD_OP_ALLGATHER;
+    const uint64_t callBytes = (blockLayout ? uint64_t(c.nRanks) : 1u) * count * es;  // RS input / AG output
     s.blocks = c.ipcBlocks != 0 ? c.ipcBlocks : DefaultIpcBlocks(callBytes);
     if (c.transport->SharedDevice()) s.blocks = std::min(s.blocks, kIpcBlocks);
     const uint64_t V = 16 / es;
