@@ -215,11 +215,11 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
         default: return HCCL_E_NOT_SUPPORT;
     }
     // Stream capture: the barrier epochs live on the device (status word kIpcEpochWord, advanced once per launch by
-    // the block that completes its arrival count), so a captured launch replays correctly: each replay takes the next epochs, as a new call
-    // would. Two things cannot be captured: the collective set-up of the first call (allocation, host exchange,
-    // device synchronisation) and the loopback world, which exchanges events between host threads per call. Those
-    // report NOT_SUPPORT under capture; a communicator with RCCL then takes the RCCL schedule of the same family.
-    // Every rank of a collective is captured alike, so they all decide the same way.
+    // the block that completes its arrival count), so a captured launch replays correctly: each replay takes the
+    // next epochs, as a new call would. Two things cannot be captured: the collective set-up of the first call
+    // (allocation, host exchange, device synchronisation) and the loopback world, which exchanges events between
+    // host threads per call. Those report NOT_SUPPORT under capture; a communicator with RCCL then takes the RCCL
+    // schedule of the same family. Every rank of a collective is captured alike, so they all decide the same way.
     hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(stream, &capture) != hipSuccess) return HCCL_E_NOT_SUPPORT;
     if (capture != hipStreamCaptureStatusNone && (!c.ipc.ready || c.transport->SharedDevice())) {
