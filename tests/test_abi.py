@@ -152,3 +152,17 @@ int main(void) {
                     str(exe), "-L", libdir, "-lhccl_amd", f"-Wl,-rpath,{libdir}"], check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0 and out.stdout.strip() == "OK", (out.stdout, out.stderr)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    """No fallback: with the shared object absent, importing the package raises instead of running anything else.
+    Checked on a copy of the package in a scratch directory, so the real build is untouched."""
+    import shutil
+    pkg = tmp_path / "hccl_amd"
+    shutil.copytree(os.path.join(ROOT, "hccl_amd"), pkg,
+                    ignore=shutil.ignore_patterns("*.so", "build", "csrc", "__pycache__", "Makefile"))
+    code = "import hccl_amd"
+    out = subprocess.run([os.sys.executable, "-c", code], cwd=str(tmp_path), capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode != 0
+    assert "ImportError" in out.stderr and "no fallback" in out.stderr, out.stderr[-2000:]
