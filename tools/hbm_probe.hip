@@ -197,3 +197,12 @@ int probe_launch(int kind, int variant, int blocksPerCu, const void* a, const vo
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 }
+
+// Uncached (MTYPE UC) allocations, the IPC staging's memory type, to compare streams that read or write it.
+extern "C" void* probe_alloc_uncached(uint64_t bytes)
+{
+    void* p = nullptr;
+    return hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) == hipSuccess ? p : nullptr;
+}
+
+extern "C" int probe_free(void* p) { return hipFree(p) == hipSuccess ? 0 : 1; }
