@@ -96,6 +96,12 @@ def set_reduce_launch(blocks_per_cu: int = 0, unroll: int = 0, cache_policy: int
     check("HcclAmdSetReduceLaunch", lib.HcclAmdSetReduceLaunch(blocks_per_cu, unroll, cache_policy))
 
 
+def set_fold_mode(mode: int = 0) -> None:
+    """Operand pipelining of the n-ary fold (0 default, 1 serial, 2 prefetch, 3 all operands first);
+    see HcclAmdSetFoldMode in include/hccl_amd.h."""
+    check("HcclAmdSetFoldMode", lib.HcclAmdSetFoldMode(mode))
+
+
 # ----------------------------------------------------------------------------------------- schedules
 
 
@@ -174,6 +180,12 @@ class Comm:
         """Status word of the IPC path (bit 0: a cross-rank barrier timed out on the last IPC AllReduce)."""
         v = ctypes.c_uint32(0)
         check("HcclAmdCommIpcStatus", lib.HcclAmdCommIpcStatus(self.handle, ctypes.byref(v)))
+        return v.value
+
+    def async_error(self) -> int:
+        """HcclGetCommAsyncError: HCCL_E_TIMEOUT after an IPC barrier timeout, an RCCL asynchronous error, or 0."""
+        v = ctypes.c_int(0)
+        check("HcclGetCommAsyncError", lib.HcclGetCommAsyncError(self.handle, ctypes.byref(v)))
         return v.value
 
     def all_reduce(self, send: torch.Tensor, recv: torch.Tensor, op: int = HcclReduceOp.SUM, stream=None) -> None:

@@ -139,11 +139,13 @@ SIGNATURES = {
     "HcclCommDestroy": (_res, [_vp]),
     "HcclGetRankSize": (_res, [_vp, ctypes.POINTER(_u32)]),
     "HcclGetRankId": (_res, [_vp, ctypes.POINTER(_u32)]),
+    "HcclGetCommAsyncError": (_res, [_vp, ctypes.POINTER(ctypes.c_int)]),
     # include/hccl_amd.h
     "HcclAmdLocalReduce": (_res, [_vp, _vp, _u64, _i32, _i32, _vp]),
     "HcclAmdLocalReduce2": (_res, [_vp, _vp, _vp, _u64, _i32, _i32, _vp]),
     "HcclAmdLocalReduceN": (_res, [_vp, ctypes.POINTER(_vp), _u32, _u64, _i32, _i32, _vp]),
     "HcclAmdSetReduceLaunch": (_res, [_u32, _u32, _u32]),
+    "HcclAmdSetFoldMode": (_res, [_u32]),
     "HcclAmdDataTypeSize": (_u32, [_i32]),
     "HcclAmdGetErrorString": (ctypes.c_char_p, [_i32]),
     "HcclAmdSelectAlgo": (_i32, [_i32, _u32, _u64, _i32]),
@@ -160,6 +162,7 @@ SIGNATURES = {
     "HcclAmdCommSetIpcBlocks": (_res, [_vp, _u32]),
     "HcclAmdCommLastAlgo": (_i32, [_vp]),
     "HcclAmdCommIpcStatus": (_res, [_vp, ctypes.POINTER(_u32)]),
+    "HcclAmdIpcTimeoutMs": (_u64, []),
     "HcclAmdCommInitHostExchange": (_res, [_u32, _u32, _vp, _vp, ctypes.POINTER(_vp)]),
     "HcclAmdRankTableInfo": (_res, [ctypes.c_char_p, _u32, ctypes.POINTER(_u32), ctypes.POINTER(ctypes.c_int32)]),
     "HcclCommInitClusterInfo": (_res, [ctypes.c_char_p, _u32, ctypes.POINTER(_vp)]),

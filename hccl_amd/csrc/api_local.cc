@@ -46,6 +46,27 @@ bool IsReduceDataType(HcclDataType dt)
     }
 }
 
+bool ParseExecTimeoutSeconds(const char* env, double* seconds)
+{
+    // ParseExecTimeout / IsValidNumberFormat (src/common/alg_env_config.cc:43-110): digits, optionally one '.' with
+    // digits on both sides and at most two after it; at most UINT32_MAX. Unset or empty: not set.
+    if (env == nullptr || env[0] == '\0') return false;
+    const size_t len = std::strlen(env);
+    const char* dot = std::strchr(env, '.');
+    for (size_t i = 0; i < len; ++i) {
+        if (env + i == dot) continue;
+        if (env[i] < '0' || env[i] > '9') return false;
+    }
+    if (dot != nullptr) {
+        const size_t decimals = len - size_t(dot - env) - 1;
+        if (dot == env || decimals == 0 || decimals > 2) return false;
+    }
+    const double v = std::strtod(env, nullptr);
+    if (!(v >= 0.0) || v > 4294967295.0) return false;
+    *seconds = v;
+    return true;
+}
+
 bool DebugEnabled()
 {
     static int v = [] {
@@ -97,6 +118,8 @@ HcclResult HcclAmdSetReduceLaunch(uint32_t blocksPerCu, uint32_t unroll, uint32_
 {
     return SetReduceLaunch(blocksPerCu, unroll, cachePolicy);
 }
+
+HcclResult HcclAmdSetFoldMode(uint32_t mode) { return SetFoldMode(mode); }
 
 uint32_t HcclAmdDataTypeSize(HcclDataType dataType) { return DataTypeSize(dataType); }
 

@@ -73,6 +73,29 @@ HcclResult Comm::NextEvent(hipEvent_t* e)
     return HCCL_SUCCESS;
 }
 
+HcclResult Comm::PollAsyncError()
+{
+    if (failCode != HCCL_SUCCESS) return failCode;
+    if (ipc.failWatch != nullptr && *ipc.failWatch != 0) {
+        failCode = HCCL_E_TIMEOUT;  // an IPC barrier wait exceeded its bound (IpcTimeoutTicks)
+    } else if (transport != nullptr) {
+        failCode = transport->AsyncError();
+    }
+    return failCode;
+}
+
+HcclResult Comm::Gate()
+{
+    if (failed) return HCCL_E_SUSPENDING;
+    const HcclResult e = PollAsyncError();
+    if (e != HCCL_SUCCESS) {
+        failed = true;
+        HCCL_AMD_ERR("rank %u: communicator failed (%s); later collectives return HCCL_E_SUSPENDING", rank,
+                     HcclAmdGetErrorString(e));
+    }
+    return e;
+}
+
 Comm::~Comm()
 {
     magic = 0;
@@ -129,6 +152,12 @@ public:
         return FromNccl(ncclGroupEnd(), "ncclGroupEnd");
     }
     const char* Name() const override { return "rccl"; }
+    HcclResult AsyncError() override
+    {
+        ncclResult_t a = ncclSuccess;
+        if (ncclCommGetAsyncError(comm, &a) != ncclSuccess) return HCCL_E_INTERNAL;
+        return (a == ncclSuccess || a == ncclInProgress) ? HCCL_SUCCESS : FromNccl(a, "RCCL asynchronous error");
+    }
     HcclResult AllGatherHost(const void* mine, size_t bytes, void* all) override
     {
         int n = 0;

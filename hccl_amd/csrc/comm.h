@@ -38,6 +38,8 @@ public:
     virtual bool SharedDevice() const { return false; }
     // False for a bootstrap-only transport: the communicator's only data path is the one-sided IPC kernel.
     virtual bool HasSendRecv() const { return true; }
+    // An asynchronous failure of the transport (RCCL: ncclCommGetAsyncError), HCCL_SUCCESS if none. Non-blocking.
+    virtual HcclResult AsyncError() { return HCCL_SUCCESS; }
 };
 
 std::unique_ptr<Transport> MakeRcclTransport(void* uniqueId, uint32_t nRanks, uint32_t rank, HcclResult* err);
@@ -73,8 +75,20 @@ struct Comm {
     IpcState ipc;  // one-sided AllReduce path, set up on first use (collectively)
     uint32_t ipcBlocks = 0;  // workgroups per IPC launch, 0 = DefaultIpcBlocks(bytes) (HcclAmdCommSetIpcBlocks)
 
+    // Failure state. Work is stream-ordered and asynchronous, so a failure (an IPC barrier timeout, an RCCL async
+    // error) surfaces after the call that enqueued it has returned: the first collective entry that sees it returns
+    // the error itself (HCCL_E_TIMEOUT for a barrier timeout) and marks the communicator failed; every later entry
+    // returns HCCL_E_SUSPENDING, the reference's status gate (Selector, src/ops/op_common/op_common.cc:89-97: a
+    // communicator whose status is not READY). HcclGetCommAsyncError reports the error without changing state.
+    bool failed = false;
+    HcclResult failCode = HCCL_SUCCESS;
+
     HcclResult Init(int dev);
     HcclResult NextEvent(hipEvent_t* e);
+    // Non-blocking: the first asynchronous error seen on this communicator, HCCL_SUCCESS if none.
+    HcclResult PollAsyncError();
+    // Entry gate of every collective (call with mu held).
+    HcclResult Gate();
     ~Comm();
 };
 

@@ -29,6 +29,7 @@ HcclResult LaunchReduce2(void* out, const void* src, const void* dst, uint64_t c
 HcclResult LaunchReduceN(void* out, const void* const* srcs, uint32_t n, uint64_t count, HcclDataType dt,
                          HcclReduceOp op, hipStream_t stream);
 HcclResult SetReduceLaunch(uint32_t blocksPerCu, uint32_t unroll, uint32_t cachePolicy);
+HcclResult SetFoldMode(uint32_t mode);
 
 // Several independent ordered folds with the same operand count in ONE launch (blockIdx.y = segment): the executor
 // batches the consecutive REDUCE records of a schedule step (a MeshChunk piece's O6 sub-slices, the R rings' or RHD
@@ -42,6 +43,12 @@ struct FoldSeg {
 };
 HcclResult LaunchReduceNBatch(const FoldSeg* segs, uint32_t nseg, uint32_t nsrc, HcclDataType dt, HcclReduceOp op,
                               hipStream_t stream);
+
+// HCCL_EXEC_TIMEOUT in the reference's format (ParseExecTimeout, alg_env_config.cc:75-110): false when unset or
+// malformed, else *seconds (>= 0, <= UINT32_MAX, at most two decimals).
+bool ParseExecTimeoutSeconds(const char* env, double* seconds);
+// Barrier wait bound of the IPC kernel in s_memrealtime ticks (100 MHz); ipc.cc.
+uint64_t IpcTimeoutTicks();
 
 // ---- logging
 bool DebugEnabled();

@@ -25,6 +25,8 @@ struct Exported {
 struct RawPtrs {
     void* stg;
     uint32_t* flags;
+    uint32_t* failHost;
+    uint8_t ok;
 };
 
 // HCCL_AMD_IPC_L2_SCRUB=0 skips the scrub of fresh staging (diagnostics only: tests/test_gpu_collectives.py shows the
@@ -53,19 +55,35 @@ HcclResult IpcSetup(Comm& c)
               hipExtMallocWithFlags(reinterpret_cast<void**>(&s.flags), flagBytes, hipDeviceMallocUncached) ==
                   hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&s.status), kIpcStatusBytes) == hipSuccess &&
+              hipHostMalloc(reinterpret_cast<void**>(&s.failHost), 64, hipHostMallocCoherent | hipHostMallocMapped) ==
+                  hipSuccess &&
+              hipHostGetDevicePointer(reinterpret_cast<void**>(&s.failDev), s.failHost, 0) == hipSuccess &&
               hipDeviceSynchronize() == hipSuccess && (!ScrubEnabled() || ScrubL2(c.reduceStream) == HCCL_SUCCESS) &&
               hipMemset(s.flags, 0, flagBytes) == hipSuccess && hipMemset(s.status, 0, kIpcStatusBytes) == hipSuccess &&
               hipDeviceSynchronize() == hipSuccess;
-    if (!ok) HCCL_AMD_ERR("rank %u: IPC staging allocation failed", me);
+    if (ok) {
+        *s.failHost = 0;
+        s.failWatch = s.failHost;
+    } else {
+        HCCL_AMD_ERR("rank %u: IPC staging allocation failed", me);
+    }
     if (c.transport->SharedDevice()) {
-        if (!ok) return HCCL_E_MEMORY;
-        RawPtrs mine{s.stg, s.flags};
+        // Every rank thread takes part in the exchange whatever its local outcome (a rank that returned early
+        // would leave the others blocked in the rendezvous), and they all agree on the result.
+        RawPtrs mine{s.stg, s.flags, s.failHost, static_cast<uint8_t>(ok ? 1 : 0)};
         std::vector<RawPtrs> all(n);
-        HCCL_CHK(c.transport->AllGatherHost(&mine, sizeof mine, all.data()));
+        const HcclResult xr = c.transport->AllGatherHost(&mine, sizeof mine, all.data());
+        for (uint32_t r = 0; r < n && xr == HCCL_SUCCESS; ++r) ok = ok && all[r].ok != 0;
+        if (xr != HCCL_SUCCESS || !ok) {
+            IpcRelease(c);
+            s.unavailable = true;
+            return xr != HCCL_SUCCESS ? xr : HCCL_E_MEMORY;
+        }
         for (uint32_t r = 0; r < n; ++r) {
             s.peerStg[r] = all[r].stg;
             s.peerFlags[r] = all[r].flags;
         }
+        s.failWatch = all[0].failHost;  // the world's single launch is issued by rank 0 with its words
     } else {
         // Every rank takes part in both exchanges whatever happens locally, and the outcome is agreed: either all
         // ranks have every peer mapped or all release and report NOT_SUPPORT (the caller then runs the RCCL
@@ -114,17 +132,32 @@ bool Aligned16(const void* p, const void* q)
     return ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(q)) & 15u) == 0;
 }
 
-// Wall-time bound of one barrier wait: HCCL_AMD_IPC_TIMEOUT_MS (default 60 s), in 100 MHz s_memrealtime ticks.
+}  // namespace
+
+// Wall-time bound of one barrier wait, in 100 MHz s_memrealtime ticks. The IPC kernel is the reference's AIV engine,
+// so HCCL_EXEC_TIMEOUT follows its AIV-mode rule (docs/zh/user_guide/hccl_env/HCCL_EXEC_TIMEOUT.md): seconds with
+// at most two decimals, default 1091, and 0 or anything above 1091 taken as 1091. A malformed value is ignored with
+// the default, as ParseExecTimeout does (src/common/alg_env_config.cc:75-110). HCCL_AMD_IPC_TIMEOUT_MS (1 ms ..
+// 1 h), when set, takes precedence: it is the tests' and the benchmark's short bound.
 uint64_t IpcTimeoutTicks()
 {
-    uint64_t ms = 60000;
+    constexpr uint64_t kTicksPerMs = 100000;
     const char* e = std::getenv("HCCL_AMD_IPC_TIMEOUT_MS");
     if (e != nullptr && *e != '\0') {
         const unsigned long long v = std::strtoull(e, nullptr, 0);
-        if (v >= 1 && v <= 3600000ull) ms = v;
+        if (v >= 1 && v <= 3600000ull) return v * kTicksPerMs;
     }
-    return ms * 100000ull;
+    constexpr uint64_t kAivMaxMs = 1091000;
+    uint64_t ms = kAivMaxMs;
+    double sec = 0;
+    if (ParseExecTimeoutSeconds(std::getenv("HCCL_EXEC_TIMEOUT"), &sec) && sec > 0) {
+        const double m = sec * 1000.0;
+        ms = m >= double(kAivMaxMs) ? kAivMaxMs : std::max<uint64_t>(1, static_cast<uint64_t>(m + 0.5));
+    }
+    return ms * kTicksPerMs;
 }
+
+namespace {
 
 }  // namespace
 
@@ -157,7 +190,10 @@ void IpcRelease(Comm& c)
     if (s.stg != nullptr) (void)hipFree(s.stg);
     if (s.flags != nullptr) (void)hipFree(s.flags);
     if (s.status != nullptr) (void)hipFree(s.status);
+    if (s.failHost != nullptr) (void)hipHostFree(s.failHost);
+    const bool unavailable = s.unavailable;
     s = IpcState{};
+    s.unavailable = unavailable;
 }
 
 // Default workgroups per launch by the bytes of one rank's input. Every block runs its own cross-rank barrier (a
@@ -250,6 +286,7 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
     a.root = root;
     a.timeoutTicks = IpcTimeoutTicks();  // a lost peer ends the kernel with status bit 0, never a hang
     a.status = s.status;
+    a.failHost = s.failDev;
     a.callSeq = ++s.callSeq;  // equal on every rank of a loopback world (each runs this once per call)
     a.outStride = count;
     a.altOff = s.stgInBytes + s.stgResBytes;

@@ -81,6 +81,8 @@ struct IpcArgs {
     uint64_t altOff;    // byte offset of the alternate slot areas from stgIn[c] (same layout on every rank)
     uint64_t altBytes;  // bytes of one alternate area
     uint64_t timeoutTicks;  // per barrier wait, in s_memrealtime ticks (100 MHz)
+    uint32_t* failHost;  // host-visible word (pinned, coherent): set to 1 by the block whose barrier times out, read by
+                         // the host at every collective entry (Comm::Gate) and by HcclGetCommAsyncError
     uint32_t* status;  // [0] bit 0: a barrier timed out (sticky per communicator); [2..3]: (callSeq << 32) | longest
                        // wait of that call, in polls (64-bit max); [4]: epoch counter (barriers so far, per block);
                        // [5]: blocks of the running launch that have finished (kIpcEpochWord, kIpcDoneWord)
@@ -102,6 +104,10 @@ struct IpcState {
     uint32_t* flags = nullptr;     // own flags, uncached, zeroed
     uint32_t* status = nullptr;    // device words: [0] bit 0 = barrier timeout, [2..3] = tagged longest wait (IpcArgs)
     uint32_t callSeq = 0;          // IPC calls issued on the communicator (tags the wait diagnostic)
+    uint32_t* failHost = nullptr;  // pinned host word the kernel sets on a barrier timeout (hipHostMalloc, coherent)
+    uint32_t* failDev = nullptr;   // its device address (IpcArgs::failHost)
+    const volatile uint32_t* failWatch = nullptr;  // the word this rank's host polls: its own, or, in a loopback world
+                                                   // (one launch for all ranks, issued by rank 0), rank 0's
     void* peerStg[kIpcMaxRanks] = {};
     uint32_t* peerFlags[kIpcMaxRanks] = {};
     bool opened[kIpcMaxRanks] = {};

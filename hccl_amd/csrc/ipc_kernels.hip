@@ -79,7 +79,10 @@ __device__ __forceinline__ bool Barrier(const IpcArgs& a, FlagLane fl, uint32_t 
         uint32_t polls = 0;
         bool cut = false;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz constant clock
-        while (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+        // wrap-safe: the 32-bit epochs never reset (2 per round and call); a peer's flag is behind while the signed
+        // difference is negative, which stays true across the wrap at 2^32
+        while (static_cast<int32_t>(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) <
+               0) {
             ++polls;
             if ((polls & 63u) == 0) {
                 // a timeout anywhere (this or another block of this rank) ends the wait at once
@@ -89,6 +92,9 @@ __device__ __forceinline__ bool Barrier(const IpcArgs& a, FlagLane fl, uint32_t 
                 }
                 if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeoutTicks) {
                     __hip_atomic_fetch_or(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    // the host sees the failure without a device synchronisation: the next collective on this
+                    // communicator returns HCCL_E_TIMEOUT (Comm::Gate), every later one HCCL_E_SUSPENDING
+                    __hip_atomic_store(a.failHost, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     cut = true;
                     break;
                 }

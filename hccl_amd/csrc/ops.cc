@@ -67,6 +67,7 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
                          HcclReduceOp op, uint32_t root, hipStream_t stream)
 {
     std::lock_guard<std::mutex> lk(c.mu);
+    HCCL_CHK(c.Gate());  // a failed communicator takes no more work (op_common.cc:89-97)
     HIP_CHK(hipSetDevice(c.device));
     const uint32_t es = DataTypeSize(dt);
     if (c.nRanks == 1) {
@@ -239,6 +240,17 @@ HcclResult HcclCommDestroy(HcclComm comm)
     delete c;
     return HCCL_SUCCESS;
 }
+
+HcclResult HcclGetCommAsyncError(HcclComm comm, HcclResult* asyncError)
+{
+    Comm* c = AsComm(comm);
+    if (c == nullptr || asyncError == nullptr) return HCCL_E_PTR;
+    std::lock_guard<std::mutex> lk(c->mu);
+    *asyncError = c->PollAsyncError();
+    return HCCL_SUCCESS;
+}
+
+uint64_t HcclAmdIpcTimeoutMs(void) { return IpcTimeoutTicks() / 100000; }
 
 HcclResult HcclGetRankSize(HcclComm comm, uint32_t* rankSize)
 {

@@ -115,8 +115,75 @@ struct SrcPack {
     const void* p[HCCL_AMD_IR_MAX_SRC];
 };
 
+// Vector body of operand j (16-B vectors from the first aligned element).
+template <class E>
+__device__ __forceinline__ const u32x4* VecSrc(const SrcPack& srcs, int j, const Edges& edges)
+{
+    return reinterpret_cast<const u32x4*>(static_cast<const typename E::S*>(srcs.p[j]) + edges.head);
+}
+
+// Fold of one tile (U vectors per lane at base, base + kBlock, ...) over the operands, in operand order.
+// MODE 0 (serial): operand j+1 is loaded once operand j is folded, so a wave has U vectors of loads in flight.
+// MODE 1 (prefetch): operand j+1's loads are issued before operand j is folded (a register double buffer), so a wave
+// keeps 2U vectors in flight across the whole operand loop. The fold order (acc = x_j (op) acc) is the same.
+// NS > 0: the operand count is a compile-time constant and every operand's loads of the tile are issued before the
+// first combine (NS * U vectors in flight).
+template <class E, int OP, int U, int NT, int MODE, int NS>
+__device__ __forceinline__ void FoldTile(u32x4 (&acc)[U], const SrcPack& srcs, int nsrc, const Edges& edges,
+                                         uint64_t base)
+{
+    if constexpr (NS > 0) {
+        u32x4 v[NS][U];
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            const u32x4* pj = VecSrc<E>(srcs, j, edges);
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[j][u] = ld<NT>(pj + base + u * kBlock);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] = v[0][u];
+#pragma unroll
+        for (int j = 1; j < NS; ++j) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc[u] = combine<E, OP>(v[j][u], acc[u]);
+        }
+    } else if constexpr (MODE == 1) {
+        u32x4 nxt[U];
+        const u32x4* p0 = VecSrc<E>(srcs, 0, edges);
+        const u32x4* p1 = VecSrc<E>(srcs, 1, edges);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] = ld<NT>(p0 + base + u * kBlock);
+#pragma unroll
+        for (int u = 0; u < U; ++u) nxt[u] = ld<NT>(p1 + base + u * kBlock);
+        for (int j = 1; j < nsrc; ++j) {
+            u32x4 cur[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+            if (j + 1 < nsrc) {
+                const u32x4* pn = VecSrc<E>(srcs, j + 1, edges);
+#pragma unroll
+                for (int u = 0; u < U; ++u) nxt[u] = ld<NT>(pn + base + u * kBlock);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc[u] = combine<E, OP>(cur[u], acc[u]);
+        }
+    } else {
+        const u32x4* p0 = VecSrc<E>(srcs, 0, edges);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] = ld<NT>(p0 + base + u * kBlock);
+        for (int j = 1; j < nsrc; ++j) {
+            const u32x4* pj = VecSrc<E>(srcs, j, edges);
+            u32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = ld<NT>(pj + base + u * kBlock);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc[u] = combine<E, OP>(v[u], acc[u]);
+        }
+    }
+}
+
 // One ordered fold over `nvec` 16-B vectors (plus scalar edges), worked by `nblocks` workgroups, this one `bid`.
-template <class E, int OP, int U, int NT>
+template <class E, int OP, int U, int NT, int MODE = 0, int NS = 0>
 __device__ __forceinline__ void ReduceNBody(typename E::S* out, const SrcPack& srcs, int nsrc, uint64_t nvec,
                                             Edges edges, uint32_t bid, uint32_t nblocks)
 {
@@ -127,23 +194,7 @@ __device__ __forceinline__ void ReduceNBody(typename E::S* out, const SrcPack& s
     for (uint64_t t = bid; t < fullTiles; t += nblocks) {
         const uint64_t base = t * kTile + threadIdx.x;
         u32x4 acc[U];
-        const u32x4* p0 = reinterpret_cast<const u32x4*>(static_cast<const S*>(srcs.p[0]) + edges.head);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            acc[u] = ld<NT>(p0 + base + u * kBlock);
-        }
-        for (int j = 1; j < nsrc; ++j) {
-            const u32x4* pj = reinterpret_cast<const u32x4*>(static_cast<const S*>(srcs.p[j]) + edges.head);
-            u32x4 v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                v[u] = ld<NT>(pj + base + u * kBlock);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                acc[u] = combine<E, OP>(v[u], acc[u]);
-            }
-        }
+        FoldTile<E, OP, U, NT, MODE, NS>(acc, srcs, nsrc, edges, base);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             st<NT>(vout + base + u * kBlock, acc[u]);
@@ -179,11 +230,11 @@ __device__ __forceinline__ void ReduceNBody(typename E::S* out, const SrcPack& s
     }
 }
 
-template <class E, int OP, int U, int NT>
+template <class E, int OP, int U, int NT, int MODE = 0, int NS = 0>
 __global__ __launch_bounds__(kBlock) void k_reduceN(typename E::S* out, SrcPack srcs, int nsrc, uint64_t nvec,
                                                       Edges edges)
 {
-    ReduceNBody<E, OP, U, NT>(out, srcs, nsrc, nvec, edges, blockIdx.x, gridDim.x);
+    ReduceNBody<E, OP, U, NT, MODE, NS>(out, srcs, nsrc, nvec, edges, blockIdx.x, gridDim.x);
 }
 
 // A batch of independent folds: segment blockIdx.y, worked by the gridDim.x workgroups of its row.
@@ -234,6 +285,7 @@ std::atomic<uint32_t> g_blocksPerCu{0};
 std::atomic<uint32_t> g_unroll{0};
 std::atomic<uint32_t> g_policy{0};
 std::atomic<uint32_t> g_order{0};
+std::atomic<uint32_t> g_foldMode{0};  // n-ary fold operand pipelining: 0 default, 1 serial, 2 prefetch, 3 fixed n
 
 // Defaults from the interleaved launch sweep on MI355X (tools/sweep_local.py): the HBM stream
 // peaks with ~16 KiB of loads in flight per CU (2 workgroups x 256 lanes x 2 operands x 16 B) and nt loads+stores;
@@ -320,14 +372,34 @@ hipError_t Run2Variant(void* out, const void* src, const void* dst, uint64_t nve
     return hipGetLastError();
 }
 
-template <class E, int OP, int U, int NT>
+template <class E, int OP, int U, int NT, int MODE = 0, int NS = 0>
 hipError_t RunNVariant(void* out, const SrcPack& pk, int n, uint64_t nvec, Edges edges, uint32_t grid,
                        hipStream_t stream)
 {
     using S = typename E::S;
-    hipLaunchKernelGGL((k_reduceN<E, OP, U, NT>), dim3(grid), dim3(kBlock), 0, stream, static_cast<S*>(out), pk, n,
-                       nvec, edges);
+    hipLaunchKernelGGL((k_reduceN<E, OP, U, NT, MODE, NS>), dim3(grid), dim3(kBlock), 0, stream, static_cast<S*>(out),
+                       pk, n, nvec, edges);
     return hipGetLastError();
+}
+
+// Operand pipelining variants of the fold (FoldTile): FM 1 serial, 2 prefetch, 3 compile-time operand count (n = 3..8;
+// larger n takes the prefetch form).
+template <class E, int OP, int U, int FM>
+hipError_t RunNMode(void* out, const SrcPack& pk, int n, uint64_t nvec, Edges edges, uint32_t grid, hipStream_t stream)
+{
+    if constexpr (FM == 3) {
+        switch (n) {
+            case 3: return RunNVariant<E, OP, U, 3, 0, 3>(out, pk, n, nvec, edges, grid, stream);
+            case 4: return RunNVariant<E, OP, U, 3, 0, 4>(out, pk, n, nvec, edges, grid, stream);
+            case 5: return RunNVariant<E, OP, U, 3, 0, 5>(out, pk, n, nvec, edges, grid, stream);
+            case 6: return RunNVariant<E, OP, U, 3, 0, 6>(out, pk, n, nvec, edges, grid, stream);
+            case 7: return RunNVariant<E, OP, U, 3, 0, 7>(out, pk, n, nvec, edges, grid, stream);
+            case 8: return RunNVariant<E, OP, U, 3, 0, 8>(out, pk, n, nvec, edges, grid, stream);
+            default: return RunNVariant<E, OP, U, 3, 1, 0>(out, pk, n, nvec, edges, grid, stream);
+        }
+    } else {
+        return RunNVariant<E, OP, U, 3, FM == 2 ? 1 : 0, 0>(out, pk, n, nvec, edges, grid, stream);
+    }
 }
 
 // fp32 SUM (the headline path) carries every tuning variant; other (dtype, op) pairs are built at the default.
@@ -399,6 +471,18 @@ hipError_t RunN(void* out, const void* const* srcs, uint32_t n, uint64_t count, 
     }
     if constexpr (kTunable<E, OP>) {
         uint32_t grid = GridFor(nvec, kBlock * cfg.unroll, cfg);
+        const uint32_t fm = g_foldMode.load(std::memory_order_relaxed);
+        if (fm >= 2 && cfg.nt == 3) {
+            switch (cfg.unroll * 4 + fm) {
+                case 4 + 2: return RunNMode<E, OP, 1, 2>(out, pk, int(n), nvec, edges, grid, stream);
+                case 4 + 3: return RunNMode<E, OP, 1, 3>(out, pk, int(n), nvec, edges, grid, stream);
+                case 8 + 2: return RunNMode<E, OP, 2, 2>(out, pk, int(n), nvec, edges, grid, stream);
+                case 8 + 3: return RunNMode<E, OP, 2, 3>(out, pk, int(n), nvec, edges, grid, stream);
+                case 16 + 2: return RunNMode<E, OP, 4, 2>(out, pk, int(n), nvec, edges, grid, stream);
+                case 16 + 3: return RunNMode<E, OP, 4, 3>(out, pk, int(n), nvec, edges, grid, stream);
+                default: return hipErrorInvalidValue;
+            }
+        }
         switch (cfg.unroll * 4 + cfg.nt) {
             case 4 + 0: return RunNVariant<E, OP, 1, 0>(out, pk, int(n), nvec, edges, grid, stream);
             case 4 + 3: return RunNVariant<E, OP, 1, 3>(out, pk, int(n), nvec, edges, grid, stream);
@@ -469,6 +553,13 @@ HcclResult SetReduceLaunch(uint32_t blocksPerCu, uint32_t unroll, uint32_t cache
         g_policy.store(cachePolicy);
         g_order.store(cachePolicy == 0 ? 0 : 1);
     }
+    return HCCL_SUCCESS;
+}
+
+HcclResult SetFoldMode(uint32_t mode)
+{
+    if (mode > 3) return HCCL_E_PARA;
+    g_foldMode.store(mode);
     return HCCL_SUCCESS;
 }
 

@@ -61,6 +61,12 @@ extern HcclResult HcclCommInitAll(uint32_t ndev, int32_t* devices, HcclComm* com
 extern HcclResult HcclCommDestroy(HcclComm comm);
 extern HcclResult HcclGetRankSize(HcclComm comm, uint32_t* rankSize);
 extern HcclResult HcclGetRankId(HcclComm comm, uint32_t* rank);
+/* Asynchronous error of the communicator (CANN hccl_comm.h; polled by framework watchdogs such as torch_npu's
+ * ProcessGroupHCCL). Non-blocking. *asyncError = HCCL_E_TIMEOUT after a one-sided barrier wait exceeded its bound
+ * (HCCL_EXEC_TIMEOUT), the transport's error after an RCCL asynchronous failure, else HCCL_SUCCESS. Once the first
+ * collective entry has observed such an error (and returned it), every later collective on the communicator returns
+ * HCCL_E_SUSPENDING: the reference's status gate, src/ops/op_common/op_common.cc:89-97. */
+extern HcclResult HcclGetCommAsyncError(HcclComm comm, HcclResult* asyncError);
 
 #ifdef __cplusplus
 }

@@ -50,6 +50,11 @@ extern HcclResult HcclAmdLocalReduceN(void* out, const void* const* srcs, uint32
  * 5 = nt loads + stores with contiguous per-workgroup tile runs. */
 extern HcclResult HcclAmdSetReduceLaunch(uint32_t blocksPerCu, uint32_t unroll, uint32_t cachePolicy);
 
+/* Operand pipelining of the ordered n-ary fold (process-wide, tuning): 0 = default, 1 = serial (operand j+1 loaded
+ * after operand j is folded), 2 = prefetch (operand j+1 loaded before operand j is folded), 3 = every operand of a tile
+ * loaded before the first combine (compile-time operand count, 3..8). The fold order is the same in every mode. */
+extern HcclResult HcclAmdSetFoldMode(uint32_t mode);
+
 /* Byte size of one element of dataType, 0 if unknown (DATATYPE_SIZE_TABLE, alg_param.h:43-61). */
 extern uint32_t HcclAmdDataTypeSize(HcclDataType dataType);
 
@@ -154,6 +159,11 @@ extern int32_t HcclAmdCommLastAlgo(HcclComm comm);
  * failed, as after an asynchronous error). Bits 8-15: bit length of the longest barrier wait of the last IPC
  * AllReduce, in polls (diagnostic; 0 = no block ever waited). */
 extern HcclResult HcclAmdCommIpcStatus(HcclComm comm, uint32_t* status);
+
+/* The barrier wait bound of the one-sided kernel in ms, as the next IPC call would take it from the environment:
+ * HCCL_AMD_IPC_TIMEOUT_MS if set (1 .. 3600000), else HCCL_EXEC_TIMEOUT by the reference's AIV-mode rule (seconds,
+ * at most two decimals; 0, above 1091 or unset = 1091 s). A wait past it fails the communicator (HcclGetCommAsyncError). */
+extern uint64_t HcclAmdIpcTimeoutMs(void);
 
 /* Parse and validate a rank table (as HcclCommInitClusterInfo does): *nRanks = number of ranks, *deviceId = the
  * device_id of `rank`. HCCL_E_PARA for a malformed table or a rank outside it. */

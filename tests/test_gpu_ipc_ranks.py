@@ -204,7 +204,9 @@ def test_ipc_collectives_rank_mode(n):
 
 
 def _lost_peer_main(rank, port, q):
-    os.environ["HCCL_AMD_IPC_TIMEOUT_MS"] = "1500"
+    # the bound comes from the reference's own variable (AIV-mode rule: seconds, two decimals)
+    os.environ.pop("HCCL_AMD_IPC_TIMEOUT_MS", None)
+    os.environ["HCCL_EXEC_TIMEOUT"] = "1.5"
     os.makedirs("gpurun_out", exist_ok=True)
     progress = open(f"gpurun_out/ipc_lost_peer_r{rank}.log", "w", buffering=1)
     try:
@@ -220,6 +222,13 @@ def _lost_peer_main(rank, port, q):
             dist.all_gather_object(out, b)
             return out
 
+        def code_of(fn):
+            try:
+                fn()
+                return 0
+            except H.HcclError as e:
+                return e.code
+
         comm = H.comm_init_host_exchange(2, rank, all_gather)
         stream = torch.cuda.Stream()
         x = torch.full((1 << 20,), float(rank + 1), device="cuda")
@@ -227,20 +236,27 @@ def _lost_peer_main(rank, port, q):
         torch.cuda.synchronize()
         comm.all_reduce(x, y, H.HcclReduceOp.SUM, stream=stream)  # both ranks: set-up + a good call
         stream.synchronize()
-        res = {"first_status": comm.ipc_status(), "first_ok": bool(torch.all(y == 3.0).item())}
+        res = {"first_status": comm.ipc_status(), "first_ok": bool(torch.all(y == 3.0).item()),
+               "first_async": comm.async_error(), "timeout_ms": H.lib.HcclAmdIpcTimeoutMs()}
         progress.write(f"first {res}\n")
         dist.barrier()
         if rank == 0:  # rank 1 never joins this call
             t0 = time.time()
-            comm.all_reduce(x, y, H.HcclReduceOp.SUM, stream=stream)
+            comm.all_reduce(x, y, H.HcclReduceOp.SUM, stream=stream)  # enqueued: returns before the wait
+            res["lost_rc"] = 0
             stream.synchronize()
             res["lost_s"] = time.time() - t0
             res["lost_status"] = comm.ipc_status()
+            res["async_after_lost"] = comm.async_error()
+            # the next entry observes the failure and returns it; every later one finds the communicator failed
             t0 = time.time()
-            comm.all_reduce(x, y, H.HcclReduceOp.SUM, stream=stream)  # sticky: returns without waiting
+            res["next_rc"] = code_of(lambda: comm.all_reduce(x, y, H.HcclReduceOp.SUM, stream=stream))
+            res["then_rc"] = code_of(lambda: comm.all_reduce(x, y, H.HcclReduceOp.SUM, stream=stream))
+            res["rs_rc"] = code_of(lambda: comm.reduce_scatter(x, y[: x.numel() // 2], H.HcclReduceOp.SUM,
+                                                              stream=stream))
             stream.synchronize()
             res["after_s"] = time.time() - t0
-            res["after_status"] = comm.ipc_status()
+            res["async_later"] = comm.async_error()
             progress.write(f"lost {res}\n")
         dist.barrier()
         comm.destroy()
@@ -252,9 +268,11 @@ def _lost_peer_main(rank, port, q):
         time.sleep(10)
 
 
-def test_ipc_lost_peer_times_out_and_sticks():
-    """A peer that never joins: the barrier gives up after HCCL_AMD_IPC_TIMEOUT_MS with status bit 0 (no hang), the
-    communicator stays failed (the next call returns at once with the bit still set), teardown still completes."""
+def test_ipc_lost_peer_fails_the_communicator():
+    """A peer that never joins: the barrier gives up after HCCL_EXEC_TIMEOUT (no hang); the next collective returns
+    HCCL_E_TIMEOUT, every later one HCCL_E_SUSPENDING (the reference's status gate, op_common.cc:89-97), and
+    HcclGetCommAsyncError reports HCCL_E_TIMEOUT without a device synchronisation; teardown still completes."""
+    import hccl_amd as H
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -273,13 +291,18 @@ def test_ipc_lost_peer_times_out_and_sticks():
                 p.kill()
     for r in range(2):
         assert got[r][0] == "ok", f"rank {r}:\n{got[r][0]}"
-        assert got[r][1]["first_ok"] and got[r][1]["first_status"] & 1 == 0
+        res = got[r][1]
+        assert res["first_ok"] and res["first_status"] & 1 == 0 and res["first_async"] == 0, res
+        assert res["timeout_ms"] == 1500, res
     r0 = got[0][1]
+    assert r0["lost_rc"] == 0  # stream-ordered: the call that enqueued the lost barrier had already returned
     assert r0["lost_status"] & 1 == 1
     # bits 8+: bit length of the call's longest wait in polls (~100 ns each): a 1.5 s wait is millions of polls
     assert (r0["lost_status"] >> 8) >= 16, hex(r0["lost_status"])
     assert 1.0 < r0["lost_s"] < 15.0, r0
-    assert r0["after_status"] & 1 == 1
-    # the next call returns before any barrier, so it has no wait of its own (the diagnostic is per call)
-    assert (r0["after_status"] >> 8) == 0, hex(r0["after_status"])
-    assert r0["after_s"] < 1.0, r0
+    assert r0["async_after_lost"] == H.HcclResult.HCCL_E_TIMEOUT, r0
+    assert r0["next_rc"] == H.HcclResult.HCCL_E_TIMEOUT, r0
+    assert r0["then_rc"] == H.HcclResult.HCCL_E_SUSPENDING, r0
+    assert r0["rs_rc"] == H.HcclResult.HCCL_E_SUSPENDING, r0
+    assert r0["async_later"] == H.HcclResult.HCCL_E_TIMEOUT, r0
+    assert r0["after_s"] < 1.0, r0  # the gate enqueues nothing

@@ -37,14 +37,26 @@ class Violation(AssertionError):
     pass
 
 
-def _run(n, launches, seed, alternate=True, max_steps=200000):
+M32 = 1 << 32
+
+
+def _run(n, launches, seed, alternate=True, max_steps=200000, epoch_base=0, wrap_safe=True):
+    """epoch_base: value of the device epoch counter (and of every flag) before the first launch; the kernel's 32-bit
+    epochs are taken modulo 2^32, so a base near 2^32 runs the barriers across the wrap. wrap_safe: the kernel's
+    `(int32_t)(flag - epoch) < 0` wait; False models a plain unsigned `flag < epoch`."""
     rng = random.Random(seed)
     cap = 16  # elements per slot in every area
     areas = ("in", "res", "alt0", "alt1")
     # tag[owner][area][slot][elem] = (global round id, writer rank); readers[...] = reads in progress
     tag = {(o, a, q, x): None for o in range(n) for a in areas for q in range(n) for x in range(cap)}
     readers = {k: 0 for k in tag}
-    flags = {}  # (owner, block, sender) -> epoch
+    flags = {}  # (owner, block, sender) -> last stored epoch, modulo 2^32
+
+    def behind(flag, ep):
+        if wrap_safe:
+            d = (flag - ep) % M32
+            return d >= (1 << 31)  # (int32_t)(flag - ep) < 0
+        return flag < ep
 
     def store(owner, area, slot, lo, hi, val):
         for x in range(lo, hi):
@@ -136,10 +148,10 @@ def _run(n, launches, seed, alternate=True, max_steps=200000):
                 if (me, b, ep) not in signalled:  # the barrier's release store to every rank's flag
                     signalled.add((me, b, ep))
                     for c in range(n):
-                        flags[(c, b, me)] = max(flags.get((c, b, me), 0), ep)
+                        flags[(c, b, me)] = (epoch_base + ep) % M32  # a block signals its epochs in order
                     progressed = True
                     break
-                if not all(flags.get((me, b, c), 0) >= ep for c in range(n)):
+                if any(behind(flags.get((me, b, c), epoch_base % M32), (epoch_base + ep) % M32) for c in range(n)):
                     continue  # still waiting: try another block
             elif step[0] == "store":
                 store(*step[1:])
@@ -169,6 +181,28 @@ def test_single_barrier_without_alternation_races():
         rng = random.Random(seed)
         try:
             _run(3, [(SINGLE, 3, 2, 8)] + _launches(rng, 3), seed, alternate=False)
+        except Violation:
+            found += 1
+    assert found > 0
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_protocol_is_race_free_across_epoch_wrap(n):
+    """The epoch counter never resets: 2^31 two-shot calls wrap it. Starting just below 2^32, every barrier of the
+    launches below crosses the wrap; the wrap-safe compare keeps the protocol exact."""
+    for seed in range(40):
+        rng = random.Random(7000 * n + seed)
+        _run(n, _launches(rng, 6), seed, epoch_base=M32 - 5)
+
+
+def test_unsigned_compare_breaks_at_the_wrap():
+    """Negative control: with `flag < epoch` a barrier after the wrap opens without waiting."""
+    found = 0
+    for seed in range(100):
+        rng = random.Random(seed)
+        try:
+            _run(3, [(SINGLE, 3, 2, 8), (DOUBLE, 3, 2, 8)] + _launches(rng, 2), seed, epoch_base=M32 - 3,
+                 wrap_safe=False)
         except Violation:
             found += 1
     assert found > 0

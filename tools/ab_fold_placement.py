@@ -14,7 +14,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import hccl_amd as H  # noqa: E402
 
 GIB = 1 << 30
-SHAPES = [tuple(int(v) for v in x.split("x")) for x in os.environ.get("AB_SHAPES", "2x2,2x4,4x2,2x1").split(",")]
+# bpc x unroll [x fold mode]: HcclAmdSetFoldMode (0 default, 1 serial, 2 prefetch, 3 every operand first)
+SHAPES = [tuple(int(v) for v in (x + "x0").split("x")[:3]) if x.count("x") == 1 else tuple(int(v) for v in x.split("x"))
+          for x in os.environ.get("AB_SHAPES", "2x2,2x4,4x2,2x1").split(",")]
 NS = tuple(int(x) for x in os.environ.get("AB_NS", "8").split(","))
 TRIALS = int(os.environ.get("AB_TRIALS", "12"))
 POOL = int(os.environ.get("AB_POOL", "20"))
@@ -37,20 +39,31 @@ def main():
     pool = [torch.empty(GIB // 4, dtype=torch.float32, device="cuda").uniform_() for _ in range(POOL)]
     rng = random.Random(7)
     res = {}
+    mismatch = set()
     for n in NS:
         for _ in range(TRIALS):
             pick = rng.sample(range(POOL), n + 1)
             ins, out = [pool[i] for i in pick[:n]], pool[pick[n]]
             order = SHAPES[:]
             rng.shuffle(order)
-            for bpc, u in order:
+            ref = None
+            for bpc, u, fm in order:
                 H.set_reduce_launch(bpc, u, 0)
-                res.setdefault((n, bpc, u), []).append(timeit(lambda: H.local_reduce_n(out, ins)))
+                H.set_fold_mode(fm)
+                res.setdefault((n, bpc, u, fm), []).append(timeit(lambda: H.local_reduce_n(out, ins)))
+                # every shape and mode folds in the same order: the outputs must be identical bits
+                digest = out.view(torch.int32)[:: 1 << 10].clone()
+                if ref is None:
+                    ref = digest
+                elif not torch.equal(ref, digest):
+                    mismatch.add((n, bpc, u, fm))
     H.set_reduce_launch(0, 0, 0)
-    for (n, bpc, u), ts in sorted(res.items()):
+    H.set_fold_mode(0)
+    for (n, bpc, u, fm), ts in sorted(res.items()):
         ts = sorted(ts)
         med = ts[len(ts) // 2]
-        print(json.dumps({"n": n, "blocks_per_cu": bpc, "unroll": u, "median_us": round(med * 1e6, 1),
+        print(json.dumps({"n": n, "blocks_per_cu": bpc, "unroll": u, "fold_mode": fm,
+                          "bits_match": (n, bpc, u, fm) not in mismatch, "median_us": round(med * 1e6, 1),
                           "min_us": round(ts[0] * 1e6, 1), "max_us": round(ts[-1] * 1e6, 1),
                           "mean_us": round(sum(ts) / len(ts) * 1e6, 1),
                           "median_GBps": round((n + 1) * GIB / med / 1e9, 1)}), flush=True)
