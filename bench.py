@@ -10,6 +10,8 @@ Metric (BASELINE.json): "device-resident reduce GiB/s (fp32 sum) vs HBM peak; ri
   N > 1  (torchrun, one process per GPU): config C3 — HcclAllReduce fp32 SUM, 4 GiB per rank, over the RCCL
          communicator built from HcclGetRootInfo / HcclCommInitRootInfo. A step = one AllReduce.
          value = whole-job reduced input GiB/s = N x 4 GiB x K / max-over-ranks time; bus GB/s is reported beside it.
+         The headline schedule is the ring (BASELINE.json's "ring all-reduce"): HCCL_AMD_ALGO_RING, 7 arc-disjoint
+         rings at n = 8; the reference's own selection (MeshChunk) and the other families are extra rows.
 
 Every run prints exactly one JSON line on rank 0 (extra diagnostics go to stderr).
 """
@@ -230,6 +232,13 @@ def bench_local(args) -> dict:
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     per = [evs[k].elapsed_time(evs[k + 1]) / 1e3 for k in range(args.steps)]
+    # the measured kernel on the measured buffers, once more after the timed region: dst' = src + dst must be the
+    # IEEE sum torch computes elementwise (same bits: one correctly rounded add per element)
+    before = dst.clone()
+    H.local_reduce(dst, src, H.HcclReduceOp.SUM, stream)
+    torch.cuda.synchronize()
+    result_ok = bool(torch.equal(dst, torch.add(src, before)))
+    del before
     total = evs[0].elapsed_time(evs[-1]) / 1e3
     bytes_step = 3 * C2_COUNT * 4
     value = bytes_step * args.steps / total / GIB
@@ -250,6 +259,7 @@ def bench_local(args) -> dict:
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic (uniform [-1,1) fp32, device-generated)",
+        "result_ok": result_ok,
         "config": {
             "workload": "C2: 1-GPU local reduce dst = src + dst (HcclAmdLocalReduce), 2 x 1 GiB fp32 in HBM",
             "count": C2_COUNT,
@@ -650,8 +660,11 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     g = torch.Generator(device=dev).manual_seed(0x5EED0003 + rank)
     send = torch.rand(count, device=dev, generator=g).mul_(2).sub_(1)
     recv = torch.empty_like(send)
-    if args.algo:
-        comm.set_algo(H.Algo[args.algo.upper()])
+    # C3 as BASELINE.json names it: the ring AllReduce (7 arc-disjoint rings over every xGMI link at n = 8). The
+    # reference's own selection at this size (MeshChunk, order O6) and every other family run beside it in
+    # other_configs.c3_schedules.
+    headline = H.Algo[(args.algo or "ring").upper()]
+    comm.set_algo(headline)
     stream = torch.cuda.current_stream()
     for _ in range(args.warmup):
         comm.all_reduce(send, recv, H.HcclReduceOp.SUM, stream)
@@ -687,11 +700,12 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
             except Exception as e:  # noqa: BLE001  (a secondary config never hides the headline line)
                 extra[name] = {"error": f"{type(e).__name__}: {e}"}
     # correctness of the measured path at the measured size: integer-valued inputs make every order exact, so the
-    # auto AllReduce must return exactly sum_r((i % 251) + r) on every rank (checked on the GPU, AND over ranks)
+    # timed schedule must return exactly sum_r((i % 251) + r) on every rank (checked on the GPU, AND over ranks)
     check = torch.arange(count, device=dev, dtype=torch.int64) % 251
     send.copy_(check + rank)
-    comm.set_algo(H.Algo.AUTO)
+    comm.set_algo(headline)
     comm.all_reduce(send, recv, H.HcclReduceOp.SUM, stream)
+    verified_algo = H.Algo(comm.last_algo).name
     torch.cuda.synchronize()
     ok = torch.tensor([1 if torch.equal(recv, (check * world + world * (world - 1) // 2).to(recv.dtype)) else 0])
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
@@ -725,6 +739,7 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
         "busbw_GBps": round(busbw, 2),
         "algbw_GBps": round(algbw, 2),
         "result_ok": result_ok,
+        "result_ok_algorithm": verified_algo,
         "rccl_allreduce_reference": rccl_ref,
         "other_configs": extra,
         "roofline": {
@@ -757,7 +772,8 @@ def main():
     p.add_argument("--no-rccl-ref", action="store_true", help="N>1: skip timing RCCL's own all_reduce beside ours")
     p.add_argument("--no-extra-configs", action="store_true", help="N>1: skip the C4 (RS+AG) and C5 (RHD sweep) lines")
     p.add_argument("--cpu-budget", type=float, default=12.0)
-    p.add_argument("--algo", default="", help="force an AllReduce schedule (mesh_oneshot/mesh_twoshot/ring/rhd)")
+    p.add_argument("--algo", default="", help="N>1: the headline AllReduce schedule (default ring; mesh_chunk is the "
+                                              "reference's own selection at 4 GiB, auto, rhd, ipc ...)")
     args = p.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:

@@ -353,6 +353,11 @@ HcclResult ExchangeUniqueId(const std::string& host, uint16_t port, uint32_t n, 
             close(ls);
             return HCCL_E_TCP_CONNECT;
         }
+        // Ranks are counted once each (a rank that retries after a short read is served again, not counted twice),
+        // and each connection gets a short deadline of its own, so a stray client that connects and sends nothing
+        // holds the accept loop for 2 s, not until HCCL_CONNECT_TIMEOUT.
+        std::vector<bool> done(n, false);
+        done[0] = true;
         uint32_t served = 0;
         HcclResult r = HCCL_SUCCESS;
         while (served + 1 < n) {
@@ -367,9 +372,11 @@ HcclResult ExchangeUniqueId(const std::string& host, uint16_t port, uint32_t n, 
             if (poll(&pf, 1, static_cast<int>(std::min<long long>(left.count(), 1000))) <= 0) continue;
             const int cs = accept(ls, nullptr, nullptr);
             if (cs < 0) continue;
+            const auto connDeadline = std::min(deadline, std::chrono::steady_clock::now() + std::chrono::seconds(2));
             uint32_t hello[2] = {0, 0};
-            if (FullIo(cs, hello, sizeof hello, false, deadline) && hello[0] == kHelloMagic && hello[1] < n &&
-                hello[1] != 0 && FullIo(cs, id, 128, true, deadline)) {
+            if (FullIo(cs, hello, sizeof hello, false, connDeadline) && hello[0] == kHelloMagic && hello[1] < n &&
+                hello[1] != 0 && FullIo(cs, id, 128, true, connDeadline) && !done[hello[1]]) {
+                done[hello[1]] = true;
                 ++served;
             }
             close(cs);

@@ -246,6 +246,7 @@ public:
     // host all-gather among the rank threads (generation-counted so that back-to-back exchanges cannot mix)
     std::vector<std::vector<char>> slots_;
     std::vector<char> result_;
+    bool resultOk_ = false;
     uint32_t arrived_ = 0;
     uint64_t generation_ = 0;
 
@@ -255,17 +256,23 @@ public:
         const uint64_t gen = generation_;
         slots_[rank].assign(static_cast<const char*>(mine), static_cast<const char*>(mine) + bytes);
         if (++arrived_ == n_) {
+            // The last arrival completes the generation whatever happens, so no rank of this exchange is left
+            // counted in the next one; a size mismatch fails every rank of the generation alike.
             result_.clear();
+            bool sameSize = true;
             for (auto& s : slots_) {
-                if (s.size() != bytes) return HCCL_E_INTERNAL;
+                sameSize = sameSize && s.size() == bytes;
                 result_.insert(result_.end(), s.begin(), s.end());
             }
+            resultOk_ = sameSize;
             arrived_ = 0;
             generation_++;
             cv_.notify_all();
         } else if (!cv_.wait_for(lk, std::chrono::seconds(600), [&] { return generation_ != gen; })) {
+            --arrived_;  // withdraw: a later exchange must not count this rank as arrived
             return HCCL_E_TIMEOUT;
         }
+        if (!resultOk_ || result_.size() != bytes * n_) return HCCL_E_INTERNAL;
         std::memcpy(all, result_.data(), bytes * n_);
         return HCCL_SUCCESS;
     }

@@ -368,8 +368,9 @@ def test_fp32_sum(worlds, op_type, algo, n, count, streams, monkeypatch):
 @pytest.mark.parametrize("dtype", [O.INT8, O.INT16, O.INT32, O.INT64, O.UINT64, O.FP16, O.BFP16, O.FP64],
                          ids=lambda v: O.DTYPE_NAMES[v])
 @pytest.mark.parametrize("op", O.OPS, ids=lambda v: O.OP_NAMES[v])
-@pytest.mark.parametrize("op_type,algo", [(AR, 1), (AR, 2), (AR, 3), (AR, 5), (AR, 7), (AR, 8), (AR, 9), (RS, 1),
-                                          (RS, 5), (RS, 7), (RS, 8), (RS, 9), (RED, 2), (RED, 5), (RED, 7), (RED, 9)])
+@pytest.mark.parametrize("op_type,algo", [(AR, 1), (AR, 2), (AR, 3), (AR, 4), (AR, 5), (AR, 6), (AR, 7), (AR, 8),
+                                          (AR, 9), (RS, 1), (RS, 5), (RS, 6), (RS, 7), (RS, 8), (RS, 9), (RED, 2),
+                                          (RED, 5), (RED, 7), (RED, 9)])
 def test_dtypes_ops(worlds, op_type, algo, dtype, op):
     n, count, root = 4, 40961, 2
     comms = worlds(n)
@@ -386,6 +387,25 @@ def test_dtypes_ops(worlds, op_type, algo, dtype, op):
         if op_type == RED and r != root:
             continue
         assert O.equal_bits(dtype, outs[r], want[r]), r
+
+
+@pytest.mark.parametrize("nbytes", [1 << 10, 64 << 10, 1 << 20, 16 << 20, 64 << 20])
+def test_c5_rhd_fp16_random_bit_exact(worlds, nbytes):
+    """C5's schedule and dtype (RHD, fp16 SUM, 8 ranks) on random data, where the association order decides the bits:
+    bit-exact against the oracle replaying the same IR and against the closed form (n-1 concurrent RHD instances,
+    each the classic pairwise halving on its virtual ranks), from 1 KiB to 64 MiB per rank."""
+    n, count = 8, nbytes // 2
+    comms = worlds(n)
+    xs = [O.random_operands(O.FP16, count, seed=900 + r, edge=False) for r in range(n)]
+    used, outs = collective(comms, AR, R.ALGO_RHD, O.FP16, O.SUM, xs, count)
+    assert used == R.ALGO_RHD
+    want_ir = oracle_replay(AR, R.ALGO_RHD, n, count, O.FP16, O.SUM, xs, 0, 0)
+    for r in range(n):
+        assert O.equal_bits(O.FP16, outs[r], want_ir[r]), ("vs IR replay", r)
+    if nbytes <= (1 << 20):  # the numpy closed form is slow at the larger sizes; the IR replay covers them
+        want_cf = R.expected(AR, R.ALGO_RHD, O.FP16, O.SUM, xs, count)
+        for r in range(n):
+            assert O.equal_bits(O.FP16, outs[r], want_cf[r]), ("vs closed form", r)
 
 
 @pytest.mark.parametrize("algo", [1, 2, 3, 4, 5, 6, 7, 8])

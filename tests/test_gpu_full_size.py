@@ -81,6 +81,52 @@ def test_c3_full_size_two_shot_bit_exact_random(world, algo):
     del xs, outs, want
 
 
+def _bounds(count, parts, es=4):
+    """tests/sched_ref.py chunk_bounds: ceil split rounded up to 128 B."""
+    align = 128 // es
+    sc = -(-count // parts)
+    sc = -(-sc // align) * align
+    return [(min(count, c * sc), min(count, c * sc + sc)) for c in range(parts)]
+
+
+def test_c3_full_size_ring_bit_exact_random(world):
+    """C3 as BASELINE.json names it: the ring AllReduce, 8 ranks x 4 GiB fp32, random data. The schedule runs the 7
+    arc-disjoint rings of HcclAmdRingTable(8) at once, part k of the buffer on ring k; the chunk at ring position c
+    ends as acc = x_{cyc[c+1]}, then acc = acc + x_{cyc[c+j]} for j = 2 .. n (tests/sched_ref.py allreduce_ring).
+    The same IEEE fp32 adds in the same order are done by torch on the GPU: the outputs must be identical bits."""
+    count = (4 << 30) // 4
+    xs = []
+    for r in range(N):
+        g = torch.Generator(device="cuda").manual_seed(0xC3A + r)
+        xs.append(torch.rand(count, device="cuda", generator=g).mul_(2).sub_(1))
+    rings = H.ring_table(N)
+    assert len(rings) == N - 1
+    want = torch.empty(count, device="cuda")
+    for k, (pb, pe) in enumerate(_bounds(count, len(rings))):
+        cyc = rings[k]
+        for c, (b, e) in enumerate(_bounds(pe - pb, N)):
+            if e <= b:
+                continue
+            sl = slice(pb + b, pb + e)
+            acc = xs[cyc[(c + 1) % N]][sl].clone()
+            for j in range(2, N + 1):
+                acc.add_(xs[cyc[(c + j) % N]][sl])
+            want[sl] = acc
+    outs = [torch.empty(count, device="cuda") for _ in range(N)]
+    for c in world:
+        c.set_algo(H.Algo.RING)
+    try:
+        run_all(world, lambda r, s: world[r].all_reduce(xs[r], outs[r], H.HcclReduceOp.SUM, s))
+        assert world[0].last_algo == H.Algo.RING
+        for r in range(N):
+            bad = torch.count_nonzero(outs[r].view(torch.int32) != want.view(torch.int32)).item()
+            assert bad == 0, (r, bad)
+    finally:
+        for c in world:
+            c.set_algo(H.Algo.AUTO)
+    del xs, outs, want
+
+
 def test_c3_full_size_reference_selection_exact(world):
     count = (4 << 30) // 4
     xs = [pattern(count, r, torch.float32, 251) for r in range(N)]
