@@ -14,6 +14,7 @@ import torch
 
 from ._lib import (  # noqa: F401
     Algo,
+    AivVariant,
     HcclAmdIrOp,
     HcclDataType,
     HcclError,
@@ -124,6 +125,15 @@ def build_schedule(op_type: int, algo: int, n_ranks: int, rank: int, count: int,
 def select_algo(op_type: int, n_ranks: int, nbytes: int, special: bool = False) -> int:
     """The algorithm HCCL_AMD_ALGO_AUTO picks (HcclAmdSelectAlgo)."""
     return lib.HcclAmdSelectAlgo(int(op_type), n_ranks, nbytes, 1 if special else 0)
+
+
+def select_aiv_algo(op_type: int, n_ranks: int, count: int, dtype: int, op: int, core_limit: int = 0,
+                    strict: bool = False):
+    """(HcclAmdAivVariant, groupSize) the AIV engine takes (HcclAmdSelectAivAlgo); core_limit 0 = the default."""
+    g = ctypes.c_uint32(1)
+    v = lib.HcclAmdSelectAivAlgo(int(op_type), n_ranks, count, int(dtype), int(op), core_limit, 1 if strict else 0,
+                                 ctypes.byref(g))
+    return AivVariant(v), g.value
 
 
 def ring_table(n_ranks: int) -> List[List[int]]:

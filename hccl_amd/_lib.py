@@ -82,6 +82,16 @@ class Algo(enum.IntEnum):
     IPC_TWOSHOT = 7
     MESH_CHUNK = 8
     IPC = 9
+    AIV = 10
+
+
+class AivVariant(enum.IntEnum):
+    NOT_MATCHED = 0
+    AR_ONESHOT = 1
+    AR_TWOSHOT_LARGE = 2
+    AR_TWOSHOT_SMALL = 3
+    RS_BIGDATA = 4
+    RS_LOCAL_TREE = 5
 
 
 class OpType(enum.IntEnum):
@@ -149,6 +159,7 @@ SIGNATURES = {
     "HcclAmdDataTypeSize": (_u32, [_i32]),
     "HcclAmdGetErrorString": (ctypes.c_char_p, [_i32]),
     "HcclAmdSelectAlgo": (_i32, [_i32, _u32, _u64, _i32]),
+    "HcclAmdSelectAivAlgo": (_i32, [_i32, _u32, _u64, _i32, _i32, _u32, _i32, ctypes.POINTER(_u32)]),
     "HcclAmdRingTable": (_i32, [_u32, ctypes.POINTER(_u32), _u32]),
     "HcclAmdRhdTable": (_i32, [_u32, ctypes.POINTER(_u32), _u32]),
     "HcclAmdBuildSchedule": (

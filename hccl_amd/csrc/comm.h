@@ -99,6 +99,21 @@ struct Comm {
 // family).
 HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void* sendBuf, void* recvBuf,
                             uint64_t count, HcclDataType dt, HcclReduceOp op, uint32_t root, hipStream_t stream);
+// The same for an explicit plan (the AIV engine's variants, SelectAivPlan).
+HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* sendBuf, void* recvBuf, uint64_t count,
+                      HcclDataType dt, HcclReduceOp op, uint32_t root, hipStream_t stream);
+HcclResult IpcPlanForFamily(int32_t opType, int32_t family, uint32_t n, uint64_t es, uint64_t cclBytes, IpcPlan* pl);
+
+// The reference's AIV engine (HCCL_OP_EXPANSION_MODE=AIV): SelectAivAlgo's rules and the variant its kernel takes
+// for the vector-core count `coreLimit` (aivCoreLimit / the device's vector cores). Returns the variant
+// (HcclAmdAivVariant, include/hccl_amd.h), HCCL_AMD_AIV_NOT_MATCHED when the selector would fall back to the AICPU
+// engine; *plan receives the one-sided kernel's plan for a matched variant.
+int32_t SelectAivPlan(int32_t opType, uint32_t n, uint64_t count, HcclDataType dt, HcclReduceOp op, bool strict,
+                      uint64_t cclBytes, uint32_t coreLimit, IpcPlan* plan, uint32_t* group);
+// HCCL_AMD_AIV_CORE_LIMIT (default 48, MAX_NUM_BLOCKS of aiv_defines.h:35).
+uint32_t AivCoreLimit();
+// HCCL_OP_EXPANSION_MODE selects the AIV engine ("AIV").
+bool ExpansionModeAiv();
 // Collective: every rank's IPC kernels have finished before any rank unmaps or frees (called by ~Comm).
 void IpcQuiesce(Comm& c);
 void IpcRelease(Comm& c);

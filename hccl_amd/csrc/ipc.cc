@@ -210,11 +210,196 @@ uint32_t DefaultIpcBlocks(uint64_t bytes)
     return kIpcMaxBlocks;
 }
 
+// ------------------------------------------------------------------------------------------------ plans
+
+namespace {
+
+uint64_t LoopElems(uint64_t loopBytes, uint64_t es) { return std::max<uint64_t>(1, loopBytes / es); }
+
+uint64_t RoundDown128(uint64_t b) { return b / 128 * 128; }
+
+constexpr uint64_t kUbMaxDataSize = 256ull << 20;  // UB_MAX_DATA_SIZE, alg_param.h:37
+
+}  // namespace
+
+// The AICPU template whose order the kernel follows, by schedule family (the auto selector's families).
+HcclResult IpcPlanForFamily(int32_t opType, int32_t family, uint32_t n, uint64_t es, uint64_t cclBytes, IpcPlan* pl)
+{
+    IpcPlan p{};
+    switch (opType) {
+        case HCCL_AMD_OP_ALLREDUCE:
+            if (family == HCCL_AMD_ALGO_MESH_ONESHOT) {
+                p.kind = kIpcAllReduceOneShot;
+                p.order = kIpcO1;
+                p.geom = kIpcGeomWhole;
+            } else if (family == HCCL_AMD_ALGO_MESH_CHUNK) {
+                // MeshChunk CalcSliceInfoVec (…mesh_chunk.cc:79-97), loops of min(ccl, ccl / 2) rounded down to
+                // 128 B (scratch multiple 2)
+                p.kind = kIpcAllReduce;
+                p.order = kIpcO6;
+                p.geom = kIpcGeomCeil;
+                p.loopElems = LoopElems(std::min<uint64_t>(cclBytes, RoundDown128(cclBytes / 2)), es);
+            } else {
+                p.kind = kIpcAllReduce;  // two-shot: O2 does not depend on the slicing or the loops
+                p.order = kIpcO2;
+                p.geom = kIpcGeomAlignedCeil;
+            }
+            break;
+        case HCCL_AMD_OP_REDUCE_SCATTER:
+            p.kind = kIpcReduceScatter;
+            p.geom = kIpcGeomBlock;
+            if (family == HCCL_AMD_ALGO_MESH_CHUNK) {
+                // ReduceScatter MeshChunk: loops of min(ccl - 1 MiB, (ccl - 1 MiB) / (n-1)) rounded down to 128 B
+                const uint64_t tmp = cclBytes > (1ull << 20) ? cclBytes - (1ull << 20) : cclBytes;
+                p.order = kIpcO6;
+                p.subMode = kIpcSubRs4K;
+                p.loopElems = LoopElems(std::min<uint64_t>(tmp, RoundDown128(tmp / (n - 1))), es);
+            } else {
+                p.order = kIpcO1;
+            }
+            break;
+        case HCCL_AMD_OP_REDUCE:
+            p.order = kIpcO1;
+            if (family == HCCL_AMD_ALGO_MESH_ONESHOT) {
+                p.kind = kIpcReduceOneShot;
+                p.geom = kIpcGeomWhole;
+            } else {
+                // ReduceSoleExecutor loops (reduce_sole_executor.cc:120-170): min(UB_MAX_DATA_SIZE, ccl / n) rounded
+                // down to 128 B, each sliced by ReduceMesh1DTwoShot::CalcSlice on its own
+                p.kind = kIpcReduce;
+                p.geom = kIpcGeomBalanced;
+                p.group = 1;
+                p.loopElems = LoopElems(std::min<uint64_t>(kUbMaxDataSize, RoundDown128(cclBytes / n)), es);
+            }
+            break;
+        case HCCL_AMD_OP_ALLGATHER:
+            p.kind = kIpcAllGather;  // data movement only: no order
+            p.order = kIpcO1;
+            p.geom = kIpcGeomWhole;
+            break;
+        default: return HCCL_E_NOT_SUPPORT;
+    }
+    *pl = p;
+    return HCCL_SUCCESS;
+}
+
+uint32_t AivCoreLimit()
+{
+    // The reference takes the vector-core count from the comm config (aivCoreLimit) or the device
+    // (aclrtGetResInCurrentThread(ACL_RT_DEV_RES_VECTOR_CORE), op_common.cc:1063-1078). It only decides the AIV
+    // kernels' variant and slice boundaries here, so it is a parameter: HCCL_AMD_AIV_CORE_LIMIT, default 48
+    // (MAX_NUM_BLOCKS, aiv_defines.h:35).
+    const char* e = std::getenv("HCCL_AMD_AIV_CORE_LIMIT");
+    if (e != nullptr && *e != '\0') {
+        const unsigned long long v = std::strtoull(e, nullptr, 10);
+        if (v >= 1 && v <= 4096) return static_cast<uint32_t>(v);
+    }
+    return 48;
+}
+
+bool ExpansionModeAiv()
+{
+    const char* e = std::getenv("HCCL_OP_EXPANSION_MODE");  // read per call, like HCCL_DETERMINISTIC
+    return e != nullptr && std::strcmp(e, "AIV") == 0;
+}
+
+int32_t SelectAivPlan(int32_t opType, uint32_t n, uint64_t count, HcclDataType dt, HcclReduceOp op, bool strict,
+                      uint64_t cclBytes, uint32_t coreLimit, IpcPlan* plan, uint32_t* group)
+{
+    // Common rejections of AllReduceAutoSelector / ReduceScatterAutoSelector::SelectAivAlgo
+    // (all_reduce_auto_selector.cc:591-683, reduce_scatter_auto_selector.cc:537-600): the order-preserved (STRICT)
+    // mode, PROD, UINT64 / FP64 and more than MAX_RANK_SIZE ranks fall back to the AICPU engine; so does data of
+    // AIV_MAX_PER_RANK_DATA_SIZE (8 MiB, auto_selector_base.h:24) x rankSize or more, or above 16 CCL buffers
+    // (AIV_MAX_CCL_LOOP_NUM, hccl_aiv_utils.h:33). ReduceAutoSelector has no AIV selection: Reduce stays AICPU.
+    const uint64_t es = DataTypeSize(dt);
+    if (es == 0 || n < 2 || n > 512) return HCCL_AMD_AIV_NOT_MATCHED;
+    if (opType != HCCL_AMD_OP_ALLREDUCE && opType != HCCL_AMD_OP_REDUCE_SCATTER) return HCCL_AMD_AIV_NOT_MATCHED;
+    if (strict || op == HCCL_REDUCE_PROD || dt == HCCL_DATA_TYPE_UINT64 || dt == HCCL_DATA_TYPE_FP64) {
+        return HCCL_AMD_AIV_NOT_MATCHED;
+    }
+    const uint64_t maxPerRank = 8ull << 20;
+    IpcPlan p{};
+    uint32_t g = 1;
+    int32_t variant;
+    if (opType == HCCL_AMD_OP_ALLREDUCE) {
+        const uint64_t dataSize = count * es;
+        if (dataSize >= maxPerRank * n || dataSize > cclBytes * 16) return HCCL_AMD_AIV_NOT_MATCHED;
+        // n <= AR_AIV_BOARD_SIZE (8): one-shot below AR_AIV_SMALL_DATA_SIZE_IN_BOARD (128 KiB); above 8 ranks
+        // IsSmallData (< 512 KiB, auto_selector_base.cc:94)
+        const bool oneShot = n <= 8 ? dataSize < (128ull << 10) : dataSize < (512ull << 10);
+        if (oneShot) {
+            // aiv_all_reduce_mesh_1d_oneshot.h:33-48: out = slot 0, then out (op)= slot r, r = 1 .. n-1 (O2);
+            // executor loops of min(UB_MAX_DATA_SIZE, ccl / n) (scratch multiple n), which do not change O2
+            variant = HCCL_AMD_AIV_AR_ONESHOT;
+            p.kind = kIpcAllReduceOneShot;
+            p.order = kIpcO2;
+            p.geom = kIpcGeomWhole;
+            p.loopElems = LoopElems(std::min<uint64_t>(kUbMaxDataSize, RoundDown128(cclBytes / n)), es);
+        } else {
+            // AivTempAllReduceMesh1DTwoShot::CalNumBlocks (aiv_temp_all_reduce_mesh_1D_twoshot.cc:88-100) and the
+            // kernel's split (aiv_all_reduce_mesh_1d_twoshot.h:330-346): 2n blocks or more take Prepare/Process,
+            // fewer the small-core path. Executor loops of min(UB_MAX_DATA_SIZE, ccl / 4) (scratch multiple 4).
+            const uint32_t blocks = coreLimit >= n + 1 ? coreLimit / (n + 1) * (n + 1) : coreLimit;
+            p.loopElems = LoopElems(std::min<uint64_t>(kUbMaxDataSize, RoundDown128(cclBytes / 4)), es);
+            p.kind = kIpcAllReduce;
+            if (blocks >= 2 * n) {
+                // ReduceScatterLocalReduce (:145-181): groupSize = (blocks - n) / n consumer slices per rank, the
+                // loop split into groupSize * n balanced slices, rank r owning slices [r * g, (r + 1) * g); each
+                // is folded own copy first, then the other ranks ascending (O1)
+                g = (blocks - n) / n;
+                variant = HCCL_AMD_AIV_AR_TWOSHOT_LARGE;
+                p.order = kIpcO1;
+                p.geom = kIpcGeomBalanced;
+                p.group = g;
+            } else {
+                // SmallCoreReduceScatter (:224-271): chunks of ceil(count / n); slot 0 (op)= slot i, i = 1 .. n-1 (O2)
+                variant = HCCL_AMD_AIV_AR_TWOSHOT_SMALL;
+                p.order = kIpcO2;
+                p.geom = kIpcGeomCeil;
+            }
+        }
+    } else {
+        const uint64_t totalSize = count * es * n;
+        if (totalSize >= maxPerRank * n || totalSize > cclBytes * 16) return HCCL_AMD_AIV_NOT_MATCHED;
+        // AivTempReduceScatterMesh1D::CalNumBlocks (aiv_temp_reduce_scatter_mesh_1D.cc:87-97): the core limit, at most
+        // 2n below 512 KiB of output; aiv_reduce_scatter_op.h:23-37 takes the big-data kernel above 2n blocks (out =
+        // rank 0's copy, then (op)= rank 1 .. n-1: O2, aiv_reduce_scatter_mesh_1d_bigdata.h:85-101), the local tree
+        // (O4, aiv_reduce_scatter_local_tree.h:138-172, and its core-control twin) otherwise. Executor loops of
+        // min(UB_MAX_DATA_SIZE, ccl / 2n) per block (scratch multiple 2n); neither order depends on them.
+        uint32_t blocks = coreLimit;
+        if (count * es < (512ull << 10)) blocks = std::min(blocks, 2 * n);
+        p.kind = kIpcReduceScatter;
+        p.geom = kIpcGeomBlock;
+        p.loopElems = LoopElems(std::min<uint64_t>(kUbMaxDataSize, RoundDown128(cclBytes / (2ull * n))), es);
+        if (blocks > 2 * n) {
+            variant = HCCL_AMD_AIV_RS_BIGDATA;
+            p.order = kIpcO2;
+        } else {
+            variant = HCCL_AMD_AIV_RS_LOCAL_TREE;
+            p.order = kIpcO4;
+        }
+    }
+    if (plan != nullptr) *plan = p;
+    if (group != nullptr) *group = g;
+    return variant;
+}
+
 HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void* sendBuf, void* recvBuf,
                             uint64_t count, HcclDataType dt, HcclReduceOp op, uint32_t root, hipStream_t stream)
 {
+    const uint64_t es = DataTypeSize(dt);
+    if (es == 0) return HCCL_E_NOT_SUPPORT;
+    IpcPlan plan{};
+    HCCL_CHK(IpcPlanForFamily(opType, family, c.nRanks, es, c.cclBytes, &plan));
+    return RunIpcPlan(c, opType, plan, sendBuf, recvBuf, count, dt, op, root, stream);
+}
+
+HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* sendBuf, void* recvBuf,
+                      uint64_t count, HcclDataType dt, HcclReduceOp op, uint32_t root, hipStream_t stream)
+{
     uint64_t es = DataTypeSize(dt);
     if (es == 0 || c.nRanks > kIpcMaxRanks) return HCCL_E_NOT_SUPPORT;
+    uint64_t loopElems = plan.loopElems;
     if (opType == HCCL_AMD_OP_ALLGATHER) {
         // pure data movement: any dtype runs as the integer type of its size (16-B types as pairs of 8-B words)
         op = HCCL_REDUCE_SUM;
@@ -227,29 +412,7 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
             default: return HCCL_E_NOT_SUPPORT;
         }
     }
-    IpcKind kind;
-    IpcOrder order;
-    switch (opType) {
-        case HCCL_AMD_OP_ALLREDUCE:
-            kind = family == HCCL_AMD_ALGO_MESH_ONESHOT ? kIpcAllReduceOneShot : kIpcAllReduce;
-            order = family == HCCL_AMD_ALGO_MESH_ONESHOT ? kIpcO1
-                  : family == HCCL_AMD_ALGO_MESH_CHUNK   ? kIpcO6
-                                                         : kIpcO2;
-            break;
-        case HCCL_AMD_OP_REDUCE_SCATTER:
-            kind = kIpcReduceScatter;
-            order = family == HCCL_AMD_ALGO_MESH_CHUNK ? kIpcO6 : kIpcO1;
-            break;
-        case HCCL_AMD_OP_REDUCE:
-            kind = family == HCCL_AMD_ALGO_MESH_ONESHOT ? kIpcReduceOneShot : kIpcReduce;
-            order = kIpcO1;
-            break;
-        case HCCL_AMD_OP_ALLGATHER:
-            kind = kIpcAllGather;  // data movement only: no order
-            order = kIpcO1;
-            break;
-        default: return HCCL_E_NOT_SUPPORT;
-    }
+    const IpcKind kind = static_cast<IpcKind>(plan.kind);
     // Stream capture: the barrier epochs live on the device (status word kIpcEpochWord, advanced once per launch by
     // the block that completes its arrival count), so a captured launch replays correctly: each replay takes the
     // next epochs, as a new call would. Two things cannot be captured: the collective set-up of the first call
@@ -281,8 +444,8 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
     }
     a.n = n;
     a.kind = kind;
-    a.order = order;
-    a.subMode = opType == HCCL_AMD_OP_REDUCE_SCATTER ? kIpcSubRs4K : kIpcSubEven;
+    a.order = plan.order;
+    a.subMode = plan.subMode;
     a.root = root;
     a.timeoutTicks = IpcTimeoutTicks();  // a lost peer ends the kernel with status bit 0, never a hang
     a.status = s.status;
@@ -295,62 +458,50 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
     const uint64_t slotCap = ((single ? s.stgAltBytes : s.stgInBytes) / es / n) / V * V;
 
     // One launch per executor loop [off, off + cnt) of the reference template whose order the fold follows: its
-    // slicing is per loop (schedule.cc RefLoopElems and the MeshChunk loops).
+    // slicing is per loop (schedule.cc RefLoopElems and the MeshChunk loops). A ReduceScatter loop takes elements
+    // [off, off + cnt) of every block.
     struct Launch {
         uint64_t off, cnt;
     };
     std::vector<Launch> launches;
-    uint64_t loopElems = count;
-    if (kind == kIpcReduce) {
-        // ReduceSoleExecutor loops (reduce_sole_executor.cc:120-170): min(UB_MAX_DATA_SIZE, ccl / n) rounded down to
-        // 128 B, each sliced by ReduceMesh1DTwoShot::CalcSlice on its own
-        loopElems = std::max<uint64_t>(1, std::min<uint64_t>(256ull << 20, c.cclBytes / n / 128 * 128) / es);
-    } else if (order == kIpcO6 && opType == HCCL_AMD_OP_ALLREDUCE) {
-        // AllReduce MeshChunk: min(ccl, ccl / 2) rounded down to 128 B (scratch multiple 2)
-        loopElems = std::max<uint64_t>(1, std::min<uint64_t>(c.cclBytes, c.cclBytes / 2 / 128 * 128) / es);
-    } else if (order == kIpcO6) {
-        // ReduceScatter MeshChunk: min(ccl - 1 MiB, (ccl - 1 MiB) / (n-1)) rounded down to 128 B
-        const uint64_t tmp = c.cclBytes > (1ull << 20) ? c.cclBytes - (1ull << 20) : c.cclBytes;
-        loopElems = std::max<uint64_t>(1, std::min<uint64_t>(tmp, tmp / (n - 1) / 128 * 128) / es);
-    }
+    if (loopElems == 0) loopElems = count;
     for (uint64_t off = 0; off < count; off += loopElems) launches.push_back({off, std::min(loopElems, count - off)});
     auto geometry = [&](IpcArgs& g, uint64_t cnt) {
-        if (kind == kIpcReduceScatter) {
-            // block c of the input (recvCount elements, stride recvCount) is chunk c (reduce_scatter_op.cc:158-159);
-            // a MeshChunk loop takes elements [off, off + cnt) of every block
-            g.balanced = false;
-            g.chunkStride = count;
-            g.chunkLen = cnt;
-            g.total = uint64_t(n - 1) * count + cnt;
-            g.rem = 0;
-        } else if (kind == kIpcReduce) {
-            g.balanced = true;  // reduce_mesh_1D_two_shot.cc:108-131
-            g.total = cnt;
-            g.chunkLen = cnt / n;
-            g.rem = cnt % n;
-            g.chunkStride = 0;
-        } else if (kind == kIpcAllReduceOneShot || kind == kIpcReduceOneShot || kind == kIpcAllGather) {
-            // every rank holds (and, for the AllReduce, folds) the whole range; AllGather: its whole input
-            g.balanced = false;
-            g.total = cnt;
-            g.chunkStride = 0;
-            g.chunkLen = cnt;
-            g.rem = 0;
-        } else if (order == kIpcO6) {
-            // MeshChunk CalcSliceInfoVec (…mesh_chunk.cc:79-97): ceil(cnt / n), no 128-B alignment
-            g.balanced = false;
-            g.total = cnt;
-            g.chunkStride = g.chunkLen = (cnt + n - 1) / n;
-            g.rem = 0;
-        } else {
-            // ceil(count / n) rounded up to HCCL_MIN_SLICE_ALIGN = 128 B (order O2 does not depend on it)
-            const uint64_t align = 128 / es;
-            g.balanced = false;
-            g.total = cnt;
-            g.chunkStride = g.chunkLen = ((cnt + n - 1) / n + align - 1) / align * align;
-            g.rem = 0;
+        g.balanced = false;
+        g.group = 1;
+        g.rem = 0;
+        g.total = cnt;
+        switch (plan.geom) {
+            case kIpcGeomBlock:
+                // block c of the input (recvCount elements, stride recvCount) is chunk c (reduce_scatter_op.cc:158-159)
+                g.chunkStride = count;
+                g.chunkLen = cnt;
+                g.total = uint64_t(n - 1) * count + cnt;
+                break;
+            case kIpcGeomBalanced: {
+                const uint64_t slices = uint64_t(plan.group) * n;
+                g.balanced = true;
+                g.group = plan.group;
+                g.chunkLen = cnt / slices;  // slice length; the first cnt % slices slices hold one more
+                g.rem = cnt % slices;
+                g.chunkStride = 0;
+                break;
+            }
+            case kIpcGeomWhole:
+                // every rank holds (and, for the AllReduce, folds) the whole range; AllGather: its whole input
+                g.chunkStride = 0;
+                g.chunkLen = cnt;
+                break;
+            case kIpcGeomCeil:
+                g.chunkStride = g.chunkLen = (cnt + n - 1) / n;
+                break;
+            default: {
+                const uint64_t align = 128 / es;  // HCCL_MIN_SLICE_ALIGN
+                g.chunkStride = g.chunkLen = ((cnt + n - 1) / n + align - 1) / align * align;
+                break;
+            }
         }
-        const uint64_t widest = g.chunkLen + (g.rem != 0 ? 1 : 0);
+        const uint64_t widest = g.balanced ? g.group * g.chunkLen + std::min<uint64_t>(g.group, g.rem) : g.chunkLen;
         g.piece = std::max<uint64_t>(V, std::min(slotCap, (widest + V - 1) / V * V));
         g.blockElems = ((g.piece + s.blocks - 1) / s.blocks + V - 1) / V * V;
         g.rounds = static_cast<uint32_t>((widest + g.piece - 1) / g.piece);

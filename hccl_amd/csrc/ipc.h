@@ -22,9 +22,36 @@ enum IpcKind : uint32_t {
 
 // Operand order of a fold of chunk t.
 enum IpcOrder : uint32_t {
-    kIpcO2 = 0,  // x_0, x_1, .., x_{n-1}                          two-shot AllReduce
-    kIpcO1 = 1,  // x_t, then ascending q != t                      one-shot, mesh ReduceScatter, Reduce
+    kIpcO2 = 0,  // x_0, x_1, .., x_{n-1}                          two-shot AllReduce; AIV one-shot, small-core
+                 //                                                 two-shot, big-data ReduceScatter
+    kIpcO1 = 1,  // x_t, then ascending q != t                      one-shot, mesh ReduceScatter, Reduce; AIV
+                 //                                                 large-core two-shot
     kIpcO6 = 2,  // sub-slice j: x_t, then x_{t+o}, o = j+1..n-1, 1..j   MeshChunk AllReduce / ReduceScatter
+    kIpcO4 = 3,  // pow-2 tree over the source ranks (rank-independent): M = largest power of two below n,
+                 // x_j = x_{j+M} (op) x_j for j + M < n, then pairwise halving  AIV local-tree ReduceScatter
+                 // (aiv_reduce_scatter_local_tree.h:138-172) = the STRICT order-preserved tree
+};
+
+// Chunk layout of one launch (input coordinates, elements; rank c owns chunk c).
+enum IpcGeom : uint32_t {
+    kIpcGeomAlignedCeil = 0,  // ceil(cnt / n) rounded up to 128 B (two-shot AllReduce, CalcSliceInfo)
+    kIpcGeomCeil = 1,         // ceil(cnt / n), no alignment (MeshChunk CalcSliceInfoVec; AIV small-core two-shot)
+    kIpcGeomBalanced = 2,     // g * n balanced slices (the first cnt % (g*n) one longer), chunk c = slices
+                              // [c*g, (c+1)*g): Reduce two-shot (g = 1, reduce_mesh_1D_two_shot.cc:108-131) and
+                              // the AIV large-core two-shot (g = groupSize, aiv_all_reduce_mesh_1d_twoshot.h:21-58)
+    kIpcGeomBlock = 3,        // ReduceScatter: chunk c = input block c (reduce_scatter_op.cc:158-159)
+    kIpcGeomWhole = 4,        // one-shot kinds and AllGather: every chunk is the whole range
+};
+
+// Everything that decides a one-sided call's bits: the kind, the fold order, the chunk layout and the executor loop
+// that the layout is applied to (the reference slices every loop on its own).
+struct IpcPlan {
+    uint32_t kind;       // IpcKind
+    uint32_t order;      // IpcOrder
+    uint32_t geom;       // IpcGeom
+    uint32_t group = 1;  // kIpcGeomBalanced: slices per chunk
+    uint32_t subMode = 0;  // IpcSubMode (kIpcO6)
+    uint64_t loopElems = 0;  // elements per executor loop (per block for ReduceScatter); 0 = one loop
 };
 
 // Sub-slices of a chunk for kIpcO6 (chunk coordinates): the MeshChunk AllReduce's even split (the first L % (n-1)
@@ -71,7 +98,9 @@ struct IpcArgs {
     uint64_t total;
     uint64_t chunkStride;
     uint64_t chunkLen;
-    uint64_t rem;   // balanced: chunk c starts at c*chunkLen + min(c, rem) and holds chunkLen + (c < rem) elements
+    uint64_t rem;   // balanced: chunkLen is the slice length, rem the number of one-longer slices
+    uint64_t group;  // balanced: slices per chunk; chunk c starts at c*group*chunkLen + min(c*group, rem) and holds
+                     // group*chunkLen + min(group, rem - c*group clamped at 0) elements
     bool balanced;
     uint64_t piece;
     uint64_t blockElems;

@@ -149,12 +149,16 @@ struct Range {
 
 __device__ __forceinline__ uint64_t ChunkStart(const IpcArgs& a, uint32_t c)
 {
-    return a.balanced ? uint64_t(c) * a.chunkLen + min(uint64_t(c), a.rem) : uint64_t(c) * a.chunkStride;
+    const uint64_t s = uint64_t(c) * a.group;  // first slice of chunk c (balanced)
+    return a.balanced ? s * a.chunkLen + min(s, a.rem) : uint64_t(c) * a.chunkStride;
 }
 
 __device__ __forceinline__ uint64_t ChunkElems(const IpcArgs& a, uint32_t c)
 {
-    if (a.balanced) return a.chunkLen + (c < a.rem ? 1 : 0);
+    if (a.balanced) {
+        const uint64_t s = uint64_t(c) * a.group;
+        return a.group * a.chunkLen + (a.rem > s ? min(a.group, a.rem - s) : 0);
+    }
     const uint64_t start = uint64_t(c) * a.chunkStride;
     return start >= a.total ? 0 : min(a.chunkLen, a.total - start);
 }
@@ -226,10 +230,87 @@ __device__ __forceinline__ uint64_t SubStart(const IpcArgs& a, uint64_t L, uint3
     return uint64_t(j) * base + min(uint64_t(j), big);
 }
 
+template <class E, int OP>
+__device__ __forceinline__ u32x4 Comb(u32x4 s, u32x4 d)
+{
+    return combine<E, OP>(s, d);
+}
+
+template <class E, int OP>
+__device__ __forceinline__ typename E::S Comb(typename E::S s, typename E::S d)
+{
+    return E::template ap<OP>(s, d);
+}
+
+// Bit reversal of t over log2(M) bits (M a power of two), and the number of trailing one bits of t.
+template <int M>
+constexpr uint32_t BitRev(uint32_t t)
+{
+    uint32_t r = 0;
+    for (int m = M >> 1, b = 1; m > 0; m >>= 1, b <<= 1) {
+        if (t & uint32_t(b)) r |= uint32_t(m);
+    }
+    return r;
+}
+
+constexpr int TrailingOnes(int t)
+{
+    int c = 0;
+    while (t & 1) {
+        ++c;
+        t >>= 1;
+    }
+    return c;
+}
+
+constexpr int Log2(int m) { return m <= 1 ? 0 : 1 + Log2(m >> 1); }
+
+// Step T of TreeFold: first-round value number BitRev(T), then the merges its position completes.
+template <class E, int OP, int M, int T, int D, class Leaf, class V>
+__device__ __forceinline__ V TreeStep(uint32_t n, const Leaf& leaf, V (&st)[D])
+{
+    constexpr uint32_t jj = BitRev<M>(uint32_t(T));
+    V x = leaf(jj);
+    if (jj + M < n) x = Comb<E, OP>(leaf(jj + M), x);
+    constexpr int lvl = TrailingOnes(T);
+#pragma unroll
+    for (int b = 0; b < lvl; ++b) x = Comb<E, OP>(x, st[b]);  // the later partial is src, the earlier one dst
+    if constexpr (T + 1 < M) {
+        st[lvl] = x;
+        return TreeStep<E, OP, M, T + 1>(n, leaf, st);
+    } else {
+        return x;
+    }
+}
+
+// Order O4 over the n sources (leaf(q) = operand of rank q), M = the largest power of two below n
+// (GetLargestPowerOf2, aiv_reduce_scatter_local_tree.h:95-105). Round one folds x_{j+M} into x_j for j + M < n; the
+// rounds after it halve a power-of-two set: L'(j) = L(j + h) (op) L(j). Visiting the first-round values in bit-reversed
+// index order makes every later pair adjacent, so the rounds become a binary counter over a register stack: each
+// value merges as src into the partial below it (dst), exactly the (src, dst) roles of the template's
+// CpGM2GM(front, back, reduceOp) = front (op)= back. Every stack index is a compile-time constant.
+template <class E, int OP, int M, class Leaf>
+__device__ __forceinline__ auto TreeFold(uint32_t n, const Leaf& leaf)
+{
+    using V = decltype(leaf(0u));
+    V st[Log2(M) > 0 ? Log2(M) : 1];
+    return TreeStep<E, OP, M, 0>(n, leaf, st);
+}
+
+// Dispatch of TreeFold on M (n <= 16: M <= 8).
+template <class E, int OP, class Leaf>
+__device__ __forceinline__ auto TreeFoldN(uint32_t n, const Leaf& leaf)
+{
+    if (n > 8) return TreeFold<E, OP, 8>(n, leaf);
+    if (n > 4) return TreeFold<E, OP, 4>(n, leaf);
+    if (n > 2) return TreeFold<E, OP, 2>(n, leaf);
+    return TreeFold<E, OP, 1>(n, leaf);
+}
+
 // Fold of the piece range r (piece coordinates) of chunk `me` over the n operands, operand i being rank
-// OperandRank(order, n, me, j, i), written to ndst destinations. own = this rank's operand, slots = its staging (slot
-// q at q * piece). vec: the chunk's operands are 16-B aligned at piece coordinate 0; r may start and end anywhere
-// (scalar head and tail around the vector body).
+// OperandRank(order, n, me, j, i) (order O4: the tree over the ranks), written to ndst destinations. own = this rank's
+// operand, slots = its staging (slot q at q * piece). vec: the chunk's operands are 16-B aligned at piece coordinate
+// 0; r may start and end anywhere (scalar head and tail around the vector body).
 template <class E, int OP, class Dst>
 __device__ __forceinline__ void FoldSeg(const IpcArgs& a, uint32_t me, uint32_t j, const typename E::S* own,
                                         const typename E::S* slots, Dst dsts, uint32_t ndst, Range r, bool vec)
@@ -237,10 +318,30 @@ __device__ __forceinline__ void FoldSeg(const IpcArgs& a, uint32_t me, uint32_t 
     using S = typename E::S;
     constexpr uint64_t V = 16 / sizeof(S);
     const uint32_t n = a.n;
-    auto src = [&](uint32_t i) {
-        const uint32_t q = OperandRank(a.order, n, me, j, i);
-        return q == me ? own : slots + uint64_t(q) * a.piece;
-    };
+    auto rankSrc = [&](uint32_t q) { return q == me ? own : slots + uint64_t(q) * a.piece; };
+    if (a.order == kIpcO4) {
+        // rank-independent tree: one vector (or element) per lane and step keeps the register stack small
+        const uint64_t vb = (r.lo + V - 1) / V, ve = r.hi / V;
+        auto scalarTree = [&](uint64_t lo, uint64_t hi) {
+            for (uint64_t e = lo + threadIdx.x; e < hi; e += kIpcBlock) {
+                const S acc = TreeFoldN<E, OP>(n, [&](uint32_t q) { return rankSrc(q)[e]; });
+                for (uint32_t d = 0; d < ndst; ++d) dsts(d)[e] = acc;
+            }
+        };
+        if (!vec || vb >= ve) {
+            scalarTree(r.lo, r.hi);
+            return;
+        }
+        scalarTree(r.lo, vb * V);
+        for (uint64_t v = vb + threadIdx.x; v < ve; v += kIpcBlock) {
+            const u32x4 acc = TreeFoldN<E, OP>(
+                n, [&](uint32_t q) { return reinterpret_cast<const u32x4*>(rankSrc(q))[v]; });
+            for (uint32_t d = 0; d < ndst; ++d) reinterpret_cast<u32x4*>(dsts(d))[v] = acc;
+        }
+        scalarTree(ve * V, r.hi);
+        return;
+    }
+    auto src = [&](uint32_t i) { return rankSrc(OperandRank(a.order, n, me, j, i)); };
     auto scalar = [&](uint64_t lo, uint64_t hi) {
         for (uint64_t e = lo + threadIdx.x; e < hi; e += kIpcBlock) {
             S acc = src(0)[e];

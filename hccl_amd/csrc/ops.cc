@@ -81,6 +81,23 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     ScheduleParams p;
     p.opType = opType;
     p.algo = c.algoOverride;
+    // The AIV engine (HCCL_OP_EXPANSION_MODE=AIV, or forced per communicator): SelectAivAlgo's choice and its
+    // kernels' orders on the one-sided kernel. What it does not match, or cannot run (no peer mappings, a capture
+    // before the set-up), takes the AICPU engine's selection below, as the reference falls back
+    // (AutoSelectorBase::ProcessAivConfig, auto_selector_base.cc:353-371).
+    if (p.algo == HCCL_AMD_ALGO_AIV || (p.algo == HCCL_AMD_ALGO_AUTO && ExpansionModeAiv())) {
+        IpcPlan plan{};
+        const int32_t v = SelectAivPlan(opType, c.nRanks, count, dt, op, NeedStrictOrder(opType, dt, op, c.nRanks),
+                                        c.cclBytes, AivCoreLimit(), &plan, nullptr);
+        if (v != HCCL_AMD_AIV_NOT_MATCHED) {
+            const HcclResult r = RunIpcPlan(c, opType, plan, sendBuf, recvBuf, count, dt, op, root, stream);
+            if (r != HCCL_E_NOT_SUPPORT) {
+                c.lastAlgo = HCCL_AMD_ALGO_AIV;
+                return r;
+            }
+        }
+        p.algo = HCCL_AMD_ALGO_AUTO;
+    }
     // an IPC-only communicator (bootstrap transport without send/recv) runs every reducing op on the IPC kernel in
     // the auto family, whatever schedule family was asked for
     if (!c.transport->HasSendRecv() && p.algo != HCCL_AMD_ALGO_IPC_TWOSHOT) p.algo = HCCL_AMD_ALGO_IPC;
@@ -309,7 +326,7 @@ HcclResult HcclAmdCommSetAlgo(HcclComm comm, int32_t algo)
 {
     Comm* c = AsComm(comm);
     if (c == nullptr) return HCCL_E_PTR;
-    if (algo < HCCL_AMD_ALGO_AUTO || algo > HCCL_AMD_ALGO_IPC) return HCCL_E_PARA;
+    if (algo < HCCL_AMD_ALGO_AUTO || algo > HCCL_AMD_ALGO_AIV) return HCCL_E_PARA;
     c->algoOverride = algo;
     return HCCL_SUCCESS;
 }
@@ -355,6 +372,13 @@ int32_t HcclAmdRhdTable(uint32_t nRanks, uint32_t* realOfVirtual, uint32_t capac
         std::memcpy(realOfVirtual + size_t(k) * nRanks, t[k].data(), nRanks * sizeof(uint32_t));
     }
     return static_cast<int32_t>(t.size());
+}
+
+int32_t HcclAmdSelectAivAlgo(int32_t opType, uint32_t nRanks, uint64_t count, HcclDataType dataType, HcclReduceOp op,
+                             uint32_t coreLimit, int32_t strict, uint32_t* groupSize)
+{
+    return SelectAivPlan(opType, nRanks, count, dataType, op, strict != 0, CclBytesDefault(),
+                         coreLimit != 0 ? coreLimit : AivCoreLimit(), nullptr, groupSize);
 }
 
 int32_t HcclAmdSelectAlgo(int32_t opType, uint32_t nRanks, uint64_t bytes, int32_t special)

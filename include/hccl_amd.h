@@ -108,9 +108,30 @@ typedef enum {
     HCCL_AMD_ALGO_IPC_TWOSHOT = 7,     /* AllReduce: one kernel over peer-mapped staging (AIV GM_IN model), O2 */
     HCCL_AMD_ALGO_MESH_CHUNK = 8,      /* AllReduce / ReduceScatter: the reference's MeshChunk templates, order O6
                                           (owner first, then the peers in a per-sub-slice rotated order) */
-    HCCL_AMD_ALGO_IPC = 9              /* the one-sided kernel in the order family the auto selector picks (one-shot
+    HCCL_AMD_ALGO_IPC = 9,             /* the one-sided kernel in the order family the auto selector picks (one-shot
                                           O1 / two-shot O2 / MeshChunk O6 ...): the auto path's bits over IPC */
+    HCCL_AMD_ALGO_AIV = 10             /* the reference's AIV engine (HCCL_OP_EXPANSION_MODE=AIV): SelectAivAlgo's
+                                          choice and orders on the one-sided kernel; what it does not match runs
+                                          the auto (AICPU) selection, as the reference falls back */
 } HcclAmdAlgo;
+
+/* Variant of the reference's AIV engine a call takes (HcclAmdSelectAivAlgo). */
+typedef enum {
+    HCCL_AMD_AIV_NOT_MATCHED = 0,       /* SelectAivAlgo does not match: the AICPU engine runs */
+    HCCL_AMD_AIV_AR_ONESHOT = 1,        /* aiv_all_reduce_mesh_1d_oneshot.h:33-48, order O2 */
+    HCCL_AMD_AIV_AR_TWOSHOT_LARGE = 2,  /* aiv_all_reduce_mesh_1d_twoshot.h:145-181: O1 over groupSize * n
+                                           balanced slices, rank r owning [r * groupSize, (r + 1) * groupSize) */
+    HCCL_AMD_AIV_AR_TWOSHOT_SMALL = 3,  /* aiv_all_reduce_mesh_1d_twoshot.h:224-271: O2 over ceil(count / n) */
+    HCCL_AMD_AIV_RS_BIGDATA = 4,        /* aiv_reduce_scatter_mesh_1d_bigdata.h:85-101: O2 */
+    HCCL_AMD_AIV_RS_LOCAL_TREE = 5      /* aiv_reduce_scatter_local_tree.h:138-172: O4 (pow-2 tree) */
+} HcclAmdAivVariant;
+
+/* The AIV-engine variant an operation would take (opType ALLREDUCE or REDUCE_SCATTER; count = recvCount for
+ * ReduceScatter) on nRanks ranks with `coreLimit` vector cores (0 = HCCL_AMD_AIV_CORE_LIMIT, default 48), the CCL
+ * buffer HCCL_BUFFSIZE and strict != 0 for HCCL_DETERMINISTIC=strict. *groupSize (may be NULL) receives the slices per
+ * rank of HCCL_AMD_AIV_AR_TWOSHOT_LARGE (1 otherwise). Returns an HcclAmdAivVariant. */
+extern int32_t HcclAmdSelectAivAlgo(int32_t opType, uint32_t nRanks, uint64_t count, HcclDataType dataType,
+                                    HcclReduceOp op, uint32_t coreLimit, int32_t strict, uint32_t* groupSize);
 
 /* Build rank `rank`'s schedule. If ops == NULL only *numOps is written. scratchElems receives the number of
  * scratch elements the schedule addresses. pieceBytes = 0 picks the default pipelining granule. */

@@ -424,6 +424,71 @@ def reduce_scatter_meshchunk(dtype, op, xs, rc, ccl=None):
     return outs
 
 
+# ----------------------------------------------------------------------------------------- AIV engine
+
+AIV_NOT_MATCHED, AIV_AR_ONESHOT, AIV_AR_TWOSHOT_LARGE, AIV_AR_TWOSHOT_SMALL, AIV_RS_BIGDATA, AIV_RS_LOCAL_TREE = range(6)
+AIV_CORE_LIMIT = 48  # MAX_NUM_BLOCKS, aiv_defines.h:35
+
+
+def aiv_select(op_type, n, count, es, dt64, prod, strict=False, ccl=None, core_limit=AIV_CORE_LIMIT):
+    """SelectAivAlgo (all_reduce_auto_selector.cc:591-683, reduce_scatter_auto_selector.cc:537-600) and the variant
+    the AIV kernels take for `core_limit` vector cores (aiv_temp_all_reduce_mesh_1D_twoshot.cc:88-100,
+    aiv_all_reduce_mesh_1d_twoshot.h:330-346; aiv_temp_reduce_scatter_mesh_1D.cc:87-97, aiv_reduce_scatter_op.h:23-37).
+    dt64: UINT64 or FP64 (the AIV path rejects them). Returns (variant, groupSize)."""
+    ccl = ccl_bytes_from_env() if ccl is None else ccl
+    if op_type not in (0, 1) or strict or prod or dt64 or n < 2:
+        return AIV_NOT_MATCHED, 1
+    if op_type == 0:
+        size = count * es
+        if size >= (8 << 20) * n or size > ccl * 16:
+            return AIV_NOT_MATCHED, 1
+        if size < ((128 << 10) if n <= 8 else (512 << 10)):
+            return AIV_AR_ONESHOT, 1
+        blocks = core_limit // (n + 1) * (n + 1) if core_limit >= n + 1 else core_limit
+        if blocks >= 2 * n:
+            return AIV_AR_TWOSHOT_LARGE, (blocks - n) // n
+        return AIV_AR_TWOSHOT_SMALL, 1
+    total = count * es * n
+    if total >= (8 << 20) * n or total > ccl * 16:
+        return AIV_NOT_MATCHED, 1
+    blocks = core_limit
+    if count * es < (512 << 10):
+        blocks = min(blocks, 2 * n)
+    return (AIV_RS_BIGDATA if blocks > 2 * n else AIV_RS_LOCAL_TREE), 1
+
+
+def allreduce_aiv(dtype, op, xs, variant, group, ccl=None):
+    """AIV AllReduce. One-shot (aiv_all_reduce_mesh_1d_oneshot.h:33-48) and small-core two-shot (:224-271): out =
+    x_0, then (op)= x_1 .. x_{n-1}, order O2. Large-core two-shot (:145-181) per executor loop of
+    min(UB_MAX_DATA_SIZE, ccl / 4): the loop is split into group * n balanced slices (the first cnt % (group*n) one
+    longer); rank c owns slices [c*group, (c+1)*group) and folds its own copy first, then the others ascending (O1)."""
+    if variant in (AIV_AR_ONESHOT, AIV_AR_TWOSHOT_SMALL):
+        return allreduce_o2(dtype, op, xs)
+    assert variant == AIV_AR_TWOSHOT_LARGE
+    ccl = ccl_bytes_from_env() if ccl is None else ccl
+    n = len(xs)
+    es = xs[0].itemsize
+    out = np.empty_like(xs[0])
+    for off, cnt in ref_loops(xs[0].size, es, UB_MAX_DATA_SIZE, 4, ccl):
+        sl = balanced_bounds(cnt, group * n)
+        for c in range(n):
+            b, e = off + sl[c * group][0], off + sl[(c + 1) * group - 1][1]
+            if e > b:
+                out[b:e] = fold(dtype, op, [xs[c][b:e]] + [xs[q][b:e] for q in range(n) if q != c])
+    return [out.copy() for _ in xs]
+
+
+def reduce_scatter_aiv(dtype, op, xs, rc, variant):
+    """AIV ReduceScatter: the big-data kernel folds rank 0's copy of the block, then ranks 1 .. n-1 (O2,
+    aiv_reduce_scatter_mesh_1d_bigdata.h:85-101); the local tree folds the pow-2 tree over the ranks (O4,
+    aiv_reduce_scatter_local_tree.h:138-172)."""
+    n = len(xs)
+    if variant == AIV_RS_LOCAL_TREE:
+        return reduce_scatter_tree(dtype, op, xs, rc)
+    assert variant == AIV_RS_BIGDATA
+    return [fold(dtype, op, [x[me * rc:(me + 1) * rc] for x in xs]) for me in range(n)]
+
+
 ALGO_ONESHOT, ALGO_TWOSHOT, ALGO_RING, ALGO_RHD, ALGO_NHR, ALGO_TREE, ALGO_IPC, ALGO_MESHCHUNK = 1, 2, 3, 4, 5, 6, 7, 8
 ALGO_IPC_AUTO = 9
 

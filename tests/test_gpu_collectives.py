@@ -408,6 +408,62 @@ def test_c5_rhd_fp16_random_bit_exact(worlds, nbytes):
             assert O.equal_bits(O.FP16, outs[r], want_cf[r]), ("vs closed form", r)
 
 
+def aiv_expected(op_type, dtype, op, xs, count, n, core_limit):
+    es = np.dtype(O.NP_STORAGE[dtype]).itemsize
+    variant, group = R.aiv_select(op_type, n, count, es, dtype in (O.UINT64, O.FP64), op == O.PROD,
+                                  core_limit=core_limit)
+    if op_type == AR:
+        return variant, R.allreduce_aiv(dtype, op, xs, variant, group)
+    return variant, R.reduce_scatter_aiv(dtype, op, xs, count, variant)
+
+
+# (op, n, count, core limit): every variant of the AIV engine -- one-shot (O2), large-core two-shot (O1 over
+# groupSize * n balanced slices; ragged counts put chunk starts off the 16-B grid), small-core two-shot (O2, a core
+# limit below 2n blocks), ReduceScatter local tree (O4: small output, or a core limit of at most 2n) and big-data (O2)
+AIV_CASES = [(AR, 2, 5001, 48), (AR, 8, 30000, 48), (AR, 4, (1 << 20) + 3, 48), (AR, 8, (1 << 20) + 7, 48),
+             (AR, 8, 100003, 48), (AR, 3, 400001, 56), (AR, 8, 70001, 9), (AR, 4, 300007, 8),
+             (RS, 4, 1001, 48), (RS, 8, 30001, 48), (RS, 2, (1 << 17) + 5, 48), (RS, 8, (1 << 17) + 1, 48),
+             (RS, 8, (1 << 17) + 1, 16), (RS, 3, 200003, 6)]
+
+
+@pytest.mark.parametrize("dtype,op", [(O.FP32, O.SUM), (O.FP16, O.SUM), (O.BFP16, O.MAX), (O.INT8, O.SUM),
+                                      (O.FP32, O.MIN)], ids=lambda v: str(v))
+@pytest.mark.parametrize("op_type,n,count,core_limit", AIV_CASES)
+def test_aiv_engine_orders(worlds, monkeypatch, op_type, n, count, core_limit, dtype, op):
+    """HCCL_AMD_ALGO_AIV (= HCCL_OP_EXPANSION_MODE=AIV): SelectAivAlgo's variant for the core limit, each folded in
+    its kernel's order on the one-sided kernel, bit-exact against the closed forms of tests/sched_ref.py."""
+    monkeypatch.setenv("HCCL_AMD_AIV_CORE_LIMIT", str(core_limit))
+    comms = worlds(n)
+    in_count = count * n if op_type == RS else count
+    xs = [O.random_operands(dtype, in_count, seed=1300 + 7 * n + r, edge=False) for r in range(n)]
+    variant, want = aiv_expected(op_type, dtype, op, xs, count, n, core_limit)
+    assert variant != R.AIV_NOT_MATCHED
+    assert int(H.select_aiv_algo(op_type, n, count, dtype, op, core_limit)[0]) == variant
+    used, outs = collective(comms, op_type, H.Algo.AIV, dtype, op, xs, count)
+    assert used == H.Algo.AIV
+    for r in range(n):
+        assert O.equal_bits(dtype, outs[r], want[r]), (r, variant)
+
+
+def test_aiv_expansion_mode_env_and_fallback(worlds, monkeypatch):
+    """HCCL_OP_EXPANSION_MODE=AIV on an auto communicator takes the AIV engine; what SelectAivAlgo does not match
+    (PROD, FP64, 64 MiB at 8 ranks) runs the AICPU selection, as the reference falls back."""
+    monkeypatch.setenv("HCCL_OP_EXPANSION_MODE", "AIV")
+    n = 4
+    comms = worlds(n)
+    xs = [O.random_operands(O.FP32, 3001, seed=1400 + r, edge=False) for r in range(n)]
+    used, outs = collective(comms, AR, H.Algo.AUTO, O.FP32, O.SUM, xs, 3001)
+    assert used == H.Algo.AIV
+    want = R.allreduce_o2(O.FP32, O.SUM, xs)
+    for r in range(n):
+        assert O.equal_bits(O.FP32, outs[r], want[r]), r
+    used, outs = collective(comms, AR, H.Algo.AUTO, O.FP32, O.PROD, xs, 3001)
+    assert used == R.ALGO_ONESHOT  # AICPU one-shot (O1)
+    want = R.allreduce_o1(O.FP32, O.PROD, xs)
+    for r in range(n):
+        assert O.equal_bits(O.FP32, outs[r], want[r]), r
+
+
 @pytest.mark.parametrize("algo", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_allreduce_inplace(worlds, algo):
     n, count = 4, 300007

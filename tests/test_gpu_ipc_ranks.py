@@ -37,6 +37,10 @@ CASES = [
     # AllGather (data movement, one barrier per round): ragged, several rounds, and between reducing calls
     (AG, O.FP16, O.SUM, 33333, 9), (AG, O.FP32, O.SUM, (20 << 20) + 3, 9), (AG, O.INT8, O.SUM, 5, 9),
     (AR, O.FP32, O.SUM, 4099, 9),
+    # HCCL_AMD_ALGO_AIV (10): the AIV engine's variants (default 48 vector cores): one-shot O2, large-core two-shot
+    # O1 over balanced groups (ragged: chunk starts off the vector grid), ReduceScatter local tree O4 and big-data O2
+    (AR, O.FP32, O.SUM, 5001, 10), (AR, O.FP32, O.SUM, (1 << 20) + 3, 10), (AR, O.BFP16, O.MAX, 300001, 10),
+    (RS, O.FP32, O.SUM, 1001, 10), (RS, O.FP16, O.SUM, (1 << 18) + 5, 10), (AR, O.FP32, O.SUM, 4099, 9),
 ]
 UNALIGNED_CASE = CASES.index((AR, O.FP32, O.SUM, 250001))
 ROOT = 1
@@ -112,7 +116,13 @@ def _rank_main(rank, n, port, q):
                     special = dtype in (O.INT64, O.UINT64, O.FP64) or op == O.PROD
                     nbytes = count * O.NP_STORAGE[dtype]().itemsize
                     fam = H.select_algo(kind, n, nbytes, special)
-                want = R.expected(kind, fam, dtype, op, xs, count, root=ROOT % n)[rank]
+                if forced == 10:
+                    es = O.NP_STORAGE[dtype]().itemsize
+                    variant, group = R.aiv_select(kind, n, count, es, dtype in (O.UINT64, O.FP64), op == O.PROD)
+                    want = (R.allreduce_aiv(dtype, op, xs, variant, group) if kind == AR
+                            else R.reduce_scatter_aiv(dtype, op, xs, count, variant))[rank]
+                else:
+                    want = R.expected(kind, fam, dtype, op, xs, count, root=ROOT % n)[rank]
                 ok = O.equal_bits(dtype, got, want)
             progress.write(f"case {i} done status {status} algo {comm.last_algo} ok {ok}\n")
             results.append((i, status, comm.last_algo, ok))

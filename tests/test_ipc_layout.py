@@ -14,9 +14,10 @@ STG_BYTES = 128 << 20  # kIpcStagingBytes (slot area and result area each)
 BLOCKS = 128           # kIpcBlocks
 AR, RS, RED = 0, 1, 2
 AR1, RED1, ARMC = 3, 4, 5  # one-shot AllReduce, one-shot Reduce, MeshChunk AllReduce (order O6, unaligned ceil)
+ARBAL = 6  # AIV large-core two-shot AllReduce: group * n balanced slices, rank c owning [c*group, (c+1)*group)
 
 
-def geometry(kind, n, count, es):
+def geometry(kind, n, count, es, group=1):
     """RunIpcCollective for one launch: (chunks [(start, len)] in input coordinates, piece, block elems, rounds).
     AllReduce: ceil(count/n) rounded to 128 B; ReduceScatter: the blocks; Reduce: the balanced two-shot split;
     one-shot kinds: every chunk is the whole range; MeshChunk AllReduce: ceil(count/n) without alignment."""
@@ -28,9 +29,11 @@ def geometry(kind, n, count, es):
         chunks = [(min(count, c * cs), max(0, min(count, c * cs + cs) - min(count, c * cs))) for c in range(n)]
     elif kind == RS:
         chunks = [(c * count, count) for c in range(n)]
-    elif kind == RED:
-        base, rem = divmod(count, n)
-        chunks = [(c * base + min(c, rem), base + (1 if c < rem else 0)) for c in range(n)]
+    elif kind in (RED, ARBAL):
+        # kIpcGeomBalanced: group * n slices, chunk c = slices [c*group, (c+1)*group) (Reduce two-shot: group 1)
+        g = group if kind == ARBAL else 1
+        base, rem = divmod(count, g * n)
+        chunks = [(c * g * base + min(c * g, rem), g * base + max(0, min(g, rem - c * g))) for c in range(n)]
     else:
         align = 128 // es
         cs = -(-(-(-count // n)) // align) * align
@@ -207,9 +210,10 @@ def test_ipc_allgather_multi_round():
     check_allgather(n, count, 4, vec=True, blocks=default_blocks(n * count * 4))
 
 
-def check(kind, n, count, es, vec, root=0):
+def check(kind, n, count, es, vec, root=0, group=1):
     v = 16 // es
-    chunks, piece, block, rounds = geometry(kind, n, count, es)
+    chunks, piece, block, rounds = geometry(kind, n, count, es, group)
+    two_shot = kind in (AR, ARBAL)
     total = n * count if kind == RS else count
     out_len = count
     assert n * piece <= STG_BYTES // es
@@ -234,7 +238,7 @@ def check(kind, n, count, es, vec, root=0):
                         if c != me:
                             assert me * piece + a1 <= n * piece          # owner c's slot me
                             cover[0][g0:g1] += 1
-                            if kind == AR or (kind == RED and me == root):
+                            if two_shot or (kind == RED and me == root):
                                 assert c * piece + a1 <= n * piece       # my result area, chunk c
                                 assert g1 <= out_len
                                 cover[2][g0:g1] += 1
@@ -255,7 +259,7 @@ def check(kind, n, count, es, vec, root=0):
                 assert np.all(cover[1][seg] == 1), (me, c)
             else:
                 assert np.all(cover[0][seg] == 1), (me, c)
-                if kind == AR or (kind == RED and me == root):
+                if two_shot or (kind == RED and me == root):
                     assert np.all(cover[2][seg] == 1), (me, c)
         if kind != RS:
             assert sum(cl for _, cl in chunks) == count  # the chunks tile the launch exactly
@@ -276,6 +280,16 @@ def test_ipc_multi_round_geometry(kind, n, count):
     chunks, piece, block, rounds = geometry(kind, n, count, 4)
     assert rounds >= 2
     check(kind, n, count, 4, vec=True, root=1)
+
+
+@pytest.mark.parametrize("n,group", [(2, 22), (4, 8), (8, 4), (8, 1), (16, 1)])
+@pytest.mark.parametrize("es", [1, 2, 4, 8])
+@pytest.mark.parametrize("count", [1, 5, 33, 4099, 100003, 1 << 20])
+def test_ipc_aiv_balanced_groups_in_bounds_and_exact_cover(n, group, es, count):
+    """The AIV large-core two-shot's chunks (group * n balanced slices per loop, group = (blocks - n) / n for the
+    default 48 vector cores: 22 at n = 2, 8 at n = 4, 4 at n = 8): chunk starts fall anywhere."""
+    check(ARBAL, n, count, es, vec=True, group=group)
+    check(ARBAL, n, count, es, vec=False, group=group)
 
 
 def test_old_element_loop_start_is_caught():
