@@ -75,8 +75,8 @@ __host__ __device__ constexpr bool SingleBarrierKind(uint32_t kind)
 // full and blockIdx.y is the rank.
 //
 // Geometry (elements): chunk c of the input starts at c * chunkStride and holds min(chunkLen, total - c*chunkStride)
-// elements (clamped at 0), or, balanced (the two-shot Reduce's split), starts at c*chunkLen + min(c, rem) and holds
-// chunkLen + (c < rem); rank c owns chunk c. The one-shot kinds use chunkStride = 0, chunkLen = total: every "chunk"
+// elements (clamped at 0), or, balanced (group * n slices of chunkLen, the first rem one longer; chunk c = slices
+// [c*group, (c+1)*group)), as the fields below say; rank c owns chunk c. The one-shot kinds use chunkStride = 0, chunkLen = total: every "chunk"
 // is the whole range and every rank owns it. Round k handles piece k of every chunk: chunk elements
 // [k*piece, (k+1)*piece). Block b always handles piece coordinates [b*blockElems, (b+1)*blockElems), so every round
 // of a launch touches the same slot and result addresses per block and the per-block barrier is sound.
@@ -122,7 +122,7 @@ struct IpcArgs {
 HcclResult LaunchIpcCollective(const IpcArgs& a, uint32_t blocks, uint32_t worldRanks, HcclDataType dt,
                               HcclReduceOp op, hipStream_t stream);
 
-// Evicts every line of every XCD's L2 (and writes back the dirty ones); synchronous on `stream`.
+// Writes back and invalidates every XCD's L2 at system scope (one maintenance block per CU); synchronous on `stream`.
 HcclResult ScrubL2(hipStream_t stream);
 
 // Per-communicator state of the IPC path.

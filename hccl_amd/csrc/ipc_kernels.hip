@@ -70,11 +70,15 @@ __device__ __forceinline__ bool Barrier(const IpcArgs& a, FlagLane fl, uint32_t 
     const uint32_t t = threadIdx.x;
     if (t < a.n) {
         if (t == 0) failed = 0;  // every thread read the previous barrier's value before the __syncthreads above
-        // The system-scope release store below writes the L2 back first (buffer_wbl2 sc0 sc1). Every wave of the
-        // block has drained its stores (vmcnt(0)) before the workgroup barrier, so that write-back covers the
-        // whole block's data. A separate __threadfence_system() here only added a second write-back and an
-        // invalidate per barrier.
-        __hip_atomic_store(fl.remote, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        // System-scope release: the L2 write-back (buffer_wbl2 sc0 sc1). Every wave of the block has drained its
+        // stores (vmcnt(0)) before the workgroup barrier, so the write-back covers the whole block's data. The flag
+        // store must wait for the write-back, and ROCm 7.2 drops that s_waitcnt vmcnt(0) where it can prove the
+        // wave's counter empty (MI355X_MICROARCH.md, "Compiler hazard"): the release store form lost it in 8 of the
+        // 73 instantiations (the epoch load before it is a waited load), so a peer could read the data before it
+        // left this XCD's L2. The explicit wait, invisible to that pass, keeps the flag behind the write-back.
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(fl.remote, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         uint32_t* mine = fl.mine;
         uint32_t polls = 0;
         bool cut = false;
@@ -504,41 +508,33 @@ hipError_t LaunchIpcT(int op, const IpcArgs& a, dim3 grid, hipStream_t s)
     return hipGetLastError();
 }
 
-// L2 scrub for a fresh staging allocation. Its pages may have belonged to a freed cached (MTYPE RW) buffer whose lines
-// still sit in some XCD's L2; the uncached accesses of the protocol do not see through them reliably (observed: a
-// barrier flag read back from a stale line, phase 2 then copying the previous owner's bytes). Every block streams
-// its share of a buffer many times the L2 size through the normal cached path, which evicts every older line (dirty
-// ones are written back), and then writes back its XCD's L2 (system-scope release).
-__global__ __launch_bounds__(256) void k_l2_scrub(const u32x4* p, uint64_t nvec, uint32_t* sink)
-{
-    u32x4 acc = {0, 0, 0, 0};
-    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < nvec; i += uint64_t(gridDim.x) * 256) acc ^= p[i];
-    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u && threadIdx.x == 0) sink[0] = 1;  // keeps the loads
-    __threadfence_system();
-}
-
+// Cache maintenance for a fresh staging allocation: every XCD's L2 written back and invalidated at system scope
+// (buffer_wbl2 sc0 sc1, buffer_inv sc0 sc1), so that no line a freed buffer left in some L2 is read or written back
+// over the new staging. Blocks are dealt round-robin over the XCDs (MI355X_MICROARCH.md, workgroup dispatch): one
+// block per CU reaches every L2. Until r01 this was a 512 MiB stream through the cached path (probabilistic eviction,
+// ~190 us); the r01 stale-operand failure it was added for no longer reproduces without any maintenance, and the
+// barrier's dropped write-back wait (Barrier above) is the fault the symptom fits.
 }  // namespace
+
+__global__ __launch_bounds__(64) void k_l2_maintain()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 
 HcclResult ScrubL2(hipStream_t stream)
 {
-    constexpr uint64_t kBytes = 512ull << 20;  // 64 MiB per XCD: 16 x its 4 MiB L2
-    void* buf = nullptr;
-    uint32_t* sink = nullptr;
-    HIP_CHK(hipMalloc(&buf, kBytes + 256));
-    sink = reinterpret_cast<uint32_t*>(static_cast<char*>(buf) + kBytes);
     int cus = 256;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
         cus = 256;
     }
-    hipLaunchKernelGGL(k_l2_scrub, dim3(uint32_t(cus) * 4), dim3(256), 0, stream, static_cast<const u32x4*>(buf),
-                       kBytes / 16, sink);
+    hipLaunchKernelGGL(k_l2_maintain, dim3(uint32_t(cus)), dim3(64), 0, stream);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
-    (void)hipFree(buf);
     if (e != hipSuccess) {
-        HCCL_AMD_ERR("L2 scrub failed: %s", hipGetErrorString(e));
+        HCCL_AMD_ERR("L2 maintenance failed: %s", hipGetErrorString(e));
         return HCCL_E_RUNTIME;
     }
     return HCCL_SUCCESS;
