@@ -16,6 +16,7 @@ from ._lib import (  # noqa: F401
     Algo,
     AivVariant,
     HcclAmdIrOp,
+    HcclAmdUnitPlan,
     HcclDataType,
     HcclError,
     HcclReduceOp,
@@ -134,6 +135,17 @@ def select_aiv_algo(op_type: int, n_ranks: int, count: int, dtype: int, op: int,
     v = lib.HcclAmdSelectAivAlgo(int(op_type), n_ranks, count, int(dtype), int(op), core_limit, 1 if strict else 0,
                                  ctypes.byref(g))
     return AivVariant(v), g.value
+
+
+def executor_plan(ops, nops: int, elem_size: int, bases=(1 << 40, 2 << 40, 3 << 40)):
+    """HcclAmdExecutorPlan: the executor's units for an IR program (from build_schedule), as a list of dicts."""
+    base = (ctypes.c_uint64 * 3)(*bases)
+    n = ctypes.c_uint64(0)
+    check("HcclAmdExecutorPlan", lib.HcclAmdExecutorPlan(ops, nops, elem_size, base, None, 0, ctypes.byref(n)))
+    units = (HcclAmdUnitPlan * max(1, n.value))()
+    check("HcclAmdExecutorPlan", lib.HcclAmdExecutorPlan(ops, nops, elem_size, base, units, n.value, ctypes.byref(n)))
+    return [{"stream": u.stream, "comm": bool(u.isComm), "first": u.firstOp, "num": u.numOps, "wait": u.waitUnit}
+            for u in units[:n.value]]
 
 
 def ring_table(n_ranks: int) -> List[List[int]]:

@@ -127,6 +127,16 @@ class HcclAmdIrOp(ctypes.Structure):
     ]
 
 
+class HcclAmdUnitPlan(ctypes.Structure):
+    _fields_ = [
+        ("stream", ctypes.c_int32),
+        ("isComm", ctypes.c_int32),
+        ("firstOp", ctypes.c_uint64),
+        ("numOps", ctypes.c_uint64),
+        ("waitUnit", ctypes.c_int64),
+    ]
+
+
 class HcclRootInfo(ctypes.Structure):
     _fields_ = [("internal", ctypes.c_char * HCCL_ROOT_INFO_BYTES)]
 
@@ -167,6 +177,8 @@ SIGNATURES = {
         [_i32, _i32, _u32, _u32, _u64, _i32, _u32, _u64, ctypes.POINTER(HcclAmdIrOp), _u64,
          ctypes.POINTER(_u64), ctypes.POINTER(_i32), ctypes.POINTER(_u64)],
     ),
+    "HcclAmdExecutorPlan": (_res, [ctypes.POINTER(HcclAmdIrOp), _u64, _u32, ctypes.POINTER(_u64),
+                                   ctypes.POINTER(HcclAmdUnitPlan), _u64, ctypes.POINTER(_u64)]),
     "HcclAmdCommInitLoopback": (_res, [_u32, ctypes.POINTER(_vp)]),
     "HcclAmdCommSetAlgo": (_res, [_vp, _i32]),
     "HcclAmdCommSetPieceBytes": (_res, [_vp, _u64]),

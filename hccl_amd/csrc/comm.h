@@ -130,6 +130,18 @@ uint64_t ScratchBytesDefault();
 HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const bufs[3], HcclDataType dt,
                    HcclReduceOp op, hipStream_t user, bool singleStream = false);
 
+// The executor's units for one rank's IR (Execute issues exactly these): a transport group (link stream 0) or a
+// batch of folds / a copy (reduce stream 1), each with the unit of the other stream it must wait for (the latest whose
+// byte ranges conflict with it, RAW / WAR / WAW on absolute addresses), or -1.
+struct UnitPlan {
+    int stream = 0;
+    bool isComm = false;
+    size_t first = 0;  // IR records [first, first + count)
+    size_t count = 0;
+    int64_t waitUnit = -1;
+};
+std::vector<UnitPlan> PlanUnits(const std::vector<HcclAmdIrOp>& ops, void* const bufs[3], uint64_t es);
+
 // Collectives whose per-rank payload is at most this many bytes run single-stream (HCCL_AMD_SINGLE_STREAM_BYTES,
 // default 1 MiB).
 uint64_t SingleStreamBytes();

@@ -24,12 +24,6 @@ struct Range {
     bool write;
 };
 
-struct Unit {
-    int stream;  // 0 = link, 1 = reduce
-    hipEvent_t ev;
-    std::vector<Range> ranges;
-};
-
 bool Conflicts(const std::vector<Range>& a, const std::vector<Range>& b)
 {
     for (const Range& x : a) {
@@ -142,6 +136,67 @@ static HcclResult ExecuteSingleStream(Comm& c, const std::vector<HcclAmdIrOp>& o
     return HCCL_SUCCESS;
 }
 
+std::vector<UnitPlan> PlanUnits(const std::vector<HcclAmdIrOp>& ops, void* const bufs[3], uint64_t es)
+{
+    auto addr = [&](int32_t buf, uint64_t off) -> uintptr_t {
+        return reinterpret_cast<uintptr_t>(bufs[buf]) + off * es;
+    };
+    std::vector<UnitPlan> plan;
+    std::vector<std::vector<Range>> ranges;
+    std::vector<size_t> onStream[2];
+    // synced[x][y]: index into onStream[y] of the last unit stream x has already waited for (+1)
+    size_t synced[2][2] = {{0, 0}, {0, 0}};
+    size_t i = 0;
+    while (i < ops.size()) {
+        UnitPlan u;
+        std::vector<Range> rg;
+        u.first = i;
+        const HcclAmdIrOp& first = ops[i];
+        u.isComm = first.kind == HCCL_AMD_IR_SEND || first.kind == HCCL_AMD_IR_RECV;
+        u.stream = u.isComm ? 0 : 1;
+        if (u.isComm) {
+            const int32_t g = first.group;
+            while (i < ops.size() && (ops[i].kind == HCCL_AMD_IR_SEND || ops[i].kind == HCCL_AMD_IR_RECV) &&
+                   ops[i].group == g) {
+                const HcclAmdIrOp& o = ops[i];
+                const uint64_t bytes = o.count * es;
+                const uintptr_t a = o.kind == HCCL_AMD_IR_SEND ? addr(o.srcBuf[0], o.srcOff[0]) : addr(o.dstBuf, o.dstOff);
+                rg.push_back({a, a + bytes, o.kind == HCCL_AMD_IR_RECV});
+                ++i;
+            }
+        } else {
+            const size_t batch = BatchRun(ops, i, es, bufs);
+            for (size_t g = 0; g < batch; ++g) {
+                const HcclAmdIrOp& o = ops[i + g];
+                const uint64_t bytes = o.count * es;
+                const uintptr_t d = addr(o.dstBuf, o.dstOff);
+                rg.push_back({d, d + bytes, true});
+                for (int j = 0; j < o.nsrc; ++j) {
+                    const uintptr_t sa = addr(o.srcBuf[j], o.srcOff[j]);
+                    rg.push_back({sa, sa + bytes, false});
+                }
+            }
+            i += batch;
+        }
+        u.count = i - u.first;
+        // cross-stream hazards: wait for the latest conflicting unit on the other stream
+        const int x = u.stream;
+        const int y = 1 - x;
+        for (size_t k = onStream[y].size(); k > synced[x][y]; --k) {
+            const size_t prior = onStream[y][k - 1];
+            if (Conflicts(ranges[prior], rg)) {
+                u.waitUnit = static_cast<int64_t>(prior);
+                synced[x][y] = k;
+                break;
+            }
+        }
+        onStream[x].push_back(plan.size());
+        plan.push_back(u);
+        ranges.push_back(std::move(rg));
+    }
+    return plan;
+}
+
 HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const bufs[3], HcclDataType dt,
                    HcclReduceOp op, hipStream_t user, bool singleStream)
 {
@@ -159,71 +214,25 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
         return reinterpret_cast<uintptr_t>(bufs[buf]) + off * es;
     };
 
-    std::vector<Unit> units;
-    units.reserve(ops.size());
-    std::vector<size_t> onStream[2];
-    // synced[x][y]: index into onStream[y] of the last unit stream x has already waited for (+1)
-    size_t synced[2][2] = {{0, 0}, {0, 0}};
+    const std::vector<UnitPlan> plan = PlanUnits(ops, bufs, es);
+    std::vector<hipEvent_t> evs(plan.size(), nullptr);
     bool used[2] = {false, false};
-
-    size_t i = 0;
     std::vector<P2pOp> p2p;
-    while (i < ops.size()) {
-        Unit u;
-        p2p.clear();
-        const size_t firstIdx = i;
-        size_t batch = 1;
-        const HcclAmdIrOp& first = ops[i];
-        const bool isComm = first.kind == HCCL_AMD_IR_SEND || first.kind == HCCL_AMD_IR_RECV;
-        u.stream = isComm ? 0 : 1;
-        if (isComm) {
-            const int32_t g = first.group;
-            while (i < ops.size() && (ops[i].kind == HCCL_AMD_IR_SEND || ops[i].kind == HCCL_AMD_IR_RECV) &&
-                   ops[i].group == g) {
-                const HcclAmdIrOp& o = ops[i];
-                const uint64_t bytes = o.count * es;
-                if (o.kind == HCCL_AMD_IR_SEND) {
-                    uintptr_t a = addr(o.srcBuf[0], o.srcOff[0]);
-                    u.ranges.push_back({a, a + bytes, false});
-                    p2p.push_back({true, static_cast<uint32_t>(o.peer), reinterpret_cast<void*>(a), bytes});
-                } else {
-                    uintptr_t a = addr(o.dstBuf, o.dstOff);
-                    u.ranges.push_back({a, a + bytes, true});
-                    p2p.push_back({false, static_cast<uint32_t>(o.peer), reinterpret_cast<void*>(a), bytes});
-                }
-                ++i;
-            }
-        } else {
-            batch = BatchRun(ops, i, es, bufs);
-            for (size_t g = 0; g < batch; ++g) {
-                const HcclAmdIrOp& o = ops[i + g];
-                const uint64_t bytes = o.count * es;
-                uintptr_t d = addr(o.dstBuf, o.dstOff);
-                u.ranges.push_back({d, d + bytes, true});
-                for (int j = 0; j < o.nsrc; ++j) {
-                    uintptr_t s = addr(o.srcBuf[j], o.srcOff[j]);
-                    u.ranges.push_back({s, s + bytes, false});
-                }
-            }
-            i += batch;
-        }
-
-        // cross-stream hazards: wait for the latest conflicting unit on the other stream
+    for (size_t ui = 0; ui < plan.size(); ++ui) {
+        const UnitPlan& u = plan[ui];
         const int x = u.stream;
-        const int y = 1 - x;
-        for (size_t k = onStream[y].size(); k > synced[x][y]; --k) {
-            const Unit& prior = units[onStream[y][k - 1]];
-            if (Conflicts(prior.ranges, u.ranges)) {
-                HIP_CHK(hipStreamWaitEvent(streams[x], prior.ev, 0));
-                synced[x][y] = k;
-                break;
+        if (u.waitUnit >= 0) HIP_CHK(hipStreamWaitEvent(streams[x], evs[size_t(u.waitUnit)], 0));
+        if (u.isComm) {
+            p2p.clear();
+            for (size_t k = u.first; k < u.first + u.count; ++k) {
+                const HcclAmdIrOp& o = ops[k];
+                const bool send = o.kind == HCCL_AMD_IR_SEND;
+                const uintptr_t a = send ? addr(o.srcBuf[0], o.srcOff[0]) : addr(o.dstBuf, o.dstOff);
+                p2p.push_back({send, static_cast<uint32_t>(o.peer), reinterpret_cast<void*>(a), o.count * es});
             }
-        }
-
-        if (isComm) {
             HCCL_CHK(c.transport->Group(p2p, streams[x]));
         } else {
-            const HcclAmdIrOp& o = first;
+            const HcclAmdIrOp& o = ops[u.first];
             void* dst = reinterpret_cast<void*>(addr(o.dstBuf, o.dstOff));
             if (o.kind == HCCL_AMD_IR_COPY) {
                 const void* src = reinterpret_cast<const void*>(addr(o.srcBuf[0], o.srcOff[0]));
@@ -231,16 +240,14 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
                     HIP_CHK(hipMemcpyAsync(dst, src, o.count * es, hipMemcpyDeviceToDevice, streams[x]));
                 }
             } else if (o.kind == HCCL_AMD_IR_REDUCE) {
-                HCCL_CHK(LaunchFolds(ops, firstIdx, batch, es, bufs, dt, op, streams[x]));
+                HCCL_CHK(LaunchFolds(ops, u.first, u.count, es, bufs, dt, op, streams[x]));
             } else {
                 return HCCL_E_INTERNAL;
             }
         }
-        HCCL_CHK(c.NextEvent(&u.ev));
-        HIP_CHK(hipEventRecord(u.ev, streams[x]));
+        HCCL_CHK(c.NextEvent(&evs[ui]));
+        HIP_CHK(hipEventRecord(evs[ui], streams[x]));
         used[x] = true;
-        onStream[x].push_back(units.size());
-        units.push_back(std::move(u));
     }
 
     for (int s = 0; s < 2; ++s) {

@@ -374,6 +374,28 @@ int32_t HcclAmdRhdTable(uint32_t nRanks, uint32_t* realOfVirtual, uint32_t capac
     return static_cast<int32_t>(t.size());
 }
 
+HcclResult HcclAmdExecutorPlan(const HcclAmdIrOp* ops, uint64_t numOps, uint32_t elemSize, const uint64_t* bufBase,
+                               HcclAmdUnitPlan* units, uint64_t capacity, uint64_t* numUnits)
+{
+    if ((ops == nullptr && numOps != 0) || bufBase == nullptr || numUnits == nullptr) return HCCL_E_PTR;
+    if (elemSize == 0) return HCCL_E_PARA;
+    const std::vector<HcclAmdIrOp> v(ops, ops + numOps);
+    void* bufs[3];
+    for (int i = 0; i < 3; ++i) bufs[i] = reinterpret_cast<void*>(static_cast<uintptr_t>(bufBase[i]));
+    const std::vector<UnitPlan> plan = PlanUnits(v, bufs, elemSize);
+    *numUnits = plan.size();
+    if (units == nullptr) return HCCL_SUCCESS;
+    if (capacity < plan.size()) return HCCL_E_PARA;
+    for (size_t i = 0; i < plan.size(); ++i) {
+        units[i].stream = plan[i].stream;
+        units[i].isComm = plan[i].isComm ? 1 : 0;
+        units[i].firstOp = plan[i].first;
+        units[i].numOps = plan[i].count;
+        units[i].waitUnit = plan[i].waitUnit;
+    }
+    return HCCL_SUCCESS;
+}
+
 int32_t HcclAmdSelectAivAlgo(int32_t opType, uint32_t nRanks, uint64_t count, HcclDataType dataType, HcclReduceOp op,
                              uint32_t coreLimit, int32_t strict, uint32_t* groupSize)
 {

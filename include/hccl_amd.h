@@ -155,6 +155,21 @@ extern int32_t HcclAmdRingTable(uint32_t nRanks, uint32_t* cycles, uint32_t capa
  * `capacity` instances. Returns the number of instances (0 when nRanks is not a power of two or exceeds 16). */
 extern int32_t HcclAmdRhdTable(uint32_t nRanks, uint32_t* realOfVirtual, uint32_t capacity);
 
+/* The executor's plan for one rank's IR, without running it (host only; what Execute issues on the GPU): units in
+ * issue order, each a transport group (stream 0, the link stream) or a batch of folds / a copy (stream 1, the reduce
+ * stream), with the unit of the other stream it waits for (hipStreamWaitEvent), derived from RAW / WAR / WAW conflicts
+ * of the units' byte ranges at the buffer base addresses bufBase[HcclAmdBuf] (equal bases model in-place calls). */
+typedef struct {
+    int32_t stream;   /* 0 = link, 1 = reduce */
+    int32_t isComm;   /* 1: SEND/RECV group */
+    uint64_t firstOp; /* IR records [firstOp, firstOp + numOps) */
+    uint64_t numOps;
+    int64_t waitUnit; /* unit index on the other stream, or -1 */
+} HcclAmdUnitPlan;
+extern HcclResult HcclAmdExecutorPlan(const HcclAmdIrOp* ops, uint64_t numOps, uint32_t elemSize,
+                                      const uint64_t* bufBase, HcclAmdUnitPlan* units, uint64_t capacity,
+                                      uint64_t* numUnits);
+
 /* ---------------------------------------------------------------- communicator extensions */
 
 /* nRanks communicators on the current HIP device, joined by device-to-device copies. comms[r] is rank r.

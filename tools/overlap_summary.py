@@ -82,6 +82,7 @@ def main():
     red = [(s, e) for c, s, e in iv if c == "reduce"]
     lnk = [(s, e) for c, s, e in iv if c == "link"]
     ur, ul = _union(red), _union(lnk)
+    ua = _union(red + lnk)
     span = (max(e for _, _, e in iv) - min(s for _, s, _ in iv)) if iv else 0
     res = {
         "reduce_kernels": len(red), "reduce_busy_us": round(_length(ur) / 1e3, 1),
@@ -89,6 +90,10 @@ def main():
         "reduce_under_link_us": round(_intersect(ur, ul) / 1e3, 1),
         "reduce_hidden_frac": round(_intersect(ur, ul) / max(1, _length(ur)), 3),
         "span_us": round(span / 1e3, 1),
+        # GPU-side work (reduce kernels or link copies) in flight, as a fraction of the span: low means the GPU
+        # waited on the host (the loopback transport's per-group rendezvous between the rank threads)
+        "gpu_busy_frac": round(_length(ua) / max(1, span), 3),
+        "idle_gaps_over_50us": sum(1 for a0, a1 in zip(ua, ua[1:]) if a1[0] - a0[1] > 50000),
         "sources": [os.path.relpath(p, a.out_dir) for p in kt + mt],
     }
     print(json.dumps(res))

@@ -14,19 +14,22 @@ import hccl_amd as H  # noqa: E402
 
 
 def main():
-    os.environ.setdefault("HCCL_BUFFSIZE", "16")  # MeshChunk loops of 8 MiB: eight pipelined units per call
-    n, count = 8, (64 << 20) // 4
+    # TRACE_MIB per rank (default 64) and TRACE_ALGO (default MESH_CHUNK); HCCL_BUFFSIZE 16 by default (MeshChunk
+    # loops of 8 MiB: eight pipelined units per call), set it to 200 for the reference's own loop sizes
+    os.environ.setdefault("HCCL_BUFFSIZE", "16")
+    n, count = 8, (int(os.environ.get("TRACE_MIB", "64")) << 20) // 4
+    algo = H.Algo[os.environ.get("TRACE_ALGO", "MESH_CHUNK")]
     torch.cuda.set_device(0)
     comms = H.loopback_world(n)
     sends = [torch.rand(count, device="cuda") for _ in range(n)]
     recvs = [torch.empty_like(s) for s in sends]
     streams = [torch.cuda.Stream() for _ in range(n)]
     for c in comms:
-        c.set_algo(H.Algo.MESH_CHUNK)
+        c.set_algo(algo)
     torch.cuda.synchronize()
 
     def body(r):
-        for _ in range(3):
+        for _ in range(int(os.environ.get("TRACE_CALLS", "3"))):
             comms[r].all_reduce(sends[r], recvs[r], H.HcclReduceOp.SUM, streams[r])
 
     th = [threading.Thread(target=body, args=(r,)) for r in range(n)]
