@@ -272,7 +272,7 @@ def bench_local(args) -> dict:
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": load_pmc_traffic("r01_pmc_local_reduce.json"),
+            "traffic": load_pmc_traffic("r02_pmc_local_reduce.json"),
             "kernel": "k_reduce2<EFp<float>, SUM>",
             "algorithmic_bytes_per_launch": bytes_step,
             "kernel_avg_us": round(kavg * 1e6, 2),
