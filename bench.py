@@ -644,18 +644,21 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    if harness:
-        def _all_gather(b):
-            out = [None] * world
-            dist.all_gather_object(out, b)
-            return out
 
-        comm = H.comm_init_host_exchange(world, rank, _all_gather)
-    else:
+    def _all_gather(b):
+        out = [None] * world
+        dist.all_gather_object(out, b)
+        return out
+
+    def new_comm():
+        if harness:
+            return H.comm_init_host_exchange(world, rank, _all_gather)
         # root info out of band, exactly as the reference's callers do (examples/.../01_allreduce/main.cc:122-136)
         obj = [H.get_root_info() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        comm = H.comm_init_root_info(world, obj[0], rank)
+        return H.comm_init_root_info(world, obj[0], rank)
+
+    comm = new_comm()
     count = C3_BYTES // 4
     g = torch.Generator(device=dev).manual_seed(0x5EED0003 + rank)
     send = torch.rand(count, device=dev, generator=g).mul_(2).sub_(1)
@@ -689,18 +692,9 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     xgmi_peak = min(world - 1, 7) * XGMI_LINK_GBPS
     value = world * C3_BYTES * args.steps / elapsed / GIB
     algo = comm.last_algo
-    extra = {}
-    if not args.no_extra_configs:
-        for name, fn in (("c3_schedules", lambda: bench_c3_algos(comm, send, recv, world)),
-                         ("c4", lambda: bench_c4(comm, send, recv, world)),
-                         ("c5", lambda: bench_c5(comm, send, recv, world)),
-                         ("end_to_end_host_buffers", lambda: bench_e2e_allreduce(comm, world))):
-            try:
-                extra[name] = fn()
-            except Exception as e:  # noqa: BLE001  (a secondary config never hides the headline line)
-                extra[name] = {"error": f"{type(e).__name__}: {e}"}
-    # correctness of the measured path at the measured size: integer-valued inputs make every order exact, so the
-    # timed schedule must return exactly sum_r((i % 251) + r) on every rank (checked on the GPU, AND over ranks)
+    # correctness of the measured path at the measured size, right after the timed region and before anything else
+    # runs on the communicator: integer-valued inputs make every order exact, so the timed schedule must return
+    # exactly sum_r((i % 251) + r) on every rank (checked on the GPU, AND over ranks)
     check = torch.arange(count, device=dev, dtype=torch.int64) % 251
     send.copy_(check + rank)
     comm.set_algo(headline)
@@ -712,6 +706,28 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     result_ok = bool(ok.item())
     del check
     comm.destroy()
+    g = torch.Generator(device=dev).manual_seed(0x5EED0003 + rank)
+    send.copy_(torch.rand(count, device=dev, generator=g).mul_(2).sub_(1))
+    extra = {}
+    if not args.no_extra_configs:
+        # Each secondary config gets a communicator of its own: a failure in one (say an IPC barrier timeout, after
+        # which the communicator answers HCCL_E_SUSPENDING) cannot take the others, or the headline, with it.
+        for name, fn in (("c3_schedules", lambda cm: bench_c3_algos(cm, send, recv, world)),
+                         ("c4", lambda cm: bench_c4(cm, send, recv, world)),
+                         ("c5", lambda cm: bench_c5(cm, send, recv, world)),
+                         ("end_to_end_host_buffers", lambda cm: bench_e2e_allreduce(cm, world))):
+            cm = None
+            try:
+                cm = new_comm()
+                extra[name] = fn(cm)
+            except Exception as e:  # noqa: BLE001  (a secondary config never hides the headline line)
+                extra[name] = {"error": f"{type(e).__name__}: {e}"}
+            finally:
+                if cm is not None:
+                    try:
+                        cm.destroy()
+                    except Exception as e:  # noqa: BLE001
+                        extra.setdefault(name, {})["destroy_error"] = f"{type(e).__name__}: {e}"
     rccl_ref = None
     if not args.no_rccl_ref:
         rccl_ref = rccl_allreduce_reference(send, recv, world, args)

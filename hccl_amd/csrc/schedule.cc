@@ -579,19 +579,20 @@ void AllReduceRing(const ScheduleParams& p, Builder& b)
             }
         }
     }
+    // All-gather: received chunks land in recvBuf directly, so no staging bounds the granule, and there is no fold to
+    // pipeline against: every step moves whole chunks on all R rings at once (one transport group per step instead
+    // of one per staging piece, which saves a group launch per piece; tools/executor_overlap_model.py).
     for (uint32_t s = 0; s + 1 < n; ++s) {
-        for (uint64_t t = 0; t < np; ++t) {
-            for (uint32_t k = 0; k < R; ++k) {
-                const RingView& r = rings[k];
-                const uint32_t cs = (r.pos + n - s) % n;
-                const uint32_t cr = (r.pos + 2 * n - s - 1) % n;
-                const Span snd = Piece(chunkOf(k, cs), pe, t);
-                const Span rcv = Piece(chunkOf(k, cr), pe, t);
-                b.Send(r.Next(), Out(snd.begin), snd.len);
-                b.Recv(r.Prev(), Out(rcv.begin), rcv.len);
-            }
-            b.EndGroup();
+        for (uint32_t k = 0; k < R; ++k) {
+            const RingView& r = rings[k];
+            const uint32_t cs = (r.pos + n - s) % n;
+            const uint32_t cr = (r.pos + 2 * n - s - 1) % n;
+            const Span snd = chunkOf(k, cs);
+            const Span rcv = chunkOf(k, cr);
+            b.Send(r.Next(), Out(snd.begin), snd.len);
+            b.Recv(r.Prev(), Out(rcv.begin), rcv.len);
         }
+        b.EndGroup();
     }
 }
 
@@ -721,8 +722,9 @@ void AllReduceRhd(const ScheduleParams& p, Builder& b)
         first = false;
         if (d == 1) break;
     }
+    // Recursive doubling: the exchanged halves land in recvBuf directly (no staging, no fold), so every step moves
+    // whole regions in one transport group (as the ring's all-gather).
     for (uint32_t d = 1; d < n; d *= 2) {
-        const uint64_t np = std::max<uint64_t>(1, CeilDiv(range(inst[0], 0, d).len, pe));
         std::vector<Span> mine(R), theirs(R);
         std::vector<uint32_t> plo(R);
         for (uint32_t j = 0; j < R; ++j) {
@@ -732,16 +734,12 @@ void AllReduceRhd(const ScheduleParams& p, Builder& b)
             mine[j] = range(I, I.lo, I.lo + d);
             theirs[j] = range(I, plo[j], plo[j] + d);
         }
-        for (uint64_t t = 0; t < np; ++t) {
-            for (uint32_t j = 0; j < R; ++j) {
-                const uint32_t partner = inst[j].real[inst[j].v ^ d];
-                const Span mP = Piece(mine[j], pe, t);
-                const Span th = Piece(theirs[j], pe, t);
-                b.Send(partner, Out(mP.begin), mP.len);
-                b.Recv(partner, Out(th.begin), th.len);
-            }
-            b.EndGroup();
+        for (uint32_t j = 0; j < R; ++j) {
+            const uint32_t partner = inst[j].real[inst[j].v ^ d];
+            b.Send(partner, Out(mine[j].begin), mine[j].len);
+            b.Recv(partner, Out(theirs[j].begin), theirs[j].len);
         }
+        b.EndGroup();
         for (uint32_t j = 0; j < R; ++j) inst[j].lo = std::min(inst[j].lo, plo[j]);
     }
 }

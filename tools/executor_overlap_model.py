@@ -11,7 +11,8 @@ stream it waits for) for one rank's IR at the C3 shape, and replays it on a two-
 A unit starts when the previous unit of its stream and the unit it waits for have ended (every rank runs the same
 plan, so one rank's timeline stands for all). Reported per schedule: link and reduce totals, makespan, the reduce time
 that runs while a link unit is in flight (reduce_hidden_frac) and the makespan against the lower bound
-max(link total, reduce total).
+max(link total, reduce total); then the makespan again with an assumed launch cost per unit (15 us per transport
+group, 5 us per fold launch), which prices how many units the schedule issues.
 
   python tools/executor_overlap_model.py > profiles/r02_executor_overlap_model.jsonl
 """
@@ -24,9 +25,13 @@ import hccl_amd as H  # noqa: E402
 
 B_LINK = 76.8e9
 B_HBM = 6.0e12
+# launch cost per unit for the second timeline (assumed, not measured here: an RCCL grouped send/recv launch and a
+# fold kernel launch); it prices the number of units a schedule issues
+OVH_LINK = 15e-6
+OVH_REDUCE = 5e-6
 
 
-def simulate(ops, nops, es, units):
+def simulate(ops, nops, es, units, ovh_link=0.0, ovh_reduce=0.0):
     end = {0: 0.0, 1: 0.0}
     done = []
     spans = []
@@ -37,12 +42,12 @@ def simulate(ops, nops, es, units):
             for o in recs:
                 key = (o.peer, o.kind)
                 per_peer[key] = per_peer.get(key, 0) + o.count * es
-            dur = max(per_peer.values()) / B_LINK
+            dur = max(per_peer.values()) / B_LINK + ovh_link
         else:
             hbm = 0
             for o in recs:
                 hbm += (o.nsrc + 1) * o.count * es if o.kind == H.IrKind.REDUCE else 2 * o.count * es
-            dur = hbm / B_HBM
+            dur = hbm / B_HBM + ovh_reduce
         start = end[u["stream"]]
         if u["wait"] >= 0:
             start = max(start, done[u["wait"]])
@@ -72,6 +77,7 @@ def model(op_type, algo, n, count, dtype, rank=0):
     units = H.executor_plan(ops, nops, es)
     row = {"op": H.OpType(op_type).name, "algo": H.Algo(used).name, "ranks": n, "bytes_per_rank": count * es}
     row.update(simulate(ops, nops, es, units))
+    row["makespan_with_launch_cost_ms"] = simulate(ops, nops, es, units, OVH_LINK, OVH_REDUCE)["makespan_ms"]
     return row
 
 
