@@ -123,6 +123,21 @@ def build_schedule(op_type: int, algo: int, n_ranks: int, rank: int, count: int,
     return arr, nops.value, used.value, scratch.value
 
 
+def build_schedule_v(n_ranks: int, rank: int, counts: Sequence[int], displs: Sequence[int], dtype: int,
+                     piece_bytes: int = 0):
+    """ReduceScatterV schedule (HcclAmdBuildScheduleV): returns (ops, n_ops, scratch_elems)."""
+    c = (ctypes.c_uint64 * n_ranks)(*counts)
+    d = (ctypes.c_uint64 * n_ranks)(*displs)
+    nops = ctypes.c_uint64(0)
+    scratch = ctypes.c_uint64(0)
+    check("HcclAmdBuildScheduleV", lib.HcclAmdBuildScheduleV(n_ranks, rank, c, d, int(dtype), piece_bytes, None, 0,
+                                                             ctypes.byref(nops), ctypes.byref(scratch)))
+    arr = (HcclAmdIrOp * max(1, nops.value))()
+    check("HcclAmdBuildScheduleV", lib.HcclAmdBuildScheduleV(n_ranks, rank, c, d, int(dtype), piece_bytes, arr,
+                                                             nops.value, ctypes.byref(nops), ctypes.byref(scratch)))
+    return arr, nops.value, scratch.value
+
+
 def select_algo(op_type: int, n_ranks: int, nbytes: int, special: bool = False) -> int:
     """The algorithm HCCL_AMD_ALGO_AUTO picks (HcclAmdSelectAlgo)."""
     return lib.HcclAmdSelectAlgo(int(op_type), n_ranks, nbytes, 1 if special else 0)
@@ -197,6 +212,15 @@ class Comm:
     @property
     def last_algo(self) -> int:
         return lib.HcclAmdCommLastAlgo(self.handle)
+
+    def reduce_scatter_v(self, send: torch.Tensor, counts: Sequence[int], displs: Sequence[int], recv: torch.Tensor,
+                         op: int = HcclReduceOp.SUM, stream=None) -> None:
+        """HcclReduceScatterV: rank q's block of `send` is counts[q] elements at displs[q]."""
+        n = len(counts)
+        c = (ctypes.c_uint64 * n)(*counts)
+        d = (ctypes.c_uint64 * n)(*displs)
+        check("HcclReduceScatterV", lib.HcclReduceScatterV(_ptr(send), c, d, _ptr(recv), recv.numel(),
+                                                           hccl_dtype(recv), int(op), self.handle, _stream(stream)))
 
     def ipc_status(self) -> int:
         """Status word of the IPC path (bit 0: a cross-rank barrier timed out on the last IPC AllReduce)."""

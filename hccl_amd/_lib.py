@@ -99,6 +99,7 @@ class OpType(enum.IntEnum):
     REDUCE_SCATTER = 1
     REDUCE = 2
     ALLGATHER = 3
+    REDUCE_SCATTER_V = 4
 
 
 class IrKind(enum.IntEnum):
@@ -153,6 +154,7 @@ SIGNATURES = {
     "HcclAllReduce": (_res, [_vp, _vp, _u64, _i32, _i32, _vp, _vp]),
     "HcclReduceScatter": (_res, [_vp, _vp, _u64, _i32, _i32, _vp, _vp]),
     "HcclReduce": (_res, [_vp, _vp, _u64, _i32, _i32, _u32, _vp, _vp]),
+    "HcclReduceScatterV": (_res, [_vp, _vp, _vp, _vp, _u64, _i32, _i32, _vp, _vp]),
     "HcclAllGather": (_res, [_vp, _vp, _u64, _i32, _vp, _vp]),
     "HcclGetRootInfo": (_res, [ctypes.POINTER(HcclRootInfo)]),
     "HcclCommInitRootInfo": (_res, [_u32, ctypes.POINTER(HcclRootInfo), _u32, ctypes.POINTER(_vp)]),
@@ -169,6 +171,8 @@ SIGNATURES = {
     "HcclAmdDataTypeSize": (_u32, [_i32]),
     "HcclAmdGetErrorString": (ctypes.c_char_p, [_i32]),
     "HcclAmdSelectAlgo": (_i32, [_i32, _u32, _u64, _i32]),
+    "HcclAmdBuildScheduleV": (_res, [_u32, _u32, ctypes.POINTER(_u64), ctypes.POINTER(_u64), _i32, _u64,
+                                     ctypes.POINTER(HcclAmdIrOp), _u64, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     "HcclAmdSelectAivAlgo": (_i32, [_i32, _u32, _u64, _i32, _i32, _u32, _i32, ctypes.POINTER(_u32)]),
     "HcclAmdRingTable": (_i32, [_u32, ctypes.POINTER(_u32), _u32]),
     "HcclAmdRhdTable": (_i32, [_u32, ctypes.POINTER(_u32), _u32]),

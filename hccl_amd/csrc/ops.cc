@@ -147,6 +147,41 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     return Execute(c, s.ops, bufs, dt, op, stream, payload <= SingleStreamBytes());
 }
 
+// ReduceScatterV (reduce_scatter_v_op.cc:24-83, ReduceScatterVOutPlaceCommon :285-330): the mesh template's order
+// over per-rank blocks; the output holds counts[rank] elements.
+HcclResult RunReduceScatterV(Comm& c, void* sendBuf, const uint64_t* counts, const uint64_t* displs, void* recvBuf,
+                             HcclDataType dt, HcclReduceOp op, hipStream_t stream)
+{
+    std::lock_guard<std::mutex> lk(c.mu);
+    HCCL_CHK(c.Gate());
+    HIP_CHK(hipSetDevice(c.device));
+    // ReduceScatterVAutoSelector::SelectAicpuAlgo (reduce_scatter_v_auto_selector.cc:180-197): UINT64 and FP64 have
+    // no algorithm
+    if (dt == HCCL_DATA_TYPE_UINT64 || dt == HCCL_DATA_TYPE_FP64) return HCCL_E_NOT_SUPPORT;
+    // a bootstrap-only communicator has no send/recv path and the one-sided kernel has no per-rank block layout
+    if (c.nRanks > 1 && !c.transport->HasSendRecv()) return HCCL_E_NOT_SUPPORT;
+    const uint32_t es = DataTypeSize(dt);
+    ScheduleParams p;
+    p.opType = HCCL_AMD_OP_REDUCE_SCATTER_V;
+    p.nRanks = c.nRanks;
+    p.rank = c.rank;
+    p.counts.assign(counts, counts + c.nRanks);
+    p.displs.assign(displs, displs + c.nRanks);
+    p.count = counts[c.rank];
+    p.elemSize = es;
+    p.pieceBytes = c.pieceBytes;
+    p.scratchCapBytes = c.scratchBytes;
+    p.cclBytes = c.cclBytes;
+    Schedule s;
+    HCCL_CHK(static_cast<HcclResult>(BuildSchedule(p, &s)));
+    if (s.scratchElems * es > c.scratchBytes) return HCCL_E_INTERNAL;
+    c.lastAlgo = s.algo;
+    void* bufs[3] = {sendBuf, recvBuf, c.scratch};
+    uint64_t payload = 0;
+    for (uint32_t q = 0; q < c.nRanks; ++q) payload += counts[q] * es;
+    return Execute(c, s.ops, bufs, dt, op, stream, c.nRanks == 1 || payload <= SingleStreamBytes());
+}
+
 }  // namespace
 
 }  // namespace hccl_amd
@@ -185,6 +220,33 @@ HcclResult HcclReduceScatter(void* sendBuf, void* recvBuf, uint64_t recvCount, H
     HCCL_CHK(CheckReduceOp(dataType, op));
     return RunCollective(*c, HCCL_AMD_OP_REDUCE_SCATTER, sendBuf, recvBuf, recvCount, dataType, op, 0,
                          static_cast<hipStream_t>(stream));
+}
+
+HcclResult HcclReduceScatterV(void* sendBuf, const void* sendCounts, const void* sendDispls, void* recvBuf,
+                              uint64_t recvCount, HcclDataType dataType, HcclReduceOp op, HcclComm comm,
+                              aclrtStream stream)
+{
+    // CheckReduceScatterVInputParam (reduce_scatter_v_op.cc:155-183): stream, comm, sendCounts, sendDispls, then
+    // recvBuf when recvCount > 0 (sendBuf is not checked there: a rank may send nothing)
+    if (stream == nullptr || comm == nullptr || sendCounts == nullptr || sendDispls == nullptr) return HCCL_E_PTR;
+    if (recvCount > 0 && recvBuf == nullptr) return HCCL_E_PTR;
+    Comm* c = AsComm(comm);
+    if (c == nullptr) return HCCL_E_PARA;
+    const uint64_t* counts = static_cast<const uint64_t*>(sendCounts);
+    const uint64_t* displs = static_cast<const uint64_t*>(sendDispls);
+    bool any = false;
+    for (uint32_t q = 0; q < c->nRanks; ++q) any = any || counts[q] != 0;
+    if (!any) return HCCL_SUCCESS;  // every sendCounts entry 0: success (:45-53)
+    if (c->rank >= c->nRanks) return HCCL_E_PARA;  // HcomCheckUserRank
+    HCCL_CHK(CheckCount(recvCount));
+    HCCL_CHK(CheckReduceDataType(dataType));
+    HCCL_CHK(CheckReduceOp(dataType, op));
+    for (uint32_t q = 0; q < c->nRanks; ++q) HCCL_CHK(CheckCount(counts[q]));
+    // The template writes sendCounts[rank] elements to recvBuf (PostCopy, ins_temp_reduce_scatter_v_mesh_1D.cc:
+    // 107-146); a smaller recvCount would overrun it, so it is refused here (the reference has no such check).
+    if (counts[c->rank] > recvCount) return HCCL_E_PARA;
+    if (sendBuf == nullptr) return HCCL_E_PTR;  // some rank's block is non-empty: the input is read
+    return RunReduceScatterV(*c, sendBuf, counts, displs, recvBuf, dataType, op, static_cast<hipStream_t>(stream));
 }
 
 HcclResult HcclReduce(void* sendBuf, void* recvBuf, uint64_t count, HcclDataType dataType, HcclReduceOp op,
@@ -401,6 +463,37 @@ int32_t HcclAmdSelectAivAlgo(int32_t opType, uint32_t nRanks, uint64_t count, Hc
 {
     return SelectAivPlan(opType, nRanks, count, dataType, op, strict != 0, CclBytesDefault(),
                          coreLimit != 0 ? coreLimit : AivCoreLimit(), nullptr, groupSize);
+}
+
+HcclResult HcclAmdBuildScheduleV(uint32_t nRanks, uint32_t rank, const uint64_t* sendCounts,
+                                 const uint64_t* sendDispls, HcclDataType dataType, uint64_t pieceBytes,
+                                 HcclAmdIrOp* ops, uint64_t capacity, uint64_t* numOps, uint64_t* scratchElems)
+{
+    if (numOps == nullptr || sendCounts == nullptr || sendDispls == nullptr) return HCCL_E_PTR;
+    const uint32_t es = DataTypeSize(dataType);
+    if (es == 0) return HCCL_E_NOT_SUPPORT;
+    if (nRanks == 0 || rank >= nRanks) return HCCL_E_PARA;
+    ScheduleParams p;
+    p.opType = HCCL_AMD_OP_REDUCE_SCATTER_V;
+    p.nRanks = nRanks;
+    p.rank = rank;
+    p.counts.assign(sendCounts, sendCounts + nRanks);
+    p.displs.assign(sendDispls, sendDispls + nRanks);
+    p.count = sendCounts[rank];
+    p.elemSize = es;
+    p.pieceBytes = pieceBytes;
+    p.scratchCapBytes = ScratchBytesDefault();
+    p.cclBytes = CclBytesDefault();
+    Schedule s;
+    HcclResult r = static_cast<HcclResult>(BuildSchedule(p, &s));
+    if (r != HCCL_SUCCESS) return r;
+    *numOps = s.ops.size();
+    if (scratchElems != nullptr) *scratchElems = s.scratchElems;
+    if (ops != nullptr) {
+        if (capacity < s.ops.size()) return HCCL_E_PARA;
+        std::memcpy(ops, s.ops.data(), s.ops.size() * sizeof(HcclAmdIrOp));
+    }
+    return HCCL_SUCCESS;
 }
 
 int32_t HcclAmdSelectAlgo(int32_t opType, uint32_t nRanks, uint64_t bytes, int32_t special)

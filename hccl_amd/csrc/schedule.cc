@@ -988,6 +988,37 @@ void ReduceScatterMesh(const ScheduleParams& p, Builder& b)
     }
 }
 
+// ReduceScatterV mesh (O1, ins_temp_reduce_scatter_v_mesh_1D.cc:107-146, RunReduceScatterV :148-205): every rank
+// writes its input block of peer q, [displs[q], displs[q] + counts[q]), to q; rank me copies its own block to recvBuf
+// and folds the peers' copies into it in ascending rank order (PostCopy's LocalReduce loop over tmpRank). Pieces of
+// counts[me] are pipelined through two staging slot sets as in the mesh ReduceScatter; the order does not depend on
+// them.
+void ReduceScatterVMesh(const ScheduleParams& p, Builder& b)
+{
+    const uint32_t n = p.nRanks, me = p.rank;
+    uint64_t widest = 0;
+    for (uint32_t q = 0; q < n; ++q) widest = std::max(widest, p.counts[q]);
+    const uint64_t kSlots = 2;
+    const uint64_t pe = PieceElems(p, std::max<uint64_t>(1, widest), kSlots * (n - 1));
+    const uint64_t np = std::max<uint64_t>(1, CeilDiv(widest, pe));  // equal on every rank
+    auto slot = [&](uint64_t t, uint32_t q) { return Scr(((t % kSlots) * (n - 1) + PeerSlot(q, me)) * pe); };
+    for (uint64_t t = 0; t < np; ++t) {
+        const Span mine = Piece({0, p.counts[me]}, pe, t);
+        for (uint32_t q : PeerOrder(n, me)) {
+            const Span out = Piece({0, p.counts[q]}, pe, t);
+            b.Send(q, In(p.displs[q] + out.begin), out.len);
+            b.Recv(q, slot(t, q), mine.len);
+        }
+        b.EndGroup();
+        if (mine.len == 0) continue;
+        std::vector<Ref> srcs{In(p.displs[me] + mine.begin)};
+        for (uint32_t q = 0; q < n; ++q) {
+            if (q != me) srcs.push_back(slot(t, q));
+        }
+        b.Reduce(Out(mine.begin), srcs, mine.len);
+    }
+}
+
 // Ring reduce-scatter over R rings: every block is split into R parts and part k of every block travels around ring
 // k. Step s, position v sends block cycle[v-s-1] (its partial) to v+1 and folds block cycle[v-s-2] received from v-1
 // into its own input (acc = travelling partial (src) (op) own input); position v ends with block cycle[v] = its own.
@@ -1247,6 +1278,19 @@ int BuildSchedule(const ScheduleParams& p, Schedule* out)
         return HCCL_E_PARA;
     }
     if (p.opType == HCCL_AMD_OP_REDUCE && p.root >= p.nRanks) return HCCL_E_PARA;
+    if (p.opType == HCCL_AMD_OP_REDUCE_SCATTER_V) {
+        if (p.counts.size() != p.nRanks || p.displs.size() != p.nRanks) return HCCL_E_PARA;
+        Builder bv;
+        if (p.nRanks == 1) {
+            bv.Copy(Out(0), In(p.displs[0]), p.counts[0]);
+        } else {
+            ReduceScatterVMesh(p, bv);  // the only AICPU template (reduce_scatter_v_auto_selector.cc:180-197)
+        }
+        out->ops = std::move(bv.ops);
+        out->algo = HCCL_AMD_ALGO_MESH_ONESHOT;
+        out->scratchElems = bv.scratchHigh;
+        return HCCL_SUCCESS;
+    }
     Builder b;
     int32_t algo = p.algo;
     uint64_t bytes = p.count * p.elemSize;

@@ -25,6 +25,10 @@ struct ScheduleParams {
     uint64_t scratchCapBytes = 0;   // 0 = unbounded
     uint64_t cclBytes = 200ull << 20;  // HCCL_BUFFSIZE: sizes the reference's executor loops (see RefLoopElems)
     bool special = false;  // INT64 / UINT64 / FP64 data or PROD: the selectors' isDataTypeOrReduceTypeSpecial
+    // ReduceScatterV (HCCL_AMD_OP_REDUCE_SCATTER_V): rank q's block of every input is [displs[q], displs[q] +
+    // counts[q]) (elements); nRanks entries each. count is then counts[rank].
+    std::vector<uint64_t> counts;
+    std::vector<uint64_t> displs;
 };
 
 struct Schedule {

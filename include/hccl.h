@@ -7,6 +7,7 @@
  *
  *   HcclAllReduce      replaces /root/reference/include/hccl.h:35-37  (impl all_reduce_op.cc:23-52)
  *   HcclReduceScatter  replaces /root/reference/include/hccl.h:67-69  (impl reduce_scatter_op.cc:23-72)
+ *   HcclReduceScatterV replaces /root/reference/include/hccl.h:87-89  (impl reduce_scatter_v_op.cc:24-83)
  *   HcclReduce         replaces /root/reference/include/hccl.h:245-247 (impl reduce_op.cc:23-54)
  *
  * The communicator calls are the hcomm functions the reference's callers use
@@ -36,6 +37,13 @@ extern HcclResult HcclAllReduce(void* sendBuf, void* recvBuf, uint64_t count, Hc
 /* ReduceScatter: sendBuf holds rankSize blocks of recvCount; rank r receives the reduce of block r. */
 extern HcclResult HcclReduceScatter(void* sendBuf, void* recvBuf, uint64_t recvCount, HcclDataType dataType,
                                     HcclReduceOp op, HcclComm comm, aclrtStream stream);
+
+/* ReduceScatterV: rank q's block of sendBuf is sendCounts[q] elements at sendDispls[q] (uint64 arrays of rankSize
+ * entries); rank r receives the reduce of every rank's block r, sendCounts[r] elements (recvCount must hold them).
+ * Replaces /root/reference/include/hccl.h:87-89 (reduce_scatter_v_op.cc:24-83). */
+extern HcclResult HcclReduceScatterV(void* sendBuf, const void* sendCounts, const void* sendDispls, void* recvBuf,
+                                     uint64_t recvCount, HcclDataType dataType, HcclReduceOp op, HcclComm comm,
+                                     aclrtStream stream);
 
 /* Reduce: recvBuf on `root` receives the reduce of every rank's sendBuf (recvBuf must be non-null everywhere). */
 extern HcclResult HcclReduce(void* sendBuf, void* recvBuf, uint64_t count, HcclDataType dataType, HcclReduceOp op,

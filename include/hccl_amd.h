@@ -94,7 +94,8 @@ typedef enum {
     HCCL_AMD_OP_ALLREDUCE = 0,
     HCCL_AMD_OP_REDUCE_SCATTER = 1,
     HCCL_AMD_OP_REDUCE = 2,
-    HCCL_AMD_OP_ALLGATHER = 3 /* the second half of AllReduce as an operator (count = sendCount) */
+    HCCL_AMD_OP_ALLGATHER = 3, /* the second half of AllReduce as an operator (count = sendCount) */
+    HCCL_AMD_OP_REDUCE_SCATTER_V = 4 /* per-rank counts and displacements (HcclAmdBuildScheduleV) */
 } HcclAmdOpType;
 
 typedef enum {
@@ -139,6 +140,14 @@ extern HcclResult HcclAmdBuildSchedule(int32_t opType, int32_t algo, uint32_t nR
                                        HcclDataType dataType, uint32_t root, uint64_t pieceBytes, HcclAmdIrOp* ops,
                                        uint64_t capacity, uint64_t* numOps, int32_t* algoUsed,
                                        uint64_t* scratchElems);
+
+/* ReduceScatterV schedule of rank `rank`: rank q's block of every input is [sendDispls[q], sendDispls[q] +
+ * sendCounts[q]) elements (nRanks entries each); the mesh template's order O1
+ * (ins_temp_reduce_scatter_v_mesh_1D.cc:107-146). Same output conventions as HcclAmdBuildSchedule. */
+extern HcclResult HcclAmdBuildScheduleV(uint32_t nRanks, uint32_t rank, const uint64_t* sendCounts,
+                                        const uint64_t* sendDispls, HcclDataType dataType, uint64_t pieceBytes,
+                                        HcclAmdIrOp* ops, uint64_t capacity, uint64_t* numOps,
+                                        uint64_t* scratchElems);
 
 /* The algorithm HCCL_AMD_ALGO_AUTO selects for an operation of `bytes` bytes per rank (ReduceScatter: recvCount
  * bytes) on nRanks ranks; special = 64-bit data type or PROD (the reference selectors' isDataTypeOrReduceTypeSpecial).

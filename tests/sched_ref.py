@@ -305,6 +305,18 @@ def reduce_scatter_ring(dtype, op, xs, rc):
     return outs
 
 
+def reduce_scatter_v_o1(dtype, op, xs, counts, displs):
+    """ReduceScatterV mesh (ins_temp_reduce_scatter_v_mesh_1D.cc:107-146): rank me copies its own block
+    [displs[me], displs[me] + counts[me]) and folds every peer's copy of it in ascending rank order (O1)."""
+    n = len(xs)
+    outs = []
+    for me in range(n):
+        b, e = displs[me], displs[me] + counts[me]
+        outs.append(fold(dtype, op, [xs[me][b:e]] + [xs[q][b:e] for q in range(n) if q != me]) if e > b
+                    else np.empty(0, xs[0].dtype))
+    return outs
+
+
 def reduce_oneshot(dtype, op, xs, root):
     n = len(xs)
     return fold(dtype, op, [xs[root]] + [xs[q] for q in range(n) if q != root])

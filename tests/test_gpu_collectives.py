@@ -464,6 +464,44 @@ def test_aiv_expansion_mode_env_and_fallback(worlds, monkeypatch):
         assert O.equal_bits(O.FP32, outs[r], want[r]), r
 
 
+@pytest.mark.parametrize("n,layout", [(2, "ragged"), (4, "gapped"), (8, "ragged"), (8, "overlap"), (3, "empty")])
+@pytest.mark.parametrize("dtype,op", [(O.FP32, O.SUM), (O.FP16, O.SUM), (O.BFP16, O.MAX), (O.INT32, O.PROD),
+                                      (O.INT64, O.MIN)], ids=lambda v: str(v))
+@pytest.mark.parametrize("streams", ["auto", "two"])
+def test_reduce_scatter_v(worlds, monkeypatch, n, layout, dtype, op, streams):
+    """HcclReduceScatterV through the executor: rank r's output is the mesh template's O1 fold of every rank's block r
+    (ins_temp_reduce_scatter_v_mesh_1D.cc:107-146), bit-exact against the closed form and the oracle's IR replay."""
+    if streams == "two":
+        monkeypatch.setenv("HCCL_AMD_SINGLE_STREAM_BYTES", "0")
+    comms = worlds(n)
+    if layout == "gapped":
+        counts, displs = [70001] * n, [q * 80000 + 3 for q in range(n)]
+    elif layout == "overlap":
+        counts, displs = [300007] * n, [q * 1000 for q in range(n)]
+    else:
+        counts = [(40961 * (q + 3)) % 150001 + (0 if layout != "empty" or q != 1 else -((40961 * 4) % 150001))
+                  for q in range(n)]
+        displs = list(np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(int))
+    in_count = max(c + d for c, d in zip(counts, displs))
+    xs = [O.random_operands(dtype, in_count, seed=1500 + r, edge=False) for r in range(n)]
+    sends = [to_device(dtype, x) for x in xs]
+    recvs = [to_device(dtype, np.zeros(max(1, counts[r]), O.NP_STORAGE[dtype])) for r in range(n)]
+    streams_ = [torch.cuda.Stream() for _ in range(n)]
+    for c in comms:
+        c.set_piece_bytes(64 << 10)
+    torch.cuda.synchronize()
+    try:
+        run_ranks(n, lambda r: comms[r].reduce_scatter_v(sends[r], counts, displs, recvs[r], op, streams_[r]))
+        torch.cuda.synchronize()
+    finally:
+        for c in comms:
+            c.set_piece_bytes(0)
+    want = R.reduce_scatter_v_o1(dtype, op, xs, counts, displs)
+    for r in range(n):
+        got = to_host(dtype, recvs[r])[:counts[r]]
+        assert O.equal_bits(dtype, got, want[r]), (r, counts[r])
+
+
 @pytest.mark.parametrize("algo", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_allreduce_inplace(worlds, algo):
     n, count = 4, 300007
