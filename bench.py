@@ -591,10 +591,12 @@ def bench_c3_algos(comm, send, recv, world) -> dict:
     digests = {}
     twin = {H.Algo.IPC_TWOSHOT: H.Algo.MESH_TWOSHOT, H.Algo.IPC: H.Algo.MESH_CHUNK}
     try:
-        # (schedule, IPC workgroups per launch; 0 = default 128)
-        for algo, blocks in ((H.Algo.MESH_CHUNK, 0), (H.Algo.IPC, 0), (H.Algo.IPC, 256), (H.Algo.MESH_TWOSHOT, 0),
-                             (H.Algo.IPC_TWOSHOT, 0), (H.Algo.RING, 0), (H.Algo.RHD, 0), (H.Algo.NHR, 0),
-                             (H.Algo.MESH_ONESHOT, 0)):
+        # (schedule, IPC workgroups per launch; 0 = the default by size). The RCCL schedules run first: an IPC
+        # barrier timeout fails the communicator (later calls answer HCCL_E_SUSPENDING), so the one-sided rows come
+        # last, after their RCCL twins have left the digests they are compared with.
+        for algo, blocks in ((H.Algo.MESH_CHUNK, 0), (H.Algo.MESH_TWOSHOT, 0), (H.Algo.RING, 0), (H.Algo.RHD, 0),
+                             (H.Algo.NHR, 0), (H.Algo.MESH_ONESHOT, 0), (H.Algo.IPC, 0), (H.Algo.IPC, 256),
+                             (H.Algo.IPC_TWOSHOT, 0)):
             name = algo.name if blocks == 0 else f"{algo.name}_{blocks}_BLOCKS"
             comm.set_algo(algo)
             comm.set_ipc_blocks(blocks)
