@@ -481,49 +481,56 @@ def bench_c4(comm, send, recv, world) -> dict:
 def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
     """C5: AllReduce fp16 SUM, 1 KiB .. 4 GiB: latency at small sizes, busbw at large. Each size runs the RHD schedule
     (the config's algorithm), the auto selection (what the reference would run: one-shot / two-shot / MeshChunk) and,
-    up to 256 MiB, the one-sided IPC kernel in the same order family (one launch per call: the latency end)."""
+    up to 256 MiB, the one-sided IPC kernel in the same order family (one launch per call: the latency end). The RCCL
+    rows of every size run before the IPC rows: an IPC barrier timeout fails the communicator."""
     s = torch.cuda.current_stream()
-    rows = []
+    sizes = []
     nbytes = 1 << 10
+    while nbytes <= max_bytes:
+        sizes.append(nbytes)
+        nbytes *= 2
+    rows = {b: {"bytes": b} for b in sizes}
     f = 2 * (world - 1) / world
+    key = {H.Algo.RHD: "rhd", H.Algo.AUTO: "auto", H.Algo.IPC: "ipc"}
     try:
-        while nbytes <= max_bytes:
-            a = send.view(torch.float16)[: nbytes // 2]
-            b = recv.view(torch.float16)[: nbytes // 2]
-            iters = 20 if nbytes <= (64 << 20) else 3
-            row = {"bytes": nbytes}
-            algos = (H.Algo.RHD, H.Algo.AUTO) + ((H.Algo.IPC,) if nbytes <= (256 << 20) else ())
-            for algo in algos:
-                comm.set_algo(algo)
-                key = {H.Algo.RHD: "rhd", H.Algo.AUTO: "auto", H.Algo.IPC: "ipc"}[algo]
+        for algo in (H.Algo.RHD, H.Algo.AUTO, H.Algo.IPC):
+            comm.set_algo(algo)
+            for nbytes in sizes:
+                if algo == H.Algo.IPC and nbytes > (256 << 20):
+                    break
+                row = rows[nbytes]
+                a = send.view(torch.float16)[: nbytes // 2]
+                b = recv.view(torch.float16)[: nbytes // 2]
+                iters = 20 if nbytes <= (64 << 20) else 3
                 try:
                     t = _timed(lambda: comm.all_reduce(a, b, H.HcclReduceOp.SUM, s), iters)
                 except H.HcclError as e:
-                    row[f"{key}_error"] = str(e)
+                    row[f"{key[algo]}_error"] = str(e)
                     continue
-                row[f"{key}_us"] = round(t * 1e6, 1)
-                row[f"{key}_busbw_GBps"] = round(nbytes / t / 1e9 * f, 2)
+                row[f"{key[algo]}_us"] = round(t * 1e6, 1)
+                row[f"{key[algo]}_busbw_GBps"] = round(nbytes / t / 1e9 * f, 2)
                 if algo == H.Algo.AUTO:
                     row["auto_algo"] = H.Algo(comm.last_algo).name
                 if algo == H.Algo.IPC:
                     row["ipc_ran"] = H.Algo(comm.last_algo).name
                     row["ipc_barrier_timeouts"] = comm.ipc_status() & 1
-            if nbytes <= (1 << 20) and row.get("ipc_ran") == "IPC":
-                # the latency end replayed from a HIP graph (50 captured calls per replay; device-side epochs)
-                try:
-                    comm.set_algo(H.Algo.IPC)
-                    row["ipc_graph_us"] = round(_graph_us(lambda st: comm.all_reduce(a, b, H.HcclReduceOp.SUM, st)),
-                                                1)
-                    row["ipc_graph_barrier_timeouts"] = comm.ipc_status() & 1
-                except Exception as e:  # noqa: BLE001  (capture problems never end the sweep)
-                    row["ipc_graph_error"] = f"{type(e).__name__}: {e}"
-                finally:
-                    comm.set_algo(H.Algo.AUTO)
-            rows.append(row)
-            nbytes *= 2
+        for nbytes in sizes:
+            row = rows[nbytes]
+            if nbytes > (1 << 20) or row.get("ipc_ran") != "IPC":
+                continue
+            # the latency end replayed from a HIP graph (50 captured calls per replay; device-side epochs)
+            a = send.view(torch.float16)[: nbytes // 2]
+            b = recv.view(torch.float16)[: nbytes // 2]
+            try:
+                comm.set_algo(H.Algo.IPC)
+                row["ipc_graph_us"] = round(_graph_us(lambda st: comm.all_reduce(a, b, H.HcclReduceOp.SUM, st)), 1)
+                row["ipc_graph_barrier_timeouts"] = comm.ipc_status() & 1
+            except Exception as e:  # noqa: BLE001  (capture problems never end the sweep)
+                row["ipc_graph_error"] = f"{type(e).__name__}: {e}"
     finally:
         comm.set_algo(H.Algo.AUTO)
-    return {"workload": "C5: AllReduce fp16 SUM, size sweep (RHD schedule and auto selection)", "points": rows}
+    return {"workload": "C5: AllReduce fp16 SUM, size sweep (RHD schedule and auto selection)",
+            "points": [rows[b] for b in sizes]}
 
 
 def bench_e2e_allreduce(comm, world, nbytes: int = 256 << 20, iters: int = 5, chunk: int = 32 << 20) -> dict:
