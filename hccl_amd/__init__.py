@@ -213,6 +213,12 @@ class Comm:
     def last_algo(self) -> int:
         return lib.HcclAmdCommLastAlgo(self.handle)
 
+    def compile_stats(self) -> tuple:
+        """(hits, misses) of the communicator's compiled-collective cache (HcclAmdCommCompileStats)."""
+        h, m = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        check("HcclAmdCommCompileStats", lib.HcclAmdCommCompileStats(self.handle, ctypes.byref(h), ctypes.byref(m)))
+        return h.value, m.value
+
     def reduce_scatter_v(self, send: torch.Tensor, counts: Sequence[int], displs: Sequence[int], recv: torch.Tensor,
                          op: int = HcclReduceOp.SUM, stream=None) -> None:
         """HcclReduceScatterV: rank q's block of `send` is counts[q] elements at displs[q]."""

@@ -188,6 +188,7 @@ SIGNATURES = {
     "HcclAmdCommSetPieceBytes": (_res, [_vp, _u64]),
     "HcclAmdCommSetIpcBlocks": (_res, [_vp, _u32]),
     "HcclAmdCommLastAlgo": (_i32, [_vp]),
+    "HcclAmdCommCompileStats": (_res, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     "HcclAmdCommIpcStatus": (_res, [_vp, ctypes.POINTER(_u32)]),
     "HcclAmdIpcTimeoutMs": (_u64, []),
     "HcclAmdCommInitHostExchange": (_res, [_u32, _u32, _vp, _vp, ctypes.POINTER(_vp)]),

@@ -52,6 +52,31 @@ std::unique_ptr<Transport> MakeLoopbackTransport(std::shared_ptr<LoopbackWorld> 
 std::shared_ptr<LoopbackWorld> MakeLoopbackWorld(uint32_t nRanks);
 std::unique_ptr<Transport> MakeHostExchangeTransport(HcclAmdHostAllGatherFn fn, void* ctx);
 
+// The executor's units for one rank's IR (Execute issues exactly these): a transport group (link stream 0) or a
+// batch of folds / a copy (reduce stream 1), each with the unit of the other stream it must wait for (the latest whose
+// byte ranges conflict with it, RAW / WAR / WAW on absolute addresses), or -1.
+struct UnitPlan {
+    int stream = 0;
+    bool isComm = false;
+    size_t first = 0;  // IR records [first, first + count)
+    size_t count = 0;
+    int64_t waitUnit = -1;
+};
+
+// One rank's compiled collective: the schedule for a set of ScheduleParams and the executor's plan for it. The plan
+// depends on the buffers only through how they overlap (conflicts compare absolute addresses, and a translation of
+// one buffer changes nothing while it stays clear of the others), so it is kept with the overlap relation it was
+// made for and rebuilt only when a call's relation differs (an in-place call after out-of-place ones).
+struct CompiledSchedule {
+    ScheduleParams params;
+    Schedule sched;
+    uint64_t extent[3] = {0, 0, 0};  // bytes of {sendBuf, recvBuf, scratch} the IR addresses
+    int64_t relation[3] = {0, 0, 0};  // pairs (0,1), (0,2), (1,2): kDisjoint or the base difference
+    bool hasPlan = false;
+    std::vector<UnitPlan> plan;
+    uint64_t lastUse = 0;
+};
+
 struct Comm {
     uint32_t magic = 0x48434C41;  // "HCLA"
     uint32_t rank = 0;
@@ -82,6 +107,13 @@ struct Comm {
     // communicator whose status is not READY). HcclGetCommAsyncError reports the error without changing state.
     bool failed = false;
     HcclResult failCode = HCCL_SUCCESS;
+
+    // Compiled collectives, least recently used evicted (a training loop repeats the same few bucket calls: they skip
+    // BuildSchedule and PlanUnits after the first). HCCL_AMD_PLAN_CACHE=0 compiles every call.
+    std::vector<std::unique_ptr<CompiledSchedule>> compiled;
+    uint64_t compileTick = 0;
+    uint64_t compileHits = 0;
+    uint64_t compileMisses = 0;
 
     HcclResult Init(int dev);
     HcclResult NextEvent(hipEvent_t* e);
@@ -127,20 +159,17 @@ uint64_t ScratchBytesDefault();
 
 // Runs one rank's schedule. bufs = {sendBuf, recvBuf, scratch}. Stream-ordered after `user`; `user` waits for the
 // whole schedule before anything enqueued later on it runs. singleStream puts every unit on `user` in program order.
+// plan = PlanUnits(ops, bufs, es) if the caller has it (CompileCollective), else nullptr.
 HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const bufs[3], HcclDataType dt,
-                   HcclReduceOp op, hipStream_t user, bool singleStream = false);
+                   HcclReduceOp op, hipStream_t user, bool singleStream = false,
+                   const std::vector<UnitPlan>* plan = nullptr);
 
-// The executor's units for one rank's IR (Execute issues exactly these): a transport group (link stream 0) or a
-// batch of folds / a copy (reduce stream 1), each with the unit of the other stream it must wait for (the latest whose
-// byte ranges conflict with it, RAW / WAR / WAW on absolute addresses), or -1.
-struct UnitPlan {
-    int stream = 0;
-    bool isComm = false;
-    size_t first = 0;  // IR records [first, first + count)
-    size_t count = 0;
-    int64_t waitUnit = -1;
-};
 std::vector<UnitPlan> PlanUnits(const std::vector<HcclAmdIrOp>& ops, void* const bufs[3], uint64_t es);
+
+// The compiled form of p for the buffers bufs (cached on c; call with c.mu held): BuildSchedule's result and, when
+// withPlan, the plan for the buffers' overlap relation. The pointer stays valid until the next call on c.
+HcclResult CompileCollective(Comm& c, const ScheduleParams& p, void* const bufs[3], bool withPlan,
+                             const CompiledSchedule** out);
 
 // Collectives whose per-rank payload is at most this many bytes run single-stream (HCCL_AMD_SINGLE_STREAM_BYTES,
 // default 1 MiB).

@@ -11,6 +11,8 @@
 // This is the reference ST's memory-conflict rule (test/st/algorithm/.../mem_conflict_check) turned into the
 // synchronisation itself. The host never blocks (except loopback rendezvous); the user stream is joined at the end.
 #include <algorithm>
+#include <climits>
+#include <cstring>
 
 #include "comm.h"
 
@@ -197,8 +199,96 @@ std::vector<UnitPlan> PlanUnits(const std::vector<HcclAmdIrOp>& ops, void* const
     return plan;
 }
 
+namespace {
+
+constexpr int64_t kDisjoint = INT64_MIN;
+constexpr size_t kCompiledMax = 32;
+
+bool SameParams(const ScheduleParams& a, const ScheduleParams& b)
+{
+    return a.opType == b.opType && a.algo == b.algo && a.nRanks == b.nRanks && a.rank == b.rank && a.count == b.count &&
+           a.elemSize == b.elemSize && a.root == b.root && a.pieceBytes == b.pieceBytes &&
+           a.scratchCapBytes == b.scratchCapBytes && a.cclBytes == b.cclBytes && a.special == b.special &&
+           a.counts == b.counts && a.displs == b.displs;
+}
+
+// How the buffers of pair (x, y) lie against each other over the bytes the IR addresses: kDisjoint, or base(y) -
+// base(x) when the addressed ranges overlap (every conflict test between them is then fixed by that difference).
+void Relation(const uint64_t ext[3], void* const bufs[3], int64_t rel[3])
+{
+    static const int kPair[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+    for (int k = 0; k < 3; ++k) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(bufs[kPair[k][0]]);
+        const uintptr_t b = reinterpret_cast<uintptr_t>(bufs[kPair[k][1]]);
+        const uint64_t ea = ext[kPair[k][0]];
+        const uint64_t eb = ext[kPair[k][1]];
+        const bool overlap = ea != 0 && eb != 0 && a < b + eb && b < a + ea;
+        rel[k] = overlap ? static_cast<int64_t>(b - a) : kDisjoint;
+    }
+}
+
+bool PlanCacheEnabled()
+{
+    const char* e = std::getenv("HCCL_AMD_PLAN_CACHE");  // read per call: tests switch it
+    return e == nullptr || std::strcmp(e, "0") != 0;
+}
+
+}  // namespace
+
+HcclResult CompileCollective(Comm& c, const ScheduleParams& p, void* const bufs[3], bool withPlan,
+                             const CompiledSchedule** out)
+{
+    const bool cache = PlanCacheEnabled();
+    if (!cache) c.compiled.clear();
+    CompiledSchedule* hit = nullptr;
+    for (auto& e : c.compiled) {
+        if (SameParams(e->params, p)) {
+            hit = e.get();
+            break;
+        }
+    }
+    if (hit == nullptr) {
+        ++c.compileMisses;
+        auto e = std::make_unique<CompiledSchedule>();
+        e->params = p;
+        HCCL_CHK(static_cast<HcclResult>(BuildSchedule(p, &e->sched)));
+        for (const HcclAmdIrOp& o : e->sched.ops) {
+            const uint64_t bytes = o.count * p.elemSize;
+            if (o.dstBuf >= 0 && o.dstBuf < 3) {
+                e->extent[o.dstBuf] = std::max(e->extent[o.dstBuf], (o.dstOff + o.count) * p.elemSize);
+            }
+            const int nsrc = o.kind == HCCL_AMD_IR_RECV ? 0 : std::max(0, std::min(o.nsrc, HCCL_AMD_IR_MAX_SRC));
+            for (int j = 0; j < nsrc; ++j) {
+                const int32_t sb = o.srcBuf[j];
+                if (sb >= 0 && sb < 3) e->extent[sb] = std::max(e->extent[sb], o.srcOff[j] * p.elemSize + bytes);
+            }
+        }
+        if (c.compiled.size() >= kCompiledMax) {
+            auto lru = std::min_element(c.compiled.begin(), c.compiled.end(),
+                                        [](const auto& x, const auto& y) { return x->lastUse < y->lastUse; });
+            c.compiled.erase(lru);
+        }
+        hit = e.get();
+        c.compiled.push_back(std::move(e));
+    } else {
+        ++c.compileHits;
+    }
+    hit->lastUse = ++c.compileTick;
+    if (withPlan) {
+        int64_t rel[3];
+        Relation(hit->extent, bufs, rel);
+        if (!hit->hasPlan || std::memcmp(rel, hit->relation, sizeof rel) != 0) {
+            hit->plan = PlanUnits(hit->sched.ops, bufs, p.elemSize);
+            std::memcpy(hit->relation, rel, sizeof rel);
+            hit->hasPlan = true;
+        }
+    }
+    *out = hit;
+    return HCCL_SUCCESS;
+}
+
 HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const bufs[3], HcclDataType dt,
-                   HcclReduceOp op, hipStream_t user, bool singleStream)
+                   HcclReduceOp op, hipStream_t user, bool singleStream, const std::vector<UnitPlan>* cached)
 {
     if (singleStream) return ExecuteSingleStream(c, ops, bufs, dt, op, user);
     const uint64_t es = DataTypeSize(dt);
@@ -214,7 +304,9 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
         return reinterpret_cast<uintptr_t>(bufs[buf]) + off * es;
     };
 
-    const std::vector<UnitPlan> plan = PlanUnits(ops, bufs, es);
+    std::vector<UnitPlan> fresh;
+    if (cached == nullptr) fresh = PlanUnits(ops, bufs, es);
+    const std::vector<UnitPlan>& plan = cached != nullptr ? *cached : fresh;
     std::vector<hipEvent_t> evs(plan.size(), nullptr);
     bool used[2] = {false, false};
     std::vector<P2pOp> p2p;

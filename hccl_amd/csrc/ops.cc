@@ -131,9 +131,12 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     p.scratchCapBytes = c.scratchBytes;
     p.cclBytes = c.cclBytes;
     p.special = IsSpecialForSelector(dt, op);
-    Schedule s;
-    HcclResult r = static_cast<HcclResult>(BuildSchedule(p, &s));
-    if (r != HCCL_SUCCESS) return r;
+    void* bufs[3] = {sendBuf, recvBuf, c.scratch};
+    const uint64_t payload = count * es * (opType == HCCL_AMD_OP_REDUCE_SCATTER ? c.nRanks : 1);
+    const bool single = payload <= SingleStreamBytes();
+    const CompiledSchedule* cs = nullptr;
+    HCCL_CHK(CompileCollective(c, p, bufs, !single, &cs));
+    const Schedule& s = cs->sched;
     if (s.scratchElems * es > c.scratchBytes) {
         HCCL_AMD_ERR("schedule needs %llu B of staging, communicator has %llu B",
                      (unsigned long long)(s.scratchElems * es), (unsigned long long)c.scratchBytes);
@@ -142,9 +145,7 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     c.lastAlgo = s.algo;
     HCCL_AMD_LOG("rank %u op %d algo %d count %llu ops %zu", c.rank, opType, s.algo, (unsigned long long)count,
                  s.ops.size());
-    void* bufs[3] = {sendBuf, recvBuf, c.scratch};
-    const uint64_t payload = count * es * (opType == HCCL_AMD_OP_REDUCE_SCATTER ? c.nRanks : 1);
-    return Execute(c, s.ops, bufs, dt, op, stream, payload <= SingleStreamBytes());
+    return Execute(c, s.ops, bufs, dt, op, stream, single, single ? nullptr : &cs->plan);
 }
 
 // ReduceScatterV (reduce_scatter_v_op.cc:24-83, ReduceScatterVOutPlaceCommon :285-330): the mesh template's order
@@ -172,14 +173,16 @@ HcclResult RunReduceScatterV(Comm& c, void* sendBuf, const uint64_t* counts, con
     p.pieceBytes = c.pieceBytes;
     p.scratchCapBytes = c.scratchBytes;
     p.cclBytes = c.cclBytes;
-    Schedule s;
-    HCCL_CHK(static_cast<HcclResult>(BuildSchedule(p, &s)));
-    if (s.scratchElems * es > c.scratchBytes) return HCCL_E_INTERNAL;
-    c.lastAlgo = s.algo;
     void* bufs[3] = {sendBuf, recvBuf, c.scratch};
     uint64_t payload = 0;
     for (uint32_t q = 0; q < c.nRanks; ++q) payload += counts[q] * es;
-    return Execute(c, s.ops, bufs, dt, op, stream, c.nRanks == 1 || payload <= SingleStreamBytes());
+    const bool single = c.nRanks == 1 || payload <= SingleStreamBytes();
+    const CompiledSchedule* cs = nullptr;
+    HCCL_CHK(CompileCollective(c, p, bufs, !single, &cs));
+    const Schedule& s = cs->sched;
+    if (s.scratchElems * es > c.scratchBytes) return HCCL_E_INTERNAL;
+    c.lastAlgo = s.algo;
+    return Execute(c, s.ops, bufs, dt, op, stream, single, single ? nullptr : &cs->plan);
 }
 
 }  // namespace
@@ -414,6 +417,16 @@ int32_t HcclAmdCommLastAlgo(HcclComm comm)
 {
     Comm* c = AsComm(comm);
     return c == nullptr ? -1 : c->lastAlgo;
+}
+
+HcclResult HcclAmdCommCompileStats(HcclComm comm, uint64_t* hits, uint64_t* misses)
+{
+    Comm* c = AsComm(comm);
+    if (c == nullptr || hits == nullptr || misses == nullptr) return HCCL_E_PTR;
+    std::lock_guard<std::mutex> lk(c->mu);
+    *hits = c->compileHits;
+    *misses = c->compileMisses;
+    return HCCL_SUCCESS;
 }
 
 int32_t HcclAmdRingTable(uint32_t nRanks, uint32_t* cycles, uint32_t capacity)

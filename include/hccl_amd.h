@@ -199,6 +199,12 @@ extern HcclResult HcclAmdCommSetPieceBytes(HcclComm comm, uint64_t pieceBytes);
 /* Algorithm the last collective on comm executed (HcclAmdAlgo), or -1. */
 extern int32_t HcclAmdCommLastAlgo(HcclComm comm);
 
+/* Compiled-collective cache of comm: a call whose schedule parameters (operation, family, ranks, count, type, root,
+ * piece size, buffer size) match an earlier one reuses its schedule and, for the same overlap of sendBuf / recvBuf /
+ * staging, its executor plan (up to 32 entries, least recently used evicted; HCCL_AMD_PLAN_CACHE=0 disables it).
+ * *hits and *misses count the RCCL-path calls that reused or built one. */
+extern HcclResult HcclAmdCommCompileStats(HcclComm comm, uint64_t* hits, uint64_t* misses);
+
 /* Status of the IPC path of comm (synchronous read). Bit 0: a cross-rank barrier wait exceeded HCCL_AMD_IPC_TIMEOUT_MS
  * (default 60000) — the results of that and every later IPC AllReduce on comm are invalid (sticky: the communicator is
  * failed, as after an asynchronous error). Bits 8-15: bit length of the longest barrier wait of the last IPC

@@ -605,6 +605,46 @@ def test_repeated_calls_reuse_resources(worlds):
         assert O.equal_bits(O.FP32, to_host(O.FP32, recvs[r]), want)
 
 
+@pytest.mark.parametrize("algo", [R.ALGO_TWOSHOT, 3, R.ALGO_MESHCHUNK])
+@pytest.mark.parametrize("cache", ["1", "0"])
+def test_compiled_schedule_cache(worlds, monkeypatch, algo, cache):
+    """Repeated calls reuse the compiled schedule and plan (HcclAmdCommCompileStats); a call whose buffers overlap
+    differently (in-place after out-of-place, a new buffer pair, another count) still gets a plan for its own overlap,
+    so every result stays bit-exact. HCCL_AMD_PLAN_CACHE=0 compiles every call."""
+    monkeypatch.setenv("HCCL_AMD_PLAN_CACHE", cache)
+    n = 4
+    comms = worlds(n)
+    counts = [(3 << 20) // 4 + 5, (3 << 20) // 4 + 5, (3 << 20) // 4 + 5, (2 << 20) // 4 + 9, (3 << 20) // 4 + 5]
+    inplace = [False, True, False, False, True]
+    streams = [torch.cuda.Stream() for _ in range(n)]
+    for c in comms:
+        c.set_algo(algo)
+        c.set_piece_bytes(256 << 10)  # several pieces: the two-stream executor and its plan
+    try:
+        before = [c.compile_stats() for c in comms]
+        for k, (count, ip) in enumerate(zip(counts, inplace)):
+            xs = [O.random_operands(O.FP32, count, seed=3000 + 10 * k + r, edge=False) for r in range(n)]
+            sends = [to_device(O.FP32, x) for x in xs]
+            recvs = [s if ip else torch.zeros_like(s) for s in sends]
+            torch.cuda.synchronize()
+            run_ranks(n, lambda r: comms[r].all_reduce(sends[r], recvs[r], O.SUM, streams[r]))
+            torch.cuda.synchronize()
+            want = R.expected(AR, comms[0].last_algo, O.FP32, O.SUM, xs, count)
+            for r in range(n):
+                assert O.equal_bits(O.FP32, to_host(O.FP32, recvs[r]), want[r]), (k, r)
+        for c, (h0, m0) in zip(comms, before):
+            h, m = c.compile_stats()
+            if cache == "1":
+                assert (h - h0, m - m0) == (3, 2)  # counts 0 and 3 compile; calls 1, 2 and 4 reuse
+            else:
+                assert (h - h0, m - m0) == (0, 5)
+    finally:
+        torch.cuda.synchronize()
+        for c in comms:
+            c.set_algo(0)
+            c.set_piece_bytes(0)
+
+
 def test_entry_checks_match_reference(worlds):
     """Validation order and codes of all_reduce_op.cc:23-157, reduce_scatter_op.cc, reduce_op.cc:106-156."""
     comms = worlds(2)
