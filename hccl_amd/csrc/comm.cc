@@ -75,13 +75,19 @@ HcclResult Comm::NextEvent(hipEvent_t* e)
 
 HcclResult Comm::PollAsyncError()
 {
-    if (failCode != HCCL_SUCCESS) return failCode;
-    if (ipc.failWatch != nullptr && *ipc.failWatch != 0) {
-        failCode = HCCL_E_TIMEOUT;  // an IPC barrier wait exceeded its bound (IpcTimeoutTicks)
+    const int32_t known = failCode.load(std::memory_order_acquire);
+    if (known != HCCL_SUCCESS) return static_cast<HcclResult>(known);
+    HcclResult e = HCCL_SUCCESS;
+    const volatile uint32_t* w = failWord.load(std::memory_order_acquire);
+    if (w != nullptr && *w != 0) {
+        e = HCCL_E_TIMEOUT;  // an IPC barrier wait exceeded its bound (IpcTimeoutTicks)
     } else if (transport != nullptr) {
-        failCode = transport->AsyncError();
+        e = transport->AsyncError();
     }
-    return failCode;
+    if (e == HCCL_SUCCESS) return HCCL_SUCCESS;
+    int32_t expected = HCCL_SUCCESS;  // the first error seen sticks, whichever thread saw it
+    failCode.compare_exchange_strong(expected, e, std::memory_order_acq_rel);
+    return static_cast<HcclResult>(failCode.load(std::memory_order_acquire));
 }
 
 HcclResult Comm::Gate()
@@ -238,6 +244,12 @@ public:
         bool failed = false;
     };
     explicit LoopbackWorld(uint32_t n) : n_(n), boxes_(size_t(n) * n), slots_(n) {}
+    ~LoopbackWorld()
+    {
+        if (failHost_ != nullptr) (void)hipHostFree(failHost_);
+    }
+    LoopbackWorld(const LoopbackWorld&) = delete;
+    LoopbackWorld& operator=(const LoopbackWorld&) = delete;
     uint32_t n_;
     std::mutex mu_;
     std::condition_variable cv_;
@@ -249,6 +261,32 @@ public:
     bool resultOk_ = false;
     uint32_t arrived_ = 0;
     uint64_t generation_ = 0;
+
+    // the failure word of the world's IPC launches (Transport::SharedFailWord), allocated by the first rank to ask
+    uint32_t* failHost_ = nullptr;
+    uint32_t* failDev_ = nullptr;
+
+    uint32_t* FailWord(uint32_t** dev)
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (failHost_ == nullptr) {
+            uint32_t* h = nullptr;
+            if (hipHostMalloc(reinterpret_cast<void**>(&h), 64, hipHostMallocCoherent | hipHostMallocMapped) !=
+                hipSuccess) {
+                *dev = nullptr;
+                return nullptr;
+            }
+            if (hipHostGetDevicePointer(reinterpret_cast<void**>(&failDev_), h, 0) != hipSuccess) {
+                (void)hipHostFree(h);
+                *dev = nullptr;
+                return nullptr;
+            }
+            *h = 0;
+            failHost_ = h;
+        }
+        *dev = failDev_;
+        return failHost_;
+    }
 
     HcclResult Exchange(uint32_t rank, const void* mine, size_t bytes, void* all)
     {
@@ -291,6 +329,7 @@ public:
     {
         return w_->Exchange(me_, mine, bytes, all);
     }
+    uint32_t* SharedFailWord(uint32_t** dev) override { return w_->FailWord(dev); }
 
     HcclResult Group(const std::vector<P2pOp>& ops, hipStream_t stream) override
     {

@@ -6,6 +6,7 @@
 // helper streams (the reference's slave "threads") and events (its notifies).
 #pragma once
 
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <memory>
@@ -38,8 +39,16 @@ public:
     virtual bool SharedDevice() const { return false; }
     // False for a bootstrap-only transport: the communicator's only data path is the one-sided IPC kernel.
     virtual bool HasSendRecv() const { return true; }
-    // An asynchronous failure of the transport (RCCL: ncclCommGetAsyncError), HCCL_SUCCESS if none. Non-blocking.
+    // An asynchronous failure of the transport (RCCL: ncclCommGetAsyncError), HCCL_SUCCESS if none. Non-blocking and
+    // callable from any thread.
     virtual HcclResult AsyncError() { return HCCL_SUCCESS; }
+    // Loopback world: the pinned failure word all its ranks share (the world's single IPC launch writes it), owned by
+    // the world so that it outlives every rank's communicator; *dev receives its device address. nullptr elsewhere.
+    virtual uint32_t* SharedFailWord(uint32_t** dev)
+    {
+        *dev = nullptr;
+        return nullptr;
+    }
 };
 
 std::unique_ptr<Transport> MakeRcclTransport(void* uniqueId, uint32_t nRanks, uint32_t rank, HcclResult* err);
@@ -105,8 +114,11 @@ struct Comm {
     // the error itself (HCCL_E_TIMEOUT for a barrier timeout) and marks the communicator failed; every later entry
     // returns HCCL_E_SUSPENDING, the reference's status gate (Selector, src/ops/op_common/op_common.cc:89-97: a
     // communicator whose status is not READY). HcclGetCommAsyncError reports the error without changing state.
+    // failCode and failWord are read without the lock (HcclGetCommAsyncError is polled by watchdog threads while
+    // another thread may sit in a collective).
     bool failed = false;
-    HcclResult failCode = HCCL_SUCCESS;
+    std::atomic<int32_t> failCode{HCCL_SUCCESS};
+    std::atomic<const volatile uint32_t*> failWord{nullptr};  // the pinned word the IPC launches set on a timeout
 
     // Compiled collectives, least recently used evicted (a training loop repeats the same few bucket calls: they skip
     // BuildSchedule and PlanUnits after the first). HCCL_AMD_PLAN_CACHE=0 compiles every call.
@@ -117,7 +129,7 @@ struct Comm {
 
     HcclResult Init(int dev);
     HcclResult NextEvent(hipEvent_t* e);
-    // Non-blocking: the first asynchronous error seen on this communicator, HCCL_SUCCESS if none.
+    // Non-blocking, lock-free: the first asynchronous error seen on this communicator, HCCL_SUCCESS if none.
     HcclResult PollAsyncError();
     // Entry gate of every collective (call with mu held).
     HcclResult Gate();

@@ -25,7 +25,6 @@ struct Exported {
 struct RawPtrs {
     void* stg;
     uint32_t* flags;
-    uint32_t* failHost;
     uint8_t ok;
 };
 
@@ -63,14 +62,19 @@ HcclResult IpcSetup(Comm& c)
               hipDeviceSynchronize() == hipSuccess;
     if (ok) {
         *s.failHost = 0;
-        s.failWatch = s.failHost;
     } else {
         HCCL_AMD_ERR("rank %u: IPC staging allocation failed", me);
     }
+    const volatile uint32_t* watch = s.failHost;
     if (c.transport->SharedDevice()) {
+        // The world runs one launch for all ranks (issued by rank 0): its timeouts go to the world's word, which every
+        // rank watches and which outlives each rank's communicator.
+        uint32_t* wdev = nullptr;
+        uint32_t* word = ok ? c.transport->SharedFailWord(&wdev) : nullptr;
+        ok = ok && word != nullptr;
         // Every rank thread takes part in the exchange whatever its local outcome (a rank that returned early
         // would leave the others blocked in the rendezvous), and they all agree on the result.
-        RawPtrs mine{s.stg, s.flags, s.failHost, static_cast<uint8_t>(ok ? 1 : 0)};
+        RawPtrs mine{s.stg, s.flags, static_cast<uint8_t>(ok ? 1 : 0)};
         std::vector<RawPtrs> all(n);
         const HcclResult xr = c.transport->AllGatherHost(&mine, sizeof mine, all.data());
         for (uint32_t r = 0; r < n && xr == HCCL_SUCCESS; ++r) ok = ok && all[r].ok != 0;
@@ -83,7 +87,8 @@ HcclResult IpcSetup(Comm& c)
             s.peerStg[r] = all[r].stg;
             s.peerFlags[r] = all[r].flags;
         }
-        s.failWatch = all[0].failHost;  // the world's single launch is issued by rank 0 with its words
+        s.failDev = wdev;
+        watch = word;
     } else {
         // Every rank takes part in both exchanges whatever happens locally, and the outcome is agreed: either all
         // ranks have every peer mapped or all release and report NOT_SUPPORT (the caller then runs the RCCL
@@ -92,7 +97,14 @@ HcclResult IpcSetup(Comm& c)
         ok = ok && hipIpcGetMemHandle(&mine.stg, s.stg) == hipSuccess &&
              hipIpcGetMemHandle(&mine.flags, s.flags) == hipSuccess;
         std::vector<Exported> all(n);
-        HCCL_CHK(c.transport->AllGatherHost(&mine, sizeof mine, all.data()));
+        HcclResult xr = c.transport->AllGatherHost(&mine, sizeof mine, all.data());
+        if (xr != HCCL_SUCCESS) {
+            // the bootstrap failed under us: nothing was mapped; free the staging rather than leak it (a later call
+            // would otherwise allocate again) and report the transport's error
+            IpcRelease(c);
+            s.unavailable = true;
+            return xr;
+        }
         for (uint32_t r = 0; r < n && ok; ++r) {
             if (r == me) {
                 s.peerStg[r] = s.stg;
@@ -115,14 +127,15 @@ HcclResult IpcSetup(Comm& c)
         }
         const uint8_t mineOk = ok ? 1 : 0;
         std::vector<uint8_t> allOk(n);
-        HCCL_CHK(c.transport->AllGatherHost(&mineOk, 1, allOk.data()));
-        for (uint32_t r = 0; r < n; ++r) ok = ok && allOk[r] != 0;
-        if (!ok) {
+        xr = c.transport->AllGatherHost(&mineOk, 1, allOk.data());
+        for (uint32_t r = 0; r < n && xr == HCCL_SUCCESS; ++r) ok = ok && allOk[r] != 0;
+        if (xr != HCCL_SUCCESS || !ok) {
             IpcRelease(c);
             s.unavailable = true;
-            return HCCL_E_NOT_SUPPORT;
+            return xr != HCCL_SUCCESS ? xr : HCCL_E_NOT_SUPPORT;
         }
     }
+    c.failWord.store(watch, std::memory_order_release);
     s.ready = true;
     return HCCL_SUCCESS;
 }
@@ -157,10 +170,6 @@ uint64_t IpcTimeoutTicks()
     return ms * kTicksPerMs;
 }
 
-namespace {
-
-}  // namespace
-
 void IpcQuiesce(Comm& c)
 {
     if (!c.ipc.ready) return;
@@ -190,6 +199,8 @@ void IpcRelease(Comm& c)
     if (s.stg != nullptr) (void)hipFree(s.stg);
     if (s.flags != nullptr) (void)hipFree(s.flags);
     if (s.status != nullptr) (void)hipFree(s.status);
+    // the word is no longer watched before it is freed (a failure already seen stays in Comm::failCode)
+    c.failWord.store(nullptr, std::memory_order_release);
     if (s.failHost != nullptr) (void)hipHostFree(s.failHost);
     const bool unavailable = s.unavailable;
     s = IpcState{};

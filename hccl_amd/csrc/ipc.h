@@ -134,9 +134,8 @@ struct IpcState {
     uint32_t* status = nullptr;    // device words: [0] bit 0 = barrier timeout, [2..3] = tagged longest wait (IpcArgs)
     uint32_t callSeq = 0;          // IPC calls issued on the communicator (tags the wait diagnostic)
     uint32_t* failHost = nullptr;  // pinned host word the kernel sets on a barrier timeout (hipHostMalloc, coherent)
-    uint32_t* failDev = nullptr;   // its device address (IpcArgs::failHost)
-    const volatile uint32_t* failWatch = nullptr;  // the word this rank's host polls: its own, or, in a loopback world
-                                                   // (one launch for all ranks, issued by rank 0), rank 0's
+    uint32_t* failDev = nullptr;   // the device address the launches write (IpcArgs::failHost): of failHost, or in a
+                                   // loopback world of the world's word (Transport::SharedFailWord)
     void* peerStg[kIpcMaxRanks] = {};
     uint32_t* peerFlags[kIpcMaxRanks] = {};
     bool opened[kIpcMaxRanks] = {};

@@ -327,8 +327,7 @@ HcclResult HcclGetCommAsyncError(HcclComm comm, HcclResult* asyncError)
 {
     Comm* c = AsComm(comm);
     if (c == nullptr || asyncError == nullptr) return HCCL_E_PTR;
-    std::lock_guard<std::mutex> lk(c->mu);
-    *asyncError = c->PollAsyncError();
+    *asyncError = c->PollAsyncError();  // lock-free: a watchdog thread never waits behind a collective
     return HCCL_SUCCESS;
 }
 

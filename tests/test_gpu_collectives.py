@@ -645,6 +645,54 @@ def test_compiled_schedule_cache(worlds, monkeypatch, algo, cache):
             c.set_piece_bytes(0)
 
 
+def test_async_error_does_not_wait_for_a_collective():
+    """HcclGetCommAsyncError is lock-free: a watchdog thread gets an answer at once while another thread sits inside a
+    collective on the same communicator (here rank 0 waiting in the loopback rendezvous for rank 1)."""
+    import time
+    comms = H.loopback_world(2)
+    try:
+        xs = [torch.ones(1 << 20, device="cuda") for _ in range(2)]
+        ss = [torch.cuda.Stream() for _ in range(2)]
+        for c in comms:
+            c.set_algo(R.ALGO_TWOSHOT)
+        torch.cuda.synchronize()
+        t = threading.Thread(target=lambda: comms[0].all_reduce(xs[0], xs[0], O.SUM, ss[0]))
+        t.start()
+        time.sleep(0.5)
+        assert t.is_alive()  # rank 0 holds its communicator, waiting for rank 1's sends
+        t0 = time.perf_counter()
+        assert comms[0].async_error() == 0
+        assert time.perf_counter() - t0 < 0.1
+        comms[1].all_reduce(xs[1], xs[1], O.SUM, ss[1])
+        t.join(120)
+        assert not t.is_alive()
+        torch.cuda.synchronize()
+        for x in xs:
+            assert torch.equal(x, torch.full_like(x, 2.0))
+    finally:
+        torch.cuda.synchronize()
+        for c in comms:
+            c.destroy()
+
+
+def test_loopback_failure_word_outlives_rank0():
+    """A loopback world's IPC launches report timeouts into one word the world owns, so a rank's async-error query
+    stays valid after another rank's communicator (rank 0, which issues the world's launch) is destroyed."""
+    comms = H.loopback_world(2)
+    xs = [torch.ones(4096, device="cuda") for _ in range(2)]
+    ss = [torch.cuda.Stream() for _ in range(2)]
+    for c in comms:
+        c.set_algo(7)  # IPC two-shot: sets up the one-sided path
+    torch.cuda.synchronize()
+    run_ranks(2, lambda r: comms[r].all_reduce(xs[r], xs[r], O.SUM, ss[r]))
+    torch.cuda.synchronize()
+    assert comms[0].last_algo == 7
+    assert all(torch.equal(x, torch.full_like(x, 2.0)) for x in xs)
+    comms[0].destroy()
+    assert comms[1].async_error() == 0
+    comms[1].destroy()
+
+
 def test_entry_checks_match_reference(worlds):
     """Validation order and codes of all_reduce_op.cc:23-157, reduce_scatter_op.cc, reduce_op.cc:106-156."""
     comms = worlds(2)
