@@ -61,8 +61,19 @@ bool ParseExecTimeoutSeconds(const char* env, double* seconds)
         const size_t decimals = len - size_t(dot - env) - 1;
         if (dot == env || decimals == 0 || decimals > 2) return false;
     }
-    const double v = std::strtod(env, nullptr);
-    if (!(v >= 0.0) || v > 4294967295.0) return false;
+    // parsed by hand: strtod would follow the process's LC_NUMERIC, where the decimal mark may be a comma
+    uint64_t whole = 0;
+    for (const char* q = env; *q != '\0' && q != dot; ++q) {
+        whole = whole * 10 + uint64_t(*q - '0');
+        if (whole > 4294967295ull) return false;
+    }
+    double frac = 0.0;
+    if (dot != nullptr) {
+        double scale = 0.1;
+        for (const char* q = dot + 1; *q != '\0'; ++q, scale /= 10) frac += scale * (*q - '0');
+    }
+    const double v = double(whole) + frac;
+    if (v > 4294967295.0) return false;
     *seconds = v;
     return true;
 }

@@ -532,40 +532,50 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
         return HCCL_SUCCESS;
     }
 
-    // loopback world: one launch for every rank, issued by rank 0 behind every rank's stream
+    // loopback world: one launch for every rank, issued by rank 0 behind every rank's stream. Every rank takes part in
+    // both exchanges whatever its local outcome (one that returned early would leave the others in the rendezvous),
+    // and a failure anywhere is every rank's result.
     struct Part {
         const void* in;
         void* out;
         hipEvent_t ready;
+        int32_t code;
     };
-    Part mine{sendBuf, recvBuf, nullptr};
+    Part mine{sendBuf, recvBuf, nullptr, HCCL_SUCCESS};
     c.nextEvent = 0;
-    HCCL_CHK(c.NextEvent(&mine.ready));
-    HIP_CHK(hipEventRecord(mine.ready, stream));
+    mine.code = c.NextEvent(&mine.ready);
+    if (mine.code == HCCL_SUCCESS && hipEventRecord(mine.ready, stream) != hipSuccess) mine.code = HCCL_E_RUNTIME;
     std::vector<Part> all(n);
     HCCL_CHK(c.transport->AllGatherHost(&mine, sizeof mine, all.data()));
-    hipEvent_t done = nullptr;
-    if (c.rank == 0) {
+    HcclResult code = HCCL_SUCCESS;
+    for (uint32_t r = 0; r < n && code == HCCL_SUCCESS; ++r) code = static_cast<HcclResult>(all[r].code);
+    struct Done {
+        hipEvent_t ev;
+        int32_t code;
+    };
+    Done done{nullptr, code};
+    if (c.rank == 0 && code == HCCL_SUCCESS) {
         a.me = -1;
         a.aligned = true;
-        for (uint32_t r = 0; r < n; ++r) {
+        for (uint32_t r = 0; r < n && done.code == HCCL_SUCCESS; ++r) {
             a.aligned = a.aligned && Aligned16(all[r].in, all[r].out);
-            HIP_CHK(hipStreamWaitEvent(stream, all[r].ready, 0));
+            if (hipStreamWaitEvent(stream, all[r].ready, 0) != hipSuccess) done.code = HCCL_E_RUNTIME;
         }
-        for (const Launch& l : launches) {
+        for (size_t k = 0; k < launches.size() && done.code == HCCL_SUCCESS; ++k) {
             for (uint32_t r = 0; r < n; ++r) {
-                a.in[r] = at(all[r].in, l.off);
-                a.out[r] = at(all[r].out, l.off);
+                a.in[r] = at(all[r].in, launches[k].off);
+                a.out[r] = at(all[r].out, launches[k].off);
             }
-            geometry(a, l.cnt);
-            HCCL_CHK(LaunchIpcCollective(a, s.blocks, n, dt, op, stream));
+            geometry(a, launches[k].cnt);
+            done.code = LaunchIpcCollective(a, s.blocks, n, dt, op, stream);
         }
-        HCCL_CHK(c.NextEvent(&done));
-        HIP_CHK(hipEventRecord(done, stream));
+        if (done.code == HCCL_SUCCESS) done.code = c.NextEvent(&done.ev);
+        if (done.code == HCCL_SUCCESS && hipEventRecord(done.ev, stream) != hipSuccess) done.code = HCCL_E_RUNTIME;
     }
-    std::vector<hipEvent_t> dones(n);
+    std::vector<Done> dones(n);
     HCCL_CHK(c.transport->AllGatherHost(&done, sizeof done, dones.data()));
-    if (c.rank != 0) HIP_CHK(hipStreamWaitEvent(stream, dones[0], 0));
+    if (dones[0].code != HCCL_SUCCESS) return static_cast<HcclResult>(dones[0].code);
+    if (c.rank != 0) HIP_CHK(hipStreamWaitEvent(stream, dones[0].ev, 0));
     return HCCL_SUCCESS;
 }
 
