@@ -144,10 +144,11 @@ def select_algo(op_type: int, n_ranks: int, nbytes: int, special: bool = False) 
 
 
 def select_aiv_algo(op_type: int, n_ranks: int, count: int, dtype: int, op: int, core_limit: int = 0,
-                    strict: bool = False):
+                    strict: bool = False, aiv_only: bool = False):
     """(HcclAmdAivVariant, groupSize) the AIV engine takes (HcclAmdSelectAivAlgo); core_limit 0 = the default."""
     g = ctypes.c_uint32(1)
-    v = lib.HcclAmdSelectAivAlgo(int(op_type), n_ranks, count, int(dtype), int(op), core_limit, 1 if strict else 0,
+    flags = (1 if strict else 0) | (2 if aiv_only else 0)
+    v = lib.HcclAmdSelectAivAlgo(int(op_type), n_ranks, count, int(dtype), int(op), core_limit, flags,
                                  ctypes.byref(g))
     return AivVariant(v), g.value
 

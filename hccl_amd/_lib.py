@@ -83,6 +83,7 @@ class Algo(enum.IntEnum):
     MESH_CHUNK = 8
     IPC = 9
     AIV = 10
+    AIV_ONLY = 11
 
 
 class AivVariant(enum.IntEnum):

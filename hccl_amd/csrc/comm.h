@@ -153,7 +153,7 @@ HcclResult IpcPlanForFamily(int32_t opType, int32_t family, uint32_t n, uint64_t
 // (HcclAmdAivVariant, include/hccl_amd.h), HCCL_AMD_AIV_NOT_MATCHED when the selector would fall back to the AICPU
 // engine; *plan receives the one-sided kernel's plan for a matched variant.
 int32_t SelectAivPlan(int32_t opType, uint32_t n, uint64_t count, HcclDataType dt, HcclReduceOp op, bool strict,
-                      uint64_t cclBytes, uint32_t coreLimit, IpcPlan* plan, uint32_t* group);
+                      bool aivOnly, uint64_t cclBytes, uint32_t coreLimit, IpcPlan* plan, uint32_t* group);
 // HCCL_AMD_AIV_CORE_LIMIT (default 48, MAX_NUM_BLOCKS of aiv_defines.h:35).
 uint32_t AivCoreLimit();
 // HCCL_OP_EXPANSION_MODE selects the AIV engine ("AIV").

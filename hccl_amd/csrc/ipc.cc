@@ -315,13 +315,15 @@ bool ExpansionModeAiv()
 }
 
 int32_t SelectAivPlan(int32_t opType, uint32_t n, uint64_t count, HcclDataType dt, HcclReduceOp op, bool strict,
-                      uint64_t cclBytes, uint32_t coreLimit, IpcPlan* plan, uint32_t* group)
+                      bool aivOnly, uint64_t cclBytes, uint32_t coreLimit, IpcPlan* plan, uint32_t* group)
 {
     // Common rejections of AllReduceAutoSelector / ReduceScatterAutoSelector::SelectAivAlgo
     // (all_reduce_auto_selector.cc:591-683, reduce_scatter_auto_selector.cc:537-600): the order-preserved (STRICT)
     // mode, PROD, UINT64 / FP64 and more than MAX_RANK_SIZE ranks fall back to the AICPU engine; so does data of
     // AIV_MAX_PER_RANK_DATA_SIZE (8 MiB, auto_selector_base.h:24) x rankSize or more, or above 16 CCL buffers
     // (AIV_MAX_CCL_LOOP_NUM, hccl_aiv_utils.h:33). ReduceAutoSelector has no AIV selection: Reduce stays AICPU.
+    // AIV_ONLY (OpExecuteConfig::AIV_ONLY) lifts the 8 MiB x rankSize bound, not the CCL one
+    // (all_reduce_auto_selector.cc:650-661, reduce_scatter_auto_selector.cc:597-610).
     const uint64_t es = DataTypeSize(dt);
     if (es == 0 || n < 2 || n > 512) return HCCL_AMD_AIV_NOT_MATCHED;
     if (opType != HCCL_AMD_OP_ALLREDUCE && opType != HCCL_AMD_OP_REDUCE_SCATTER) return HCCL_AMD_AIV_NOT_MATCHED;
@@ -334,7 +336,7 @@ int32_t SelectAivPlan(int32_t opType, uint32_t n, uint64_t count, HcclDataType d
     int32_t variant;
     if (opType == HCCL_AMD_OP_ALLREDUCE) {
         const uint64_t dataSize = count * es;
-        if (dataSize >= maxPerRank * n || dataSize > cclBytes * 16) return HCCL_AMD_AIV_NOT_MATCHED;
+        if ((!aivOnly && dataSize >= maxPerRank * n) || dataSize > cclBytes * 16) return HCCL_AMD_AIV_NOT_MATCHED;
         // n <= AR_AIV_BOARD_SIZE (8): one-shot below AR_AIV_SMALL_DATA_SIZE_IN_BOARD (128 KiB); above 8 ranks
         // IsSmallData (< 512 KiB, auto_selector_base.cc:94)
         const bool oneShot = n <= 8 ? dataSize < (128ull << 10) : dataSize < (512ull << 10);
@@ -371,7 +373,7 @@ int32_t SelectAivPlan(int32_t opType, uint32_t n, uint64_t count, HcclDataType d
         }
     } else {
         const uint64_t totalSize = count * es * n;
-        if (totalSize >= maxPerRank * n || totalSize > cclBytes * 16) return HCCL_AMD_AIV_NOT_MATCHED;
+        if ((!aivOnly && totalSize >= maxPerRank * n) || totalSize > cclBytes * 16) return HCCL_AMD_AIV_NOT_MATCHED;
         // AivTempReduceScatterMesh1D::CalNumBlocks (aiv_temp_reduce_scatter_mesh_1D.cc:87-97): the core limit, at most
         // 2n below 512 KiB of output; aiv_reduce_scatter_op.h:23-37 takes the big-data kernel above 2n blocks (out =
         // rank 0's copy, then (op)= rank 1 .. n-1: O2, aiv_reduce_scatter_mesh_1d_bigdata.h:85-101), the local tree

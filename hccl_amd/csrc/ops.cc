@@ -85,17 +85,21 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     // kernels' orders on the one-sided kernel. What it does not match, or cannot run (no peer mappings, a capture
     // before the set-up), takes the AICPU engine's selection below, as the reference falls back
     // (AutoSelectorBase::ProcessAivConfig, auto_selector_base.cc:353-371).
-    if (p.algo == HCCL_AMD_ALGO_AIV || (p.algo == HCCL_AMD_ALGO_AUTO && ExpansionModeAiv())) {
+    // AIV_ONLY (the reference's OpExecuteConfig::AIV_ONLY, a communicator's configured expansion mode) takes no
+    // fallback: an operation the AIV engine does not match returns HCCL_E_NOT_SUPPORT (op_common.cc:115-122).
+    const bool aivOnly = p.algo == HCCL_AMD_ALGO_AIV_ONLY;
+    if (aivOnly || p.algo == HCCL_AMD_ALGO_AIV || (p.algo == HCCL_AMD_ALGO_AUTO && ExpansionModeAiv())) {
         IpcPlan plan{};
         const int32_t v = SelectAivPlan(opType, c.nRanks, count, dt, op, NeedStrictOrder(opType, dt, op, c.nRanks),
-                                        c.cclBytes, AivCoreLimit(), &plan, nullptr);
+                                        aivOnly, c.cclBytes, AivCoreLimit(), &plan, nullptr);
         if (v != HCCL_AMD_AIV_NOT_MATCHED) {
             const HcclResult r = RunIpcPlan(c, opType, plan, sendBuf, recvBuf, count, dt, op, root, stream);
             if (r != HCCL_E_NOT_SUPPORT) {
-                c.lastAlgo = HCCL_AMD_ALGO_AIV;
+                c.lastAlgo = aivOnly ? HCCL_AMD_ALGO_AIV_ONLY : HCCL_AMD_ALGO_AIV;
                 return r;
             }
         }
+        if (aivOnly) return HCCL_E_NOT_SUPPORT;
         p.algo = HCCL_AMD_ALGO_AUTO;
     }
     // an IPC-only communicator (bootstrap transport without send/recv) runs every reducing op on the IPC kernel in
@@ -390,7 +394,7 @@ HcclResult HcclAmdCommSetAlgo(HcclComm comm, int32_t algo)
 {
     Comm* c = AsComm(comm);
     if (c == nullptr) return HCCL_E_PTR;
-    if (algo < HCCL_AMD_ALGO_AUTO || algo > HCCL_AMD_ALGO_AIV) return HCCL_E_PARA;
+    if (algo < HCCL_AMD_ALGO_AUTO || algo > HCCL_AMD_ALGO_AIV_ONLY) return HCCL_E_PARA;
     c->algoOverride = algo;
     return HCCL_SUCCESS;
 }
@@ -471,9 +475,9 @@ HcclResult HcclAmdExecutorPlan(const HcclAmdIrOp* ops, uint64_t numOps, uint32_t
 }
 
 int32_t HcclAmdSelectAivAlgo(int32_t opType, uint32_t nRanks, uint64_t count, HcclDataType dataType, HcclReduceOp op,
-                             uint32_t coreLimit, int32_t strict, uint32_t* groupSize)
+                             uint32_t coreLimit, int32_t flags, uint32_t* groupSize)
 {
-    return SelectAivPlan(opType, nRanks, count, dataType, op, strict != 0, CclBytesDefault(),
+    return SelectAivPlan(opType, nRanks, count, dataType, op, (flags & 1) != 0, (flags & 2) != 0, CclBytesDefault(),
                          coreLimit != 0 ? coreLimit : AivCoreLimit(), nullptr, groupSize);
 }
 

@@ -111,9 +111,11 @@ typedef enum {
                                           (owner first, then the peers in a per-sub-slice rotated order) */
     HCCL_AMD_ALGO_IPC = 9,             /* the one-sided kernel in the order family the auto selector picks (one-shot
                                           O1 / two-shot O2 / MeshChunk O6 ...): the auto path's bits over IPC */
-    HCCL_AMD_ALGO_AIV = 10             /* the reference's AIV engine (HCCL_OP_EXPANSION_MODE=AIV): SelectAivAlgo's
+    HCCL_AMD_ALGO_AIV = 10,            /* the reference's AIV engine (HCCL_OP_EXPANSION_MODE=AIV): SelectAivAlgo's
                                           choice and orders on the one-sided kernel; what it does not match runs
                                           the auto (AICPU) selection, as the reference falls back */
+    HCCL_AMD_ALGO_AIV_ONLY = 11        /* the AIV engine with no fallback (OpExecuteConfig::AIV_ONLY): no 8 MiB x n
+                                          bound, and what SelectAivAlgo does not match returns HCCL_E_NOT_SUPPORT */
 } HcclAmdAlgo;
 
 /* Variant of the reference's AIV engine a call takes (HcclAmdSelectAivAlgo). */
@@ -128,11 +130,12 @@ typedef enum {
 } HcclAmdAivVariant;
 
 /* The AIV-engine variant an operation would take (opType ALLREDUCE or REDUCE_SCATTER; count = recvCount for
- * ReduceScatter) on nRanks ranks with `coreLimit` vector cores (0 = HCCL_AMD_AIV_CORE_LIMIT, default 48), the CCL
- * buffer HCCL_BUFFSIZE and strict != 0 for HCCL_DETERMINISTIC=strict. *groupSize (may be NULL) receives the slices per
- * rank of HCCL_AMD_AIV_AR_TWOSHOT_LARGE (1 otherwise). Returns an HcclAmdAivVariant. */
+ * ReduceScatter) on nRanks ranks with `coreLimit` vector cores (0 = HCCL_AMD_AIV_CORE_LIMIT, default 48) and the CCL
+ * buffer HCCL_BUFFSIZE. flags: bit 0 = HCCL_DETERMINISTIC=strict, bit 1 = AIV_ONLY (HCCL_AMD_ALGO_AIV_ONLY).
+ * *groupSize (may be NULL) receives the slices per rank of HCCL_AMD_AIV_AR_TWOSHOT_LARGE (1 otherwise). Returns an
+ * HcclAmdAivVariant. */
 extern int32_t HcclAmdSelectAivAlgo(int32_t opType, uint32_t nRanks, uint64_t count, HcclDataType dataType,
-                                    HcclReduceOp op, uint32_t coreLimit, int32_t strict, uint32_t* groupSize);
+                                    HcclReduceOp op, uint32_t coreLimit, int32_t flags, uint32_t* groupSize);
 
 /* Build rank `rank`'s schedule. If ops == NULL only *numOps is written. scratchElems receives the number of
  * scratch elements the schedule addresses. pieceBytes = 0 picks the default pipelining granule. */

@@ -442,17 +442,18 @@ AIV_NOT_MATCHED, AIV_AR_ONESHOT, AIV_AR_TWOSHOT_LARGE, AIV_AR_TWOSHOT_SMALL, AIV
 AIV_CORE_LIMIT = 48  # MAX_NUM_BLOCKS, aiv_defines.h:35
 
 
-def aiv_select(op_type, n, count, es, dt64, prod, strict=False, ccl=None, core_limit=AIV_CORE_LIMIT):
+def aiv_select(op_type, n, count, es, dt64, prod, strict=False, ccl=None, core_limit=AIV_CORE_LIMIT, aiv_only=False):
     """SelectAivAlgo (all_reduce_auto_selector.cc:591-683, reduce_scatter_auto_selector.cc:537-600) and the variant
     the AIV kernels take for `core_limit` vector cores (aiv_temp_all_reduce_mesh_1D_twoshot.cc:88-100,
     aiv_all_reduce_mesh_1d_twoshot.h:330-346; aiv_temp_reduce_scatter_mesh_1D.cc:87-97, aiv_reduce_scatter_op.h:23-37).
-    dt64: UINT64 or FP64 (the AIV path rejects them). Returns (variant, groupSize)."""
+    dt64: UINT64 or FP64 (the AIV path rejects them). aiv_only: OpExecuteConfig::AIV_ONLY, which drops the
+    8 MiB x rankSize bound (all_reduce_auto_selector.cc:650-661). Returns (variant, groupSize)."""
     ccl = ccl_bytes_from_env() if ccl is None else ccl
     if op_type not in (0, 1) or strict or prod or dt64 or n < 2:
         return AIV_NOT_MATCHED, 1
     if op_type == 0:
         size = count * es
-        if size >= (8 << 20) * n or size > ccl * 16:
+        if (not aiv_only and size >= (8 << 20) * n) or size > ccl * 16:
             return AIV_NOT_MATCHED, 1
         if size < ((128 << 10) if n <= 8 else (512 << 10)):
             return AIV_AR_ONESHOT, 1
@@ -461,7 +462,7 @@ def aiv_select(op_type, n, count, es, dt64, prod, strict=False, ccl=None, core_l
             return AIV_AR_TWOSHOT_LARGE, (blocks - n) // n
         return AIV_AR_TWOSHOT_SMALL, 1
     total = count * es * n
-    if total >= (8 << 20) * n or total > ccl * 16:
+    if (not aiv_only and total >= (8 << 20) * n) or total > ccl * 16:
         return AIV_NOT_MATCHED, 1
     blocks = core_limit
     if count * es < (512 << 10):

@@ -464,6 +464,46 @@ def test_aiv_expansion_mode_env_and_fallback(worlds, monkeypatch):
         assert O.equal_bits(O.FP32, outs[r], want[r]), r
 
 
+def test_aiv_only_has_no_fallback(worlds):
+    """HCCL_AMD_ALGO_AIV_ONLY (OpExecuteConfig::AIV_ONLY): the AIV engine above 8 MiB x n as well (64 MiB at 8 ranks
+    runs the large-core two-shot, bit-exact), and an operation it does not match (PROD, Reduce) returns
+    HCCL_E_NOT_SUPPORT on every rank instead of falling back (op_common.cc:115-122)."""
+    n, count = 8, (64 << 20) // 4 + 3
+    comms = worlds(n)
+    xs = [O.random_operands(O.FP32, count, seed=1500 + r, edge=False) for r in range(n)]
+    assert H.select_aiv_algo(AR, n, count, O.FP32, O.SUM)[0] == H.AivVariant.NOT_MATCHED
+    variant, group = H.select_aiv_algo(AR, n, count, O.FP32, O.SUM, aiv_only=True)
+    assert variant == H.AivVariant.AR_TWOSHOT_LARGE
+    used, outs = collective(comms, AR, H.Algo.AIV_ONLY, O.FP32, O.SUM, xs, count)
+    assert used == H.Algo.AIV_ONLY
+    want = R.allreduce_aiv(O.FP32, O.SUM, xs, int(variant), group)
+    for r in range(n):
+        assert O.equal_bits(O.FP32, outs[r], want[r]), r
+    small = [torch.ones(1024, device="cuda") for _ in range(n)]
+    ss = [torch.cuda.Stream() for _ in range(n)]
+    for c in comms:
+        c.set_algo(H.Algo.AIV_ONLY)
+    try:
+        for call in (lambda r: comms[r].all_reduce(small[r], small[r], O.PROD, ss[r]),
+                     lambda r: comms[r].reduce(small[r], small[r], 0, O.SUM, ss[r])):
+            codes = [None] * n
+
+            def body(r, call=call):
+                try:
+                    call(r)
+                    codes[r] = 0
+                except H.HcclError as e:
+                    codes[r] = e.code
+
+            run_ranks(n, body)
+            assert codes == [H.HcclResult.HCCL_E_NOT_SUPPORT] * n, codes
+        torch.cuda.synchronize()
+        assert all(torch.equal(x, torch.ones_like(x)) for x in small)  # nothing ran
+    finally:
+        for c in comms:
+            c.set_algo(0)
+
+
 @pytest.mark.parametrize("n,layout", [(2, "ragged"), (4, "gapped"), (8, "ragged"), (8, "overlap"), (3, "empty")])
 @pytest.mark.parametrize("dtype,op", [(O.FP32, O.SUM), (O.FP16, O.SUM), (O.BFP16, O.MAX), (O.INT32, O.PROD),
                                       (O.INT64, O.MIN)], ids=lambda v: str(v))
