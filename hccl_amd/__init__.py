@@ -214,6 +214,13 @@ class Comm:
     def last_algo(self) -> int:
         return lib.HcclAmdCommLastAlgo(self.handle)
 
+    def execute(self, ops, nops: int, send: torch.Tensor, recv: torch.Tensor, op: int = HcclReduceOp.SUM,
+                single_stream: bool = False, stream=None, dtype=None) -> None:
+        """HcclAmdCommExecute: run one rank's IR program (ctypes array of HcclAmdIrOp) on this communicator."""
+        dt = hccl_dtype(send) if dtype is None else int(dtype)
+        check("HcclAmdCommExecute", lib.HcclAmdCommExecute(self.handle, ops, nops, _ptr(send), _ptr(recv), dt, int(op),
+                                                           1 if single_stream else 0, _stream(stream)))
+
     def compile_stats(self) -> tuple:
         """(hits, misses) of the communicator's compiled-collective cache (HcclAmdCommCompileStats)."""
         h, m = ctypes.c_uint64(0), ctypes.c_uint64(0)

@@ -422,6 +422,44 @@ int32_t HcclAmdCommLastAlgo(HcclComm comm)
     return c == nullptr ? -1 : c->lastAlgo;
 }
 
+HcclResult HcclAmdCommExecute(HcclComm comm, const HcclAmdIrOp* ops, uint64_t numOps, void* sendBuf, void* recvBuf,
+                              HcclDataType dataType, HcclReduceOp op, int32_t singleStream, aclrtStream stream)
+{
+    Comm* c = AsComm(comm);
+    if (c == nullptr || stream == nullptr || (ops == nullptr && numOps != 0)) return HCCL_E_PTR;
+    HCCL_CHK(CheckReduceDataType(dataType));
+    HCCL_CHK(CheckReduceOp(dataType, op));
+    const uint64_t es = DataTypeSize(dataType);
+    // Every record must be well formed; staging references must lie inside the communicator's staging (the user
+    // buffers' extents are the caller's contract, as for the collectives).
+    auto bufOk = [&](int32_t b, uint64_t off, uint64_t cnt) {
+        if (b == HCCL_AMD_BUF_INPUT) return sendBuf != nullptr;
+        if (b == HCCL_AMD_BUF_OUTPUT) return recvBuf != nullptr;
+        if (b != HCCL_AMD_BUF_SCRATCH || c->scratch == nullptr) return false;
+        return off <= c->scratchBytes / es && cnt <= c->scratchBytes / es - off;
+    };
+    for (uint64_t i = 0; i < numOps; ++i) {
+        const HcclAmdIrOp& o = ops[i];
+        const bool p2p = o.kind == HCCL_AMD_IR_SEND || o.kind == HCCL_AMD_IR_RECV;
+        if (o.kind < HCCL_AMD_IR_COPY || o.kind > HCCL_AMD_IR_RECV) return HCCL_E_PARA;
+        if (p2p && (o.peer < 0 || static_cast<uint32_t>(o.peer) >= c->nRanks)) return HCCL_E_PARA;
+        const int32_t wantSrc = o.kind == HCCL_AMD_IR_RECV ? 0 : (o.kind == HCCL_AMD_IR_REDUCE ? -1 : 1);
+        if ((wantSrc >= 0 && o.nsrc != wantSrc) || (wantSrc < 0 && (o.nsrc < 1 || o.nsrc > HCCL_AMD_IR_MAX_SRC))) {
+            return HCCL_E_PARA;
+        }
+        if (o.kind != HCCL_AMD_IR_SEND && !bufOk(o.dstBuf, o.dstOff, o.count)) return HCCL_E_PARA;
+        for (int j = 0; j < o.nsrc; ++j) {
+            if (!bufOk(o.srcBuf[j], o.srcOff[j], o.count)) return HCCL_E_PARA;
+        }
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    HCCL_CHK(c->Gate());
+    HIP_CHK(hipSetDevice(c->device));
+    const std::vector<HcclAmdIrOp> prog(ops, ops + numOps);
+    void* bufs[3] = {sendBuf, recvBuf, c->scratch};
+    return Execute(*c, prog, bufs, dataType, op, static_cast<hipStream_t>(stream), singleStream != 0);
+}
+
 HcclResult HcclAmdCommCompileStats(HcclComm comm, uint64_t* hits, uint64_t* misses)
 {
     Comm* c = AsComm(comm);

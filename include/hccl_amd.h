@@ -202,6 +202,16 @@ extern HcclResult HcclAmdCommSetPieceBytes(HcclComm comm, uint64_t pieceBytes);
 /* Algorithm the last collective on comm executed (HcclAmdAlgo), or -1. */
 extern int32_t HcclAmdCommLastAlgo(HcclComm comm);
 
+/* Runs one rank's IR program on comm's executor: what every collective runs after it has built its schedule (SEND/RECV
+ * groups on the transport, folds and copies on the reduce stream, the cross-stream waits derived from the records'
+ * byte ranges; singleStream != 0 puts everything on `stream` in program order). Collective over the peers the program
+ * names, whose programs must post matching groups. For custom schedules and for testing the transport and executor.
+ * Records are checked for form (kind, operand count, peer < rank count, buffer ids; staging inside the communicator's
+ * staging); the extents of sendBuf / recvBuf are the caller's contract. */
+extern HcclResult HcclAmdCommExecute(HcclComm comm, const HcclAmdIrOp* ops, uint64_t numOps, void* sendBuf,
+                                     void* recvBuf, HcclDataType dataType, HcclReduceOp op, int32_t singleStream,
+                                     aclrtStream stream);
+
 /* Compiled-collective cache of comm: a call whose schedule parameters (operation, family, ranks, count, type, root,
  * piece size, buffer size) match an earlier one reuses its schedule and, for the same overlap of sendBuf / recvBuf /
  * staging, its executor plan (up to 32 entries, least recently used evicted; HCCL_AMD_PLAN_CACHE=0 disables it).

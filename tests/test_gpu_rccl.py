@@ -97,3 +97,101 @@ def test_rccl_two_ranks_one_gpu(tmp_path):
         if "HcclCommInitRootInfo returned HCCL_E_PARA" in msg or "Duplicate GPU" in msg or len(res) < 2:
             pytest.skip(f"RCCL does not run two ranks on one GPU here: {msg}")
         raise AssertionError(msg)
+
+
+def _ir(kind, count, dst=(-1, 0), srcs=(), peer=-1, group=0):
+    import hccl_amd as H
+    o = H.HcclAmdIrOp()
+    o.kind, o.peer, o.nsrc, o.group, o.count = int(kind), peer, len(srcs), group, count
+    o.dstBuf, o.dstOff = dst
+    for j, (b, off) in enumerate(srcs):
+        o.srcBuf[j], o.srcOff[j] = b, off
+    return o
+
+
+def self_loop_program(n_el, pieces):
+    """A one-rank program that drives the RCCL transport and the executor the way the schedules do: `pieces` groups,
+    each sending a piece of the input to itself into one of two staging slots at the front of recvBuf (slot reuse:
+    write-after-read waits on the fold two pieces back), each followed by a two-operand fold into an accumulator;
+    then one group of several same-peer sends (matched in order) that copies the accumulator to a final region, and a
+    three-operand in-place fold over it. Layout of recvBuf: [slot 0 | slot 1 | acc (n_el) | final (n_el)]."""
+    import hccl_amd as H
+    IN, OUT = 0, 1
+    L = n_el // pieces
+    acc, fin = 2 * L, 2 * L + n_el
+    prog, g = [], 0
+    for t in range(pieces):
+        slot = (t % 2) * L
+        prog.append(_ir(H.IrKind.SEND, L, srcs=[(IN, t * L)], peer=0, group=g))
+        prog.append(_ir(H.IrKind.RECV, L, dst=(OUT, slot), peer=0, group=g))
+        g += 1
+        prog.append(_ir(H.IrKind.REDUCE, L, dst=(OUT, acc + t * L), srcs=[(IN, t * L), (OUT, slot)]))
+    for t in range(pieces):
+        prog.append(_ir(H.IrKind.SEND, L, srcs=[(OUT, acc + t * L)], peer=0, group=g))
+        prog.append(_ir(H.IrKind.RECV, L, dst=(OUT, fin + t * L), peer=0, group=g))
+    g += 1
+    for t in range(pieces):
+        prog.append(_ir(H.IrKind.REDUCE, L, dst=(OUT, fin + t * L),
+                        srcs=[(OUT, fin + t * L), (OUT, acc + t * L), (IN, t * L)]))
+    arr = (H.HcclAmdIrOp * len(prog))(*prog)
+    return arr, len(prog), 2 * L + 2 * n_el
+
+
+def _self_loop_worker(ri_path, q):
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        import torch
+        import hccl_amd as H
+        torch.cuda.set_device(0)
+        comm = H.comm_init_root_info(1, H.get_root_info(), 0)
+        results = []
+        for n_el, pieces, single in ((1 << 20, 16, False), (3 << 20, 48, False), (1 << 16, 4, True)):
+            arr, nops, out_len = self_loop_program(n_el, pieces)
+            x = torch.rand(n_el, device="cuda", dtype=torch.float32, generator=torch.Generator("cuda").manual_seed(n_el))
+            out = torch.full((out_len,), float("nan"), device="cuda")
+            s = torch.cuda.Stream()
+            torch.cuda.synchronize()
+            for _ in range(3):  # repeated: the event pool and the staging slots are reused
+                comm.execute(arr, nops, x, out, H.HcclReduceOp.SUM, single, s)
+            torch.cuda.synchronize()
+            L = n_el // pieces
+            acc = out[2 * L:2 * L + n_el]
+            fin = out[2 * L + n_el:]
+            want_acc = x + x
+            want_fin = x + (want_acc + want_acc)  # fold [fin, acc, in]: in + (acc + fin), fin = acc after the copy
+            ok = torch.equal(acc, want_acc) and torch.equal(fin, want_fin) and \
+                torch.equal(out[(pieces - 2) % 2 * L:(pieces - 2) % 2 * L + L], x[(pieces - 2) * L:(pieces - 1) * L])
+            results.append((n_el, pieces, single, ok))
+        bad = _ir(H.IrKind.SEND, 16, srcs=[(0, 0)], peer=1)  # peer outside the communicator
+        arr = (H.HcclAmdIrOp * 1)(bad)
+        try:
+            comm.execute(arr, 1, x, out, H.HcclReduceOp.SUM, False, s)
+            rejected = False
+        except H.HcclError as e:
+            rejected = e.code == H.HcclResult.HCCL_E_PARA
+        comm.destroy()
+        q.put(("ok", results, rejected))
+    except Exception as e:  # noqa: BLE001
+        q.put(("err", f"{type(e).__name__}: {e}\n{traceback.format_exc()}", None))
+
+
+def test_rccl_transport_and_executor_self_loop(tmp_path):
+    """RCCL send/recv groups on hardware through the executor (the RCCL transport had never moved data):
+    a one-rank RCCL communicator runs programs of the schedules' shape over self send/recv (HcclAmdCommExecute):
+    pipelined groups into reused staging slots on the link stream, two- and three-operand folds on the reduce stream
+    behind the derived event waits, a group of several same-peer messages, in both executor modes. Every value is
+    checked exactly; a malformed program is refused with HCCL_E_PARA."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_self_loop_worker, args=(str(tmp_path / "ri"), q))
+    p.start()
+    try:
+        status, results, rejected = q.get(timeout=300)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert status == "ok", results
+    assert all(r[3] for r in results), results
+    assert rejected
