@@ -195,3 +195,105 @@ def test_rccl_transport_and_executor_self_loop(tmp_path):
     assert status == "ok", results
     assert all(r[3] for r in results), results
     assert rejected
+
+
+def self_looped(op_type, algo, n, rank, count, dtype):
+    """Rank `rank`'s program of an n-rank schedule with every peer mapped to this one rank, each transport group's
+    receives reordered so the k-th receive has the k-th send's size (RCCL pairs same-peer messages in posting order,
+    as the oracle's FIFOs do). The data no longer means the collective, but the program keeps the schedule's shape:
+    its groups, pieces, staging slots, batched folds and waits. Returns None when a group's send and receive sizes
+    differ as multisets (no pairing exists)."""
+    import hccl_amd as H
+    ops, nops, _, scratch = H.build_schedule(op_type, algo, n, rank, count, dtype)
+    out, i = [], 0
+    while i < nops:
+        o = ops[i]
+        if o.kind not in (H.IrKind.SEND, H.IrKind.RECV):
+            out.append(o)
+            i += 1
+            continue
+        g, sends, recvs = o.group, [], []
+        while i < nops and ops[i].kind in (H.IrKind.SEND, H.IrKind.RECV) and ops[i].group == g:
+            (sends if ops[i].kind == H.IrKind.SEND else recvs).append(ops[i])
+            i += 1
+        if sorted(s.count for s in sends) != sorted(r.count for r in recvs):
+            return None
+        for s in sends:
+            r = next(x for x in recvs if x.count == s.count)
+            recvs.remove(r)
+            s.peer = r.peer = 0
+            out += [s, r]
+    return (H.HcclAmdIrOp * len(out))(*out), len(out), scratch
+
+
+# (op, algo, n, rank, count): the C3/C4/C5 families at 8 ranks and a 5-rank ring. The ring and RHD counts split evenly
+# over their 7 (4) concurrent rings or instances and n aligned chunks, so every group's messages pair up; Reduce is left
+# out (its gather has receives on the root and sends elsewhere, which no self loop pairs).
+SELF_LOOP_CASES = [
+    (0, 3, 8, 0, 7 * 8 * 64 * 512), (0, 3, 8, 5, 7 * 8 * 64 * 512), (0, 3, 5, 2, 4 * 5 * 64 * 1024),
+    (0, 8, 8, 3, (40 << 20) // 4), (0, 2, 8, 6, (16 << 20) // 4), (0, 4, 8, 1, 7 * 8 * 64 * 512),
+    (0, 5, 8, 7, (4 << 20) // 4), (0, 1, 8, 2, (1 << 20) // 4), (0, 6, 8, 4, (4 << 20) // 4),
+    (1, 8, 8, 1, (4 << 20) // 4), (1, 3, 8, 6, 7 * 64 * 512), (3, 1, 8, 3, 1 << 18)]
+
+
+def _schedule_loop_worker(q):
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        import torch
+        import hccl_amd as H
+        from oracle import oracle as O
+        from tests._util import to_device, to_host
+        torch.cuda.set_device(0)
+        comm = H.comm_init_root_info(1, H.get_root_info(), 0)
+        s = torch.cuda.Stream()
+        results = []
+        for k, (op_type, algo, n, rank, count) in enumerate(SELF_LOOP_CASES):
+            for dtype, op in ((O.FP32, O.SUM), (O.BFP16, O.MAX)):
+                prog = self_looped(op_type, algo, n, rank, count, dtype)
+                if prog is None:
+                    results.append((k, dtype, "unpaired"))
+                    continue
+                arr, nops, scratch = prog
+                in_len = count * n if op_type == 1 else count
+                out_len = count * n if op_type == 3 else count
+                x = O.random_operands(dtype, in_len, seed=4000 + k, edge=False)
+                st = O.NP_STORAGE[dtype]
+                bufs = [[x.copy(), np.zeros(out_len, st), np.zeros(max(scratch, 1), st)]]
+                rc = O.replay(1, dtype, op, [(arr, nops)], bufs)
+                if rc != 0:
+                    results.append((k, dtype, f"oracle {rc}"))
+                    continue
+                for single in (False, True):
+                    xd = to_device(dtype, x)
+                    od = to_device(dtype, np.zeros(out_len, st))
+                    torch.cuda.synchronize()
+                    comm.execute(arr, nops, xd, od, op, single, s, dtype=dtype)
+                    torch.cuda.synchronize()
+                    same = O.equal_bits(dtype, to_host(dtype, od), bufs[0][1])
+                    results.append((k, dtype, "ok" if same else f"mismatch single={single}"))
+        comm.destroy()
+        q.put(("ok", results))
+    except Exception as e:  # noqa: BLE001
+        q.put(("err", f"{type(e).__name__}: {e}\n{traceback.format_exc()}"))
+
+
+def test_rccl_runs_the_schedules_over_a_self_loop():
+    """The real schedules' programs (ring with its 7 rings, MeshChunk, two-shot, RHD, NHR, one-shot, STRICT tree,
+    ReduceScatter, AllGather, Reduce) through RCCL send/recv groups and the executor on hardware: one rank's program
+    with its peers mapped onto a one-rank RCCL communicator, every output bit-exact against the oracle replaying the
+    same program, in both executor modes."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_schedule_loop_worker, args=(q,))
+    p.start()
+    try:
+        status, results = q.get(timeout=600)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert status == "ok", results
+    bad = [r for r in results if r[2] not in ("ok", "unpaired")]
+    assert not bad, bad
+    assert sum(r[2] == "ok" for r in results) >= 2 * len(SELF_LOOP_CASES), results
