@@ -67,6 +67,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("out_dir")
     ap.add_argument("--json")
+    ap.add_argument("--link", choices=["copy", "rccl"], default="copy",
+                    help="what counts as a link op: device copies and RCCL kernels (loopback world), or only RCCL "
+                         "kernels (a real transport, where copies are the schedule's own COPY records)")
+    ap.add_argument("--after", help="count only what starts after the last kernel whose name contains this (a marker "
+                                    "the traced program launches right before its timed region)")
     a = ap.parse_args()
     kt = glob.glob(os.path.join(a.out_dir, "**", "*kernel_trace.csv"), recursive=True)
     mt = glob.glob(os.path.join(a.out_dir, "**", "*memory_copy_trace.csv"), recursive=True)
@@ -74,11 +79,17 @@ def main():
     def kpick(name):
         if "k_reduce" in name:
             return "reduce"
-        if "copy" in name.lower():
+        if "nccl" in name.lower() or (a.link == "copy" and "copy" in name.lower()):
             return "link"
         return None
 
-    iv = _intervals(kt, kpick) + [("link", s, e) for _, s, e in _intervals(mt, lambda n: "memcpy")]
+    iv = _intervals(kt, kpick)
+    if a.link == "copy":
+        iv += [("link", s, e) for _, s, e in _intervals(mt, lambda n: "memcpy")]
+    if a.after:
+        marks = [s for _, s, _ in _intervals(kt, lambda n: "mark" if a.after in n else None)]
+        if marks:
+            iv = [x for x in iv if x[1] >= max(marks)]
     red = [(s, e) for c, s, e in iv if c == "reduce"]
     lnk = [(s, e) for c, s, e in iv if c == "link"]
     ur, ul = _union(red), _union(lnk)

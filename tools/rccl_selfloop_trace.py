@@ -1,0 +1,60 @@
+"""Reduce/transfer overlap of the executor with real RCCL kernels on one GPU (hardware side).
+
+One rank's program of an n-rank schedule, its peers mapped onto a one-rank RCCL communicator (tests/test_gpu_rccl.py
+self_looped), runs through HcclAmdCommExecute: the RCCL send/recv kernels of every group on the link stream and the
+folds on the reduce stream, with the waits the executor derives. Under `rocprofv3 --kernel-trace`,
+tools/overlap_summary.py then reports how much fold time runs while an RCCL kernel is in flight and how busy the GPU
+is over the span. The self-loop "links" are HBM copies, not xGMI, so the link/fold time ratio is not the 8-GPU one;
+what the trace shows is whether the two streams run concurrently on hardware.
+
+  rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rsl -o rsl -- python tools/rccl_selfloop_trace.py --algo ring
+  python tools/overlap_summary.py gpurun_out/rsl --link rccl --after FillFunctor --json profiles/r02_overlap_rccl_selfloop_ring.json
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--algo", default="ring")
+    ap.add_argument("--ranks", type=int, default=8)
+    ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--units", type=int, default=64, help="count = 7 * 8 * 64 * 512 * units fp32 elements")
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    import torch
+    import hccl_amd as H
+    from tests.test_gpu_rccl import self_looped
+
+    algo = H.Algo[a.algo.upper()]
+    count = 7 * 8 * 64 * 512 * a.units
+    prog = self_looped(H.OpType.ALLREDUCE, int(algo), a.ranks, a.rank, count, H.HcclDataType.FP32)
+    if prog is None:
+        raise SystemExit("this schedule's groups do not pair up over a self loop at this count")
+    arr, nops, _ = prog
+    torch.cuda.set_device(0)
+    comm = H.comm_init_root_info(1, H.get_root_info(), 0)
+    x = torch.rand(count, device="cuda")
+    out = torch.empty_like(x)
+    s = torch.cuda.Stream()
+    comm.execute(arr, nops, x, out, H.HcclReduceOp.SUM, False, s)  # warm-up: RCCL connections, staging
+    torch.cuda.synchronize()
+    torch.empty(1, device="cuda").fill_(7.0)  # trace marker (a FillFunctor kernel): overlap_summary.py --after Fill
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.iters):
+        comm.execute(arr, nops, x, out, H.HcclReduceOp.SUM, False, s)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.iters
+    comm.destroy()
+    print(json.dumps({"algo": algo.name, "ranks": a.ranks, "rank": a.rank, "bytes_per_rank": count * 4,
+                      "records": nops, "ms_per_program": round(dt * 1e3, 3)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
