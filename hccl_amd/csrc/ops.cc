@@ -430,6 +430,23 @@ HcclResult HcclAmdCommExecute(HcclComm comm, const HcclAmdIrOp* ops, uint64_t nu
     HCCL_CHK(CheckReduceDataType(dataType));
     HCCL_CHK(CheckReduceOp(dataType, op));
     const uint64_t es = DataTypeSize(dataType);
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->scratch == nullptr) {
+        // a one-rank communicator has no staging until a program asks for it
+        for (uint64_t i = 0; i < numOps; ++i) {
+            bool uses = ops[i].kind != HCCL_AMD_IR_SEND && ops[i].dstBuf == HCCL_AMD_BUF_SCRATCH;
+            for (int j = 0; j < ops[i].nsrc && j < HCCL_AMD_IR_MAX_SRC; ++j) {
+                uses = uses || ops[i].srcBuf[j] == HCCL_AMD_BUF_SCRATCH;
+            }
+            if (uses) {
+                HIP_CHK(hipSetDevice(c->device));
+                c->cclBytes = CclBytesDefault();
+                HIP_CHK(hipMalloc(&c->scratch, 2 * c->cclBytes));
+                c->scratchBytes = 2 * c->cclBytes;
+                break;
+            }
+        }
+    }
     // Every record must be well formed; staging references must lie inside the communicator's staging (the user
     // buffers' extents are the caller's contract, as for the collectives).
     auto bufOk = [&](int32_t b, uint64_t off, uint64_t cnt) {
@@ -452,7 +469,6 @@ HcclResult HcclAmdCommExecute(HcclComm comm, const HcclAmdIrOp* ops, uint64_t nu
             if (!bufOk(o.srcBuf[j], o.srcOff[j], o.count)) return HCCL_E_PARA;
         }
     }
-    std::lock_guard<std::mutex> lk(c->mu);
     HCCL_CHK(c->Gate());
     HIP_CHK(hipSetDevice(c->device));
     const std::vector<HcclAmdIrOp> prog(ops, ops + numOps);

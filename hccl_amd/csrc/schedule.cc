@@ -599,7 +599,8 @@ void AllReduceRing(const ScheduleParams& p, Builder& b)
 // Recursive halving (reduce-scatter) then recursive doubling (all-gather), power-of-two n = 2^m
 // (docs/zh/user_guide/coll_algo_intro/RHD.md). One RHD instance uses one link per step (partner = rank ^ d), 3 of an
 // 8-GPU node's 7. The ranks of a power-of-two world are the vectors of GF(2)^m and the 7 XOR matchings r <-> r ^ v
-// (v != 0) partition its links, so the schedule runs n-1 instances at once, one per part of the buffer: instance j
+// (v != 0) partition its links, so the schedule runs up to n-1 instances at once (RhdInstances: fewer for small
+// calls), one per part of the buffer: instance j
 // relabels ranks by the linear map whose step-s partner vector is alpha^(s+j) in GF(2^m) (alpha primitive). At every
 // step the instances' vectors alpha^(s+j), j = 0..n-2, are all the nonzero vectors: every link carries exactly one.
 // Inside instance j the classic RHD runs on virtual ranks: region = virtual chunk range [lo, hi); at virtual distance
@@ -653,11 +654,26 @@ std::vector<std::vector<uint32_t>> RhdTable(uint32_t n)
 
 namespace {
 
+// How many of the n-1 instances a call of `bytes` per rank runs. Every instance adds one message per rank and step
+// (6 steps at n = 8), and on the executor each message costs host time whatever its size: about 10 us per transport
+// group plus 1 us per message (RCCL self-loop programs, profiles/r02_rccl_selfloop_latency.jsonl). What an instance
+// buys is link bandwidth: R instances spread 2 (n-1)/n x bytes over R links at 76.8 GB/s each. With 12 us per extra
+// instance against 22.8 us per MiB / R of transfer, the best R is about sqrt(2 x bytes / 1 MiB): one instance up to
+// 1 MiB (C5's latency range), all seven from 24.5 MiB. Ranks agree: it depends on the call's arguments only.
+uint32_t RhdInstances(uint32_t n, uint64_t bytes)
+{
+    const uint32_t most = n > 1 ? n - 1 : 1;
+    uint32_t r = 1;
+    while (r < most && uint64_t(r + 1) * (r + 1) * (1ull << 20) <= 2 * bytes) ++r;
+    return r;
+}
+
 void AllReduceRhd(const ScheduleParams& p, Builder& b)
 {
     const uint32_t n = p.nRanks, me = p.rank;
     const uint64_t alignElems = std::max<uint64_t>(1, kAlignBytes / p.elemSize);
-    const std::vector<std::vector<uint32_t>> table = RhdTable(n);
+    std::vector<std::vector<uint32_t>> table = RhdTable(n);
+    table.resize(std::min<size_t>(table.size(), RhdInstances(n, p.count * p.elemSize)));
     const uint32_t R = static_cast<uint32_t>(table.size());
     struct Inst {
         std::vector<uint32_t> real;

@@ -163,13 +163,21 @@ def rhd_virtual(dtype, op, xs, bounds):
     return out
 
 
+def rhd_instances(n, nbytes):
+    """Concurrent RHD instances for nbytes per rank: the largest R <= n-1 with R^2 MiB <= 2 x nbytes (at least 1)."""
+    r = 1
+    while r < max(1, n - 1) and (r + 1) ** 2 * (1 << 20) <= 2 * nbytes:
+        r += 1
+    return r
+
+
 def allreduce_rhd(dtype, op, xs):
-    """n-1 concurrent RHD instances (HcclAmdRhdTable): part j runs the classic RHD on virtual ranks, virtual rank v
-    being real rank table[j][v]."""
+    """rhd_instances concurrent RHD instances (the first rows of HcclAmdRhdTable): part j runs the classic RHD on
+    virtual ranks, virtual rank v being real rank table[j][v]."""
     import hccl_amd as H
     n = len(xs)
     es = xs[0].itemsize
-    table = H.rhd_table(n)
+    table = H.rhd_table(n)[:rhd_instances(n, xs[0].size * es)]
     out = np.empty_like(xs[0])
     for j, (pb, pe) in enumerate(chunk_bounds(xs[0].size, len(table), es)):
         if pe > pb:

@@ -235,12 +235,19 @@ def test_rhd_instances_cover_every_link_once_per_step(n):
     assert H.rhd_table(6) == [] and H.rhd_table(12) == []
 
 
-def test_rhd_uses_every_link_at_eight_ranks():
-    progs, used, _ = programs(AR, 4, 8, 1 << 16, O.FP32)
+@pytest.mark.parametrize("nbytes,links", [(1 << 10, 1), (1 << 20, 1), ((1 << 20) + 4, 1), (2 << 20, 2), (8 << 20, 4),
+                                          (18 << 20, 6), ((49 << 20) // 2, 7), (4 << 30, 7)])
+def test_rhd_instances_grow_with_size(nbytes, links):
+    """RHD runs one instance for latency-bound calls and spreads over more links as the call grows (R^2 MiB <= 2 x
+    bytes, at most n-1): the first group of every rank talks to exactly R peers."""
+    assert R.rhd_instances(8, nbytes) == links
+    progs, used, _ = programs(AR, 4, 8, nbytes // 4, O.FP32) if nbytes < (64 << 20) else (None, None, None)
+    if progs is None:
+        return
     assert used == R.ALGO_RHD
     for arr, nops in progs:
         g0 = [o for o in arr[:nops] if o.kind in (2, 3) and o.group == 0]
-        assert len({o.peer for o in g0 if o.kind == 2}) == 7 and len({o.peer for o in g0 if o.kind == 3}) == 7
+        assert len({o.peer for o in g0 if o.kind == 2}) == links and len({o.peer for o in g0 if o.kind == 3}) == links
 
 
 def test_rhd_non_power_of_two_falls_back_to_ring():

@@ -26,34 +26,41 @@ def main():
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--units", type=int, default=64, help="count = 7 * 8 * 64 * 512 * units fp32 elements")
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--count", type=int, default=0, help="elements (overrides --units)")
+    ap.add_argument("--dtype", default="FP32")
+    ap.add_argument("--single", action="store_true", help="the single-stream executor mode (payloads <= 1 MiB)")
     a = ap.parse_args()
     import torch
     import hccl_amd as H
     from tests.test_gpu_rccl import self_looped
 
     algo = H.Algo[a.algo.upper()]
-    count = 7 * 8 * 64 * 512 * a.units
-    prog = self_looped(H.OpType.ALLREDUCE, int(algo), a.ranks, a.rank, count, H.HcclDataType.FP32)
+    count = a.count or 7 * 8 * 64 * 512 * a.units
+    dt = H.HcclDataType[a.dtype.upper()]
+    prog = self_looped(H.OpType.ALLREDUCE, int(algo), a.ranks, a.rank, count, dt)
     if prog is None:
         raise SystemExit("this schedule's groups do not pair up over a self loop at this count")
     arr, nops, _ = prog
     torch.cuda.set_device(0)
     comm = H.comm_init_root_info(1, H.get_root_info(), 0)
-    x = torch.rand(count, device="cuda")
+    tdt = {"FP32": torch.float32, "FP16": torch.float16, "BFP16": torch.bfloat16}[a.dtype.upper()]
+    x = torch.rand(count, device="cuda").to(tdt)
     out = torch.empty_like(x)
     s = torch.cuda.Stream()
-    comm.execute(arr, nops, x, out, H.HcclReduceOp.SUM, False, s)  # warm-up: RCCL connections, staging
+    comm.execute(arr, nops, x, out, H.HcclReduceOp.SUM, a.single, s)  # warm-up: RCCL connections, staging
     torch.cuda.synchronize()
     torch.empty(1, device="cuda").fill_(7.0)  # trace marker (a FillFunctor kernel): overlap_summary.py --after Fill
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.iters):
-        comm.execute(arr, nops, x, out, H.HcclReduceOp.SUM, False, s)
+        comm.execute(arr, nops, x, out, H.HcclReduceOp.SUM, a.single, s)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.iters
     comm.destroy()
-    print(json.dumps({"algo": algo.name, "ranks": a.ranks, "rank": a.rank, "bytes_per_rank": count * 4,
-                      "records": nops, "ms_per_program": round(dt * 1e3, 3)}), flush=True)
+    groups = len({arr[i].group for i in range(nops) if arr[i].kind in (H.IrKind.SEND, H.IrKind.RECV)})
+    print(json.dumps({"algo": algo.name, "ranks": a.ranks, "rank": a.rank, "dtype": a.dtype.upper(),
+                      "bytes_per_rank": count * x.element_size(), "records": nops, "groups": groups,
+                      "single_stream": a.single, "us_per_program": round(dt * 1e6, 1)}), flush=True)
 
 
 if __name__ == "__main__":
