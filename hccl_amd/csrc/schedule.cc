@@ -523,10 +523,20 @@ struct RingView {
     uint32_t Prev() const { return At(int64_t(pos) - 1); }
 };
 
-std::vector<RingView> Rings(uint32_t n, uint32_t me)
+// How many of the rings a call uses. Every ring adds two messages per rank and step, about 1 us of host time each on
+// the executor (profiles/r02_rccl_selfloop_latency*.jsonl), and spreads the transfer over one more link (1 MiB takes
+// 13.65 us at 76.8 GB/s). The AllReduce (2(n-1) steps, 2(n-1)/n x bytes moved), the ReduceScatter and the AllGather
+// ((n-1) steps, (n-1)/n x the input / output bytes) all balance at R^2 = 13.65 x MiB / (2n): the largest R with
+// R^2 x 2n x 1 MiB <= 13.65 x bytes, at least 1 (one ring up to ~1.2 MiB at n = 8, all seven from ~57 MiB). `bytes` is
+// the AllReduce buffer, the ReduceScatter input or the AllGather output of one rank.
+std::vector<RingView> Rings(uint32_t n, uint32_t me, uint64_t bytes)
 {
+    std::vector<std::vector<uint32_t>> table = RingTable(n);
+    size_t r = 1;
+    while (r < table.size() && double(r + 1) * double(r + 1) * 2.0 * n * double(1u << 20) <= 13.65 * double(bytes)) ++r;
+    table.resize(std::min(table.size(), r));
     std::vector<RingView> v;
-    for (auto& c : RingTable(n)) {
+    for (auto& c : table) {
         RingView r{c, 0};
         for (uint32_t i = 0; i < n; ++i) {
             if (c[i] == me) r.pos = i;
@@ -546,7 +556,7 @@ void AllReduceRing(const ScheduleParams& p, Builder& b)
 {
     const uint32_t n = p.nRanks, me = p.rank;
     const uint64_t alignElems = std::max<uint64_t>(1, kAlignBytes / p.elemSize);
-    const std::vector<RingView> rings = Rings(n, me);
+    const std::vector<RingView> rings = Rings(n, me, p.count * p.elemSize);
     const uint32_t R = static_cast<uint32_t>(rings.size());
     const uint64_t kSlots = 4;
     const Span part0 = RingPart(p.count, R, 0, alignElems);
@@ -1044,7 +1054,7 @@ void ReduceScatterRing(const ScheduleParams& p, Builder& b)
     const uint32_t n = p.nRanks, me = p.rank;
     const uint64_t rc = p.count;
     const uint64_t alignElems = std::max<uint64_t>(1, kAlignBytes / p.elemSize);
-    const std::vector<RingView> rings = Rings(n, me);
+    const std::vector<RingView> rings = Rings(n, me, rc * n * p.elemSize);
     const uint32_t R = static_cast<uint32_t>(rings.size());
     const uint64_t kRound = 4;
     const uint64_t maxPart = RingPart(rc, R, 0, alignElems).len;
@@ -1242,7 +1252,7 @@ void AllGatherRing(const ScheduleParams& p, Builder& b)
     const uint32_t n = p.nRanks, me = p.rank;
     const uint64_t sc = p.count;
     const uint64_t alignElems = std::max<uint64_t>(1, kAlignBytes / p.elemSize);
-    const std::vector<RingView> rings = Rings(n, me);
+    const std::vector<RingView> rings = Rings(n, me, sc * n * p.elemSize);
     const uint32_t R = static_cast<uint32_t>(rings.size());
     const uint64_t maxPart = RingPart(sc, R, 0, alignElems).len;
     const uint64_t pe = PieceElems(p, maxPart, 0);

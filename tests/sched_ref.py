@@ -106,6 +106,16 @@ def ring_table(n):
     return H.ring_table(n)
 
 
+def ring_count(n, nbytes):
+    """Rings a call uses: the largest R (at most the table's) with R^2 x 2n x 1 MiB <= 13.65 x nbytes, at least 1;
+    nbytes = the AllReduce buffer, the ReduceScatter input or the AllGather output of one rank."""
+    most = len(ring_table(n))
+    r = 1
+    while r < most and (r + 1) ** 2 * 2.0 * n * (1 << 20) <= 13.65 * nbytes:
+        r += 1
+    return r
+
+
 def ring_parts(count, n_rings, es):
     """Part k of the buffer travels around ring k (ceil split, 128-B aligned, as chunk_bounds)."""
     return chunk_bounds(count, n_rings, es)
@@ -123,7 +133,7 @@ def ring_chunk(dtype, op, xs, cyc, c, sl):
 def allreduce_ring(dtype, op, xs):
     n = len(xs)
     es = xs[0].itemsize
-    rings = ring_table(n)
+    rings = ring_table(n)[:ring_count(n, xs[0].size * es)]
     out = np.empty_like(xs[0])
     for k, (pb, pe) in enumerate(ring_parts(xs[0].size, len(rings), es)):
         for c, (b, e) in enumerate(chunk_bounds(pe - pb, n, es)):
@@ -298,7 +308,7 @@ def reduce_scatter_ring(dtype, op, xs, rc):
     .. x_{cyc[v+n]} = its own block, the travelling partial being src."""
     n = len(xs)
     es = xs[0].itemsize
-    rings = ring_table(n)
+    rings = ring_table(n)[:ring_count(n, rc * n * es)]
     outs = [np.empty(rc, xs[0].dtype) for _ in range(n)]
     for k, (pb, pe) in enumerate(ring_parts(rc, len(rings), es)):
         if pe <= pb:

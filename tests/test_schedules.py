@@ -205,15 +205,24 @@ def test_ring_table_is_arc_disjoint_hamiltonian(n):
         assert len(rings) == sum(1 for k in range(1, n) if math.gcd(k, n) == 1)
 
 
-def test_ring_uses_every_link_at_eight_ranks():
-    """At n = 8 every rank sends to and receives from all 7 peers in every ring step (one ring per link)."""
-    progs, used, _ = programs(AR, 3, 8, 1 << 16, O.FP32)
+@pytest.mark.parametrize("op_type,nbytes,links", [(AR, 64 << 20, 7), (AR, 1 << 20, 1), (AR, 3 << 20, 1),
+                                                  (AR, 8 << 20, 2), (AR, 16 << 20, 3), (AR, 40 << 20, 5),
+                                                  (RS, 64 << 20, 7), (RS, 1 << 20, 1), (AG, 64 << 20, 7),
+                                                  (AG, 2 << 20, 1)])
+def test_ring_count_grows_with_size(op_type, nbytes, links):
+    """Rings spread over more links as the call grows (R^2 x 2n MiB <= 13.65 x bytes of the AllReduce buffer /
+    ReduceScatter input / AllGather output), up to one ring per link at n = 8: then every rank sends to and receives
+    from all 7 peers in every step."""
+    assert R.ring_count(8, nbytes) == links
+    count = nbytes // 4 if op_type == AR else nbytes // 4 // 8
+    progs, used, _ = programs(op_type, 3, 8, count, O.FP32)
     assert used == R.ALGO_RING
     for arr, nops in progs:
-        first = [o for o in arr[:nops] if o.kind in (2, 3) and o.group == 0]
+        g = min(o.group for o in arr[:nops] if o.kind in (2, 3))
+        first = [o for o in arr[:nops] if o.kind in (2, 3) and o.group == g]
         assert sorted(o.peer for o in first if o.kind == 2) == sorted(set(o.peer for o in first if o.kind == 2))
-        assert len({o.peer for o in first if o.kind == 2}) == 7
-        assert len({o.peer for o in first if o.kind == 3}) == 7
+        assert len({o.peer for o in first if o.kind == 2}) == links
+        assert len({o.peer for o in first if o.kind == 3}) == links
 
 
 @pytest.mark.parametrize("n", [1, 2, 4, 8, 16])
