@@ -19,7 +19,8 @@ namespace {
 constexpr int kInt64 = 5;
 constexpr int kSum = 0;
 
-int RunCase(int opType, int algo, uint32_t n, uint64_t count, uint64_t cclBytes, uint32_t root)
+int RunCase(int opType, int algo, uint32_t n, uint64_t count, uint64_t cclBytes, uint32_t root,
+            uint64_t pieceBytes = 4096)
 {
     std::vector<hccl_amd::Schedule> sch(n);
     for (uint32_t r = 0; r < n; ++r) {
@@ -32,7 +33,7 @@ int RunCase(int opType, int algo, uint32_t n, uint64_t count, uint64_t cclBytes,
         p.elemSize = 8;
         p.root = root;
         p.cclBytes = cclBytes;
-        p.pieceBytes = 4096;
+        p.pieceBytes = pieceBytes;
         if (hccl_amd::BuildSchedule(p, &sch[r]) != 0) return -1;  // combination not offered (e.g. RHD at n = 3)
     }
     const uint64_t inCount = opType == HCCL_AMD_OP_REDUCE_SCATTER ? count * n : count;
@@ -104,6 +105,33 @@ int main()
                 }
             }
         }
+    }
+    // The ring and RHD spread over more rings / instances as calls grow (RhdInstances, Rings): calls large enough for
+    // two and for all of them, ragged, with 1 MiB pieces.
+    struct Big {
+        int op, algo;
+        uint32_t n;
+        uint64_t count;
+    };
+    const Big bigs[] = {
+        {HCCL_AMD_OP_ALLREDUCE, HCCL_AMD_ALGO_RHD, 8, (2ull << 20) / 8 + 3},          // 2 instances
+        {HCCL_AMD_OP_ALLREDUCE, HCCL_AMD_ALGO_RHD, 8, (49ull << 19) / 8 + 5},         // 7 instances (24.5 MiB)
+        {HCCL_AMD_OP_ALLREDUCE, HCCL_AMD_ALGO_RHD, 4, (16ull << 20) / 8 + 1},         // 3 instances at n = 4
+        {HCCL_AMD_OP_ALLREDUCE, HCCL_AMD_ALGO_RING, 8, (8ull << 20) / 8 + 7},         // 2 rings
+        {HCCL_AMD_OP_ALLREDUCE, HCCL_AMD_ALGO_RING, 8, (58ull << 20) / 8 + 1},        // 7 rings
+        {HCCL_AMD_OP_REDUCE_SCATTER, HCCL_AMD_ALGO_RING, 8, (58ull << 20) / 64 + 3},  // 7 rings (input bytes)
+        {HCCL_AMD_OP_ALLGATHER, HCCL_AMD_ALGO_RING, 8, (58ull << 20) / 64 + 1},       // 7 rings (output bytes)
+        {HCCL_AMD_OP_ALLREDUCE, HCCL_AMD_ALGO_RING, 5, (40ull << 20) / 8 + 3},        // 4 rings at n = 5
+    };
+    for (const Big& b : bigs) {
+        const int rc = RunCase(b.op, b.algo, b.n, b.count, 200ull << 20, b.n / 2, 1ull << 20);
+        if (rc < 0) {
+            std::printf("NOT BUILT op %d algo %d n %u\n", b.op, b.algo, b.n);
+            ++failures;
+            continue;
+        }
+        ++cases;
+        failures += rc;
     }
     std::printf("cases %d failures %d\n", cases, failures);
     return failures == 0 && cases > 0 ? 0 : 1;
