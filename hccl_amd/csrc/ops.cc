@@ -248,7 +248,11 @@ HcclResult HcclReduceScatterV(void* sendBuf, const void* sendCounts, const void*
     HCCL_CHK(CheckCount(recvCount));
     HCCL_CHK(CheckReduceDataType(dataType));
     HCCL_CHK(CheckReduceOp(dataType, op));
-    for (uint32_t q = 0; q < c->nRanks; ++q) HCCL_CHK(CheckCount(counts[q]));
+    for (uint32_t q = 0; q < c->nRanks; ++q) {
+        HCCL_CHK(CheckCount(counts[q]));
+        // a block whose end does not fit in 64 bits would wrap the schedule's offsets onto other memory
+        if (displs[q] > UINT64_MAX / 16 - counts[q]) return HCCL_E_PARA;
+    }
     // The template writes sendCounts[rank] elements to recvBuf (PostCopy, ins_temp_reduce_scatter_v_mesh_1D.cc:
     // 107-146); a smaller recvCount would overrun it, so it is refused here (the reference has no such check).
     if (counts[c->rank] > recvCount) return HCCL_E_PARA;
@@ -543,6 +547,9 @@ HcclResult HcclAmdBuildScheduleV(uint32_t nRanks, uint32_t rank, const uint64_t*
     const uint32_t es = DataTypeSize(dataType);
     if (es == 0) return HCCL_E_NOT_SUPPORT;
     if (nRanks == 0 || rank >= nRanks) return HCCL_E_PARA;
+    for (uint32_t q = 0; q < nRanks; ++q) {
+        if (sendCounts[q] > UINT64_MAX / 16 || sendDispls[q] > UINT64_MAX / 16 - sendCounts[q]) return HCCL_E_PARA;
+    }
     ScheduleParams p;
     p.opType = HCCL_AMD_OP_REDUCE_SCATTER_V;
     p.nRanks = nRanks;

@@ -91,3 +91,14 @@ def test_reduce_scatter_v_entry_checks():
     assert f(x, c, d, None, 1, O.FP32, O.SUM, x, x) == H.HcclResult.HCCL_E_PTR       # recvBuf with recvCount > 0
     fake = ctypes.create_string_buffer(64)  # readable memory whose magic is not a communicator's
     assert f(x, c, d, x, 1, O.FP32, O.SUM, ctypes.addressof(fake), x) == H.HcclResult.HCCL_E_PARA
+
+
+def test_reduce_scatter_v_rejects_wrapping_blocks():
+    """A block whose end does not fit in 64-bit byte offsets would wrap the schedule onto other memory: refused with
+    HCCL_E_PARA before any schedule is built."""
+    counts = (ctypes.c_uint64 * 2)(8, 8)
+    for displs in ((0, (1 << 64) - 4), (0, (1 << 62))):
+        d = (ctypes.c_uint64 * 2)(*displs)
+        n_ops = ctypes.c_uint64(0)
+        assert H.lib.HcclAmdBuildScheduleV(2, 0, counts, d, O.FP32, 0, None, 0, ctypes.byref(n_ops),
+                                           None) == H.HcclResult.HCCL_E_PARA
