@@ -390,3 +390,23 @@ def test_c1_sim_two_rank_1mib_allreduce():
     for r in range(2):
         assert O.equal_bits(O.FP32, outs[r], want[r])
     assert dt < 30
+
+
+@pytest.mark.parametrize("op_type,algo,n,nbytes", [
+    (AR, 4, 8, (2 << 20) + 12),        # RHD, 2 instances
+    (AR, 4, 8, (49 << 19) + 20),       # RHD, 7 instances
+    (AR, 4, 4, (16 << 20) + 4),        # RHD, 3 instances at n = 4
+    (AR, 3, 8, (8 << 20) + 28),        # ring, 2 rings
+    (AR, 3, 8, (58 << 20) + 4),        # ring, 7 rings
+    (AR, 3, 5, (40 << 20) + 12),       # ring, 4 rings at n = 5
+    (RS, 3, 8, (58 << 20) + 8 * 12),   # ReduceScatter ring, 7 rings (input bytes)
+])
+def test_wide_rings_and_rhd_match_closed_form(op_type, algo, n, nbytes):
+    """The ring and RHD at the sizes where they spread over several rings / instances (ragged counts, 1 MiB pieces):
+    every output bit equals the closed form of sched_ref, which takes the same number of rings / instances."""
+    count = nbytes // 4 if op_type == AR else nbytes // 4 // n
+    used, xs, outs = run(op_type, algo, n, count, O.FP32, O.SUM, piece_bytes=1 << 20, seed=n + algo)
+    assert used == algo
+    want = R.expected(op_type, used, O.FP32, O.SUM, xs, count)
+    for r in range(n):
+        assert O.equal_bits(O.FP32, outs[r], want[r]), (op_type, algo, n, r)
