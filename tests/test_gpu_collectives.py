@@ -542,6 +542,21 @@ def test_reduce_scatter_v(worlds, monkeypatch, n, layout, dtype, op, streams):
         assert O.equal_bits(dtype, got, want[r]), (r, counts[r])
 
 
+@pytest.mark.parametrize("algo,nbytes", [(3, (8 << 20) + 28), (3, (58 << 20) + 4), (4, (2 << 20) + 12),
+                                         (4, (49 << 19) + 20)])
+def test_wide_rings_and_rhd(worlds, algo, nbytes):
+    """Ring and RHD on 8 ranks at the sizes where they run several rings / instances at once (2 and 7 rings; 2 and 7
+    RHD instances), random fp32: bit-exact against the closed forms of tests/sched_ref.py."""
+    n, count = 8, nbytes // 4
+    comms = worlds(n)
+    xs = [np.random.default_rng(5000 + r).uniform(-1, 1, count).astype(np.float32) for r in range(n)]
+    used, outs = collective(comms, AR, algo, O.FP32, O.SUM, xs, count)
+    assert used == algo
+    want = R.expected(AR, used, O.FP32, O.SUM, xs, count)
+    for r in range(n):
+        assert O.equal_bits(O.FP32, outs[r], want[r]), r
+
+
 @pytest.mark.parametrize("algo", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_allreduce_inplace(worlds, algo):
     n, count = 4, 300007
