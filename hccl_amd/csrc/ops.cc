@@ -8,6 +8,8 @@
 // then build this rank's schedule (schedule.cc) and run it (executor.cc).
 #include <strings.h>
 
+#include <algorithm>
+
 #include <cstring>
 
 #include "comm.h"
@@ -61,6 +63,17 @@ bool IsSpecialForSelector(HcclDataType dt, HcclReduceOp op)
 {
     return dt == HCCL_DATA_TYPE_INT64 || dt == HCCL_DATA_TYPE_UINT64 || dt == HCCL_DATA_TYPE_FP64 ||
            op == HCCL_REDUCE_PROD;
+}
+
+// Pipelining granule of a call: the communicator's (HcclAmdCommSetPieceBytes) if set. Otherwise the schedule's default
+// for the two-stream executor, and one piece per slice (as far as the staging holds) for the single-stream one, where
+// pieces cannot overlap anything and each costs a transport group (about 10 us of host time per group, RCCL self-loop
+// programs: profiles/r02_rccl_selfloop_latency*.jsonl). Pieces never change a fold order: every order is fixed per
+// executor loop and slice, and a piece only splits a slice's elements.
+uint64_t PieceBytesFor(const Comm& c, bool singleStream, uint64_t payload)
+{
+    if (c.pieceBytes != 0) return c.pieceBytes;
+    return singleStream ? std::max<uint64_t>(payload, 128) : 0;  // no slice is larger than the payload
 }
 
 HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, uint64_t count, HcclDataType dt,
@@ -131,13 +144,13 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     p.count = count;
     p.elemSize = es;
     p.root = root;
-    p.pieceBytes = c.pieceBytes;
     p.scratchCapBytes = c.scratchBytes;
     p.cclBytes = c.cclBytes;
     p.special = IsSpecialForSelector(dt, op);
     void* bufs[3] = {sendBuf, recvBuf, c.scratch};
     const uint64_t payload = count * es * (opType == HCCL_AMD_OP_REDUCE_SCATTER ? c.nRanks : 1);
     const bool single = payload <= SingleStreamBytes();
+    p.pieceBytes = PieceBytesFor(c, single, payload);
     const CompiledSchedule* cs = nullptr;
     HCCL_CHK(CompileCollective(c, p, bufs, !single, &cs));
     const Schedule& s = cs->sched;
@@ -174,13 +187,13 @@ HcclResult RunReduceScatterV(Comm& c, void* sendBuf, const uint64_t* counts, con
     p.displs.assign(displs, displs + c.nRanks);
     p.count = counts[c.rank];
     p.elemSize = es;
-    p.pieceBytes = c.pieceBytes;
     p.scratchCapBytes = c.scratchBytes;
     p.cclBytes = c.cclBytes;
     void* bufs[3] = {sendBuf, recvBuf, c.scratch};
     uint64_t payload = 0;
     for (uint32_t q = 0; q < c.nRanks; ++q) payload += counts[q] * es;
     const bool single = c.nRanks == 1 || payload <= SingleStreamBytes();
+    p.pieceBytes = PieceBytesFor(c, single, payload);
     const CompiledSchedule* cs = nullptr;
     HCCL_CHK(CompileCollective(c, p, bufs, !single, &cs));
     const Schedule& s = cs->sched;

@@ -197,14 +197,14 @@ def test_rccl_transport_and_executor_self_loop(tmp_path):
     assert rejected
 
 
-def self_looped(op_type, algo, n, rank, count, dtype):
+def self_looped(op_type, algo, n, rank, count, dtype, piece_bytes=0):
     """Rank `rank`'s program of an n-rank schedule with every peer mapped to this one rank, each transport group's
     receives reordered so the k-th receive has the k-th send's size (RCCL pairs same-peer messages in posting order,
     as the oracle's FIFOs do). The data no longer means the collective, but the program keeps the schedule's shape:
     its groups, pieces, staging slots, batched folds and waits. Returns None when a group's send and receive sizes
     differ as multisets (no pairing exists)."""
     import hccl_amd as H
-    ops, nops, _, scratch = H.build_schedule(op_type, algo, n, rank, count, dtype)
+    ops, nops, _, scratch = H.build_schedule(op_type, algo, n, rank, count, dtype, 0, piece_bytes)
     out, i = [], 0
     while i < nops:
         o = ops[i]

@@ -11,5 +11,6 @@ run --algo mesh_twoshot --count 512 --dtype FP16 --single --iters 2000
 run --algo nhr --count 512 --dtype FP16 --single --iters 2000
 run --algo rhd --count 3584 --dtype FP16 --single --iters 2000
 run --algo mesh_oneshot --count 524288 --dtype FP16 --single --iters 1000
+run --algo mesh_oneshot --count 524288 --dtype FP16 --single --iters 1000 --piece-bytes 0
 run --algo rhd --count 458752 --dtype FP16 --single --iters 1000
 cat "$out"

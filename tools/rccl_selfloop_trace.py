@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--count", type=int, default=0, help="elements (overrides --units)")
     ap.add_argument("--dtype", default="FP32")
     ap.add_argument("--single", action="store_true", help="the single-stream executor mode (payloads <= 1 MiB)")
+    ap.add_argument("--piece-bytes", type=int, default=-1,
+                    help="pipelining granule; default: what a collective call uses (the payload when --single)")
     a = ap.parse_args()
     import torch
     import hccl_amd as H
@@ -37,7 +39,9 @@ def main():
     algo = H.Algo[a.algo.upper()]
     count = a.count or 7 * 8 * 64 * 512 * a.units
     dt = H.HcclDataType[a.dtype.upper()]
-    prog = self_looped(H.OpType.ALLREDUCE, int(algo), a.ranks, a.rank, count, dt)
+    es = H.lib.HcclAmdDataTypeSize(int(dt))
+    piece = a.piece_bytes if a.piece_bytes >= 0 else (max(count * es, 128) if a.single else 0)
+    prog = self_looped(H.OpType.ALLREDUCE, int(algo), a.ranks, a.rank, count, dt, piece)
     if prog is None:
         raise SystemExit("this schedule's groups do not pair up over a self loop at this count")
     arr, nops, _ = prog
@@ -60,7 +64,8 @@ def main():
     groups = len({arr[i].group for i in range(nops) if arr[i].kind in (H.IrKind.SEND, H.IrKind.RECV)})
     print(json.dumps({"algo": algo.name, "ranks": a.ranks, "rank": a.rank, "dtype": a.dtype.upper(),
                       "bytes_per_rank": count * x.element_size(), "records": nops, "groups": groups,
-                      "single_stream": a.single, "us_per_program": round(dt * 1e6, 1)}), flush=True)
+                      "single_stream": a.single, "piece_bytes": piece, "us_per_program": round(dt * 1e6, 1)}),
+          flush=True)
 
 
 if __name__ == "__main__":
