@@ -630,6 +630,18 @@ def bench_c3_algos(comm, send, recv, world) -> dict:
     return out
 
 
+def _transport_info() -> dict:
+    """What the N > 1 numbers were taken with: the RCCL build torch carries (the process's librccl) and any NCCL_* /
+    RCCL_* / HCCL_* settings in the environment."""
+    try:
+        v = torch.cuda.nccl.version()
+        ver = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception as e:  # noqa: BLE001
+        ver = f"unknown ({type(e).__name__})"
+    env = {k: v for k, v in sorted(os.environ.items()) if k.startswith(("NCCL_", "RCCL_", "HCCL_"))}
+    return {"rccl_version": ver, "env": env}
+
+
 def bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     """Runs the N > 1 measurement on a dedicated stream: every HCCL call gets a real stream (the null default stream
     is rejected with HCCL_E_PTR, as the reference's entry check does) and every event is recorded on it."""
@@ -763,6 +775,7 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
         },
         "busbw_GBps": round(busbw, 2),
         "algbw_GBps": round(algbw, 2),
+        "transport": _transport_info(),
         "result_ok": result_ok,
         "result_ok_algorithm": verified_algo,
         "rccl_allreduce_reference": rccl_ref,
