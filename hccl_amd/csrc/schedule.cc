@@ -527,14 +527,17 @@ struct RingView {
 // the executor (profiles/r02_rccl_selfloop_latency*.jsonl), and spreads the transfer over one more link (1 MiB takes
 // 13.65 us at 76.8 GB/s). The AllReduce (2(n-1) steps, 2(n-1)/n x bytes moved), the ReduceScatter and the AllGather
 // ((n-1) steps, (n-1)/n x the input / output bytes) all balance at R^2 = 13.65 x MiB / (2n): the largest R with
-// R^2 x 2n x 1 MiB <= 13.65 x bytes, at least 1 (one ring up to ~1.2 MiB at n = 8, all seven from ~57 MiB). `bytes` is
+// R^2 x 2n x 1 MiB <= 13.65 x bytes, at least 1 (one ring up to ~4.7 MiB at n = 8, all seven from ~57 MiB). `bytes` is
 // the AllReduce buffer, the ReduceScatter input or the AllGather output of one rank.
 std::vector<RingView> Rings(uint32_t n, uint32_t me, uint64_t bytes)
 {
     std::vector<std::vector<uint32_t>> table = RingTable(n);
-    size_t r = 1;
-    while (r < table.size() && double(r + 1) * double(r + 1) * 2.0 * n * double(1u << 20) <= 13.65 * double(bytes)) ++r;
-    table.resize(std::min(table.size(), r));
+    size_t rings = 1;
+    while (rings < table.size() &&
+           double(rings + 1) * double(rings + 1) * 2.0 * n * double(1u << 20) <= 13.65 * double(bytes)) {
+        ++rings;
+    }
+    table.resize(std::min(table.size(), rings));
     std::vector<RingView> v;
     for (auto& c : table) {
         RingView r{c, 0};
