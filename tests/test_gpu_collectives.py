@@ -365,6 +365,48 @@ def test_fp32_sum(worlds, op_type, algo, n, count, streams, monkeypatch):
         assert O.equal_bits(O.FP32, outs[r], want_cf[r]), ("vs closed form", r)
 
 
+def _random_cases(k):
+    rng = np.random.default_rng(20261016)
+    fams = {AR: [0, 1, 2, 3, 4, 5, 6, 8], RS: [0, 1, 3, 5, 6, 8], RED: [0, 1, 2, 5], AG: [0, 1, 3]}
+    dts = [O.INT8, O.INT16, O.INT32, O.INT64, O.UINT64, O.FP16, O.BFP16, O.FP32, O.FP64]
+    out = []
+    for i in range(k):
+        op_type = int(rng.choice([AR, RS, RED, AG]))
+        algo = int(rng.choice(fams[op_type]))
+        n = int(rng.choice([2, 3, 4, 5, 6, 8]))
+        dtype = int(rng.choice(dts))
+        op = int(rng.choice(O.OPS)) if op_type != AG else O.SUM
+        if op == O.PROD and dtype in (O.INT16, O.BFP16):  # PROD is refused on these (CheckReduceOp)
+            op = O.MAX
+        count = int(rng.choice([1, 3, 17, 1000, 4099, 65537, 300001]))
+        piece = int(rng.choice([0, 4096, 64 << 10]))
+        inplace = bool(rng.integers(2)) and op_type == AR
+        streams = str(rng.choice(["auto", "two"]))
+        out.append((i, op_type, algo, n, dtype, op, count, piece, inplace, streams))
+    return out
+
+
+@pytest.mark.parametrize("case", _random_cases(80), ids=lambda c: f"rand{c[0]}")
+def test_random_collectives_match_oracle(worlds, monkeypatch, case):
+    """Seeded random draws over operation x family x ranks x dtype x op x count x granule x in-place x executor mode
+    (combinations the fixed matrices do not pair up), each bit-exact against the oracle replaying the same IR."""
+    _, op_type, algo, n, dtype, op, count, piece, inplace, streams = case
+    if streams == "two":
+        monkeypatch.setenv("HCCL_AMD_SINGLE_STREAM_BYTES", "0")
+    comms = worlds(n)
+    root = (count + n) % n
+    in_count = count * n if op_type == RS else count
+    xs = [O.random_operands(dtype, in_count, seed=7000 + 13 * case[0] + r, edge=False) for r in range(n)]
+    used, outs = collective(comms, op_type, algo, dtype, op, xs, count, root=root, piece_bytes=piece, inplace=inplace)
+    want = oracle_replay(op_type, used, n, count, dtype, op, xs, root, piece)
+    for r in range(n):
+        if op_type == RED and r != root:
+            if not inplace:
+                assert not outs[r].any(), "non-root recvBuf written"
+            continue
+        assert O.equal_bits(dtype, outs[r], want[r]), (case, r)
+
+
 @pytest.mark.parametrize("dtype", [O.INT8, O.INT16, O.INT32, O.INT64, O.UINT64, O.FP16, O.BFP16, O.FP64],
                          ids=lambda v: O.DTYPE_NAMES[v])
 @pytest.mark.parametrize("op", O.OPS, ids=lambda v: O.OP_NAMES[v])
