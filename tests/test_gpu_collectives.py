@@ -386,7 +386,7 @@ def _random_cases(k):
     return out
 
 
-@pytest.mark.parametrize("case", _random_cases(80), ids=lambda c: f"rand{c[0]}")
+@pytest.mark.parametrize("case", _random_cases(240), ids=lambda c: f"rand{c[0]}")
 def test_random_collectives_match_oracle(worlds, monkeypatch, case):
     """Seeded random draws over operation x family x ranks x dtype x op x count x granule x in-place x executor mode
     (combinations the fixed matrices do not pair up), each bit-exact against the oracle replaying the same IR."""
