@@ -22,6 +22,7 @@ import json
 import os
 import platform
 import sys
+import threading
 import time
 
 import numpy as np
@@ -729,30 +730,6 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     comm.destroy()
     g = torch.Generator(device=dev).manual_seed(0x5EED0003 + rank)
     send.copy_(torch.rand(count, device=dev, generator=g).mul_(2).sub_(1))
-    extra = {}
-    if not args.no_extra_configs:
-        # Each secondary config gets a communicator of its own: a failure in one (say an IPC barrier timeout, after
-        # which the communicator answers HCCL_E_SUSPENDING) cannot take the others, or the headline, with it.
-        for name, fn in (("c3_schedules", lambda cm: bench_c3_algos(cm, send, recv, world)),
-                         ("c4", lambda cm: bench_c4(cm, send, recv, world)),
-                         ("c5", lambda cm: bench_c5(cm, send, recv, world)),
-                         ("end_to_end_host_buffers", lambda cm: bench_e2e_allreduce(cm, world))):
-            cm = None
-            try:
-                cm = new_comm()
-                extra[name] = fn(cm)
-            except Exception as e:  # noqa: BLE001  (a secondary config never hides the headline line)
-                extra[name] = {"error": f"{type(e).__name__}: {e}"}
-            finally:
-                if cm is not None:
-                    try:
-                        cm.destroy()
-                    except Exception as e:  # noqa: BLE001
-                        extra.setdefault(name, {})["destroy_error"] = f"{type(e).__name__}: {e}"
-    rccl_ref = None
-    if not args.no_rccl_ref:
-        rccl_ref = rccl_allreduce_reference(send, recv, world, args)
-    dist.destroy_process_group()
     res = {
         "metric": "device-resident reduce GiB/s (fp32 sum) vs HBM peak; ring all-reduce bus GB/s",
         "value": round(value, 2),
@@ -778,8 +755,8 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
         "transport": _transport_info(),
         "result_ok": result_ok,
         "result_ok_algorithm": verified_algo,
-        "rccl_allreduce_reference": rccl_ref,
-        "other_configs": extra,
+        "rccl_allreduce_reference": None,
+        "other_configs": {},
         "roofline": {
             "bound": "xgmi",
             "achieved": round(busbw, 2),
@@ -791,7 +768,80 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
                     "x 76.8 GB/s per direction (fully connected node: one link per peer)",
         },
     }
+    # Secondary configs and the RCCL reference run under a watchdog: a collective that never returns there (a first
+    # run of some schedule on real hardware) must not cost the headline line. At the deadline every rank stops, rank
+    # 0 printing the result with what finished so far.
+    extra = res["other_configs"]
+    wd = _Watchdog(float(os.environ.get("HCCL_AMD_BENCH_EXTRAS_DEADLINE_S", "300")), rank, res)
+    wd.start()
+    if not args.no_extra_configs:
+        # Each secondary config gets a communicator of its own: a failure in one (say an IPC barrier timeout, after
+        # which the communicator answers HCCL_E_SUSPENDING) cannot take the others, or the headline, with it.
+        for name, fn in (("c3_schedules", lambda cm: bench_c3_algos(cm, send, recv, world)),
+                         ("c4", lambda cm: bench_c4(cm, send, recv, world)),
+                         ("c5", lambda cm: bench_c5(cm, send, recv, world)),
+                         ("end_to_end_host_buffers", lambda cm: bench_e2e_allreduce(cm, world))):
+            wd.stage(name)
+            cm = None
+            try:
+                cm = new_comm()
+                extra[name] = fn(cm)
+            except Exception as e:  # noqa: BLE001  (a secondary config never hides the headline line)
+                extra[name] = {"error": f"{type(e).__name__}: {e}"}
+            finally:
+                if cm is not None:
+                    try:
+                        cm.destroy()
+                    except Exception as e:  # noqa: BLE001
+                        extra.setdefault(name, {})["destroy_error"] = f"{type(e).__name__}: {e}"
+    if not args.no_rccl_ref:
+        wd.stage("rccl_allreduce_reference")
+        res["rccl_allreduce_reference"] = rccl_allreduce_reference(send, recv, world, args)
+    wd.cancel()
+    dist.destroy_process_group()
     return res if rank == 0 else None
+
+
+_PRINTED = threading.Event()
+_PRINT_LOCK = threading.Lock()
+
+
+def emit(res: dict) -> None:
+    """Prints the one JSON line, once per process (the watchdog and the normal exit may race)."""
+    with _PRINT_LOCK:
+        if _PRINTED.is_set():
+            return
+        print(json.dumps(res), flush=True)
+        _PRINTED.set()
+
+
+class _Watchdog:
+    """Ends a rank whose secondary configs overrun `seconds`: rank 0 first prints the result (headline plus what
+    finished) with a note naming the stage that overran. Every rank arms it at the same point, so they stop together."""
+
+    def __init__(self, seconds: float, rank: int, res: dict):
+        self.seconds, self.rank, self.res, self.current = seconds, rank, res, "start"
+        self.t0 = time.perf_counter()
+        self.timer = threading.Timer(seconds, self._fire)
+        self.timer.daemon = True
+
+    def start(self):
+        self.timer.start()
+
+    def stage(self, name: str):
+        self.current = name
+
+    def cancel(self):
+        self.timer.cancel()
+
+    def _fire(self):
+        if self.rank == 0:
+            self.res["watchdog"] = {"stopped_at": self.current, "after_s": round(time.perf_counter() - self.t0, 1),
+                                    "deadline_s": self.seconds}
+            emit(self.res)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
 
 
 def main():
@@ -820,7 +870,7 @@ def main():
     else:
         res = bench_local(args)
     if res is not None:
-        print(json.dumps(res), flush=True)
+        emit(res)
 
 
 if __name__ == "__main__":
