@@ -631,6 +631,23 @@ def bench_c3_algos(comm, send, recv, world) -> dict:
     return out
 
 
+class _stdout_to_stderr:
+    """Points file descriptor 1 at stderr for the duration (native libraries that print on stdout: gloo's connection
+    report), so that stdout carries nothing but the result line."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
 def _transport_info() -> dict:
     """What the N > 1 numbers were taken with: the RCCL build torch carries (the process's librccl) and any NCCL_* /
     RCCL_* / HCCL_* settings in the environment."""
@@ -665,7 +682,8 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
         args.no_rccl_ref = True
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    with _stdout_to_stderr():  # gloo announces its connections on stdout, which carries only the JSON line
+        dist.init_process_group("gloo", rank=rank, world_size=world)
 
     def _all_gather(b):
         out = [None] * world
