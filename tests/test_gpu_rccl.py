@@ -163,13 +163,20 @@ def _self_loop_worker(ri_path, q):
             ok = torch.equal(acc, want_acc) and torch.equal(fin, want_fin) and \
                 torch.equal(out[(pieces - 2) % 2 * L:(pieces - 2) % 2 * L + L], x[(pieces - 2) * L:(pieces - 1) * L])
             results.append((n_el, pieces, single, ok))
-        bad = _ir(H.IrKind.SEND, 16, srcs=[(0, 0)], peer=1)  # peer outside the communicator
-        arr = (H.HcclAmdIrOp * 1)(bad)
-        try:
-            comm.execute(arr, 1, x, out, H.HcclReduceOp.SUM, False, s)
-            rejected = False
-        except H.HcclError as e:
-            rejected = e.code == H.HcclResult.HCCL_E_PARA
+        bads = [_ir(H.IrKind.SEND, 16, srcs=[(0, 0)], peer=1),                 # peer outside the communicator
+                _ir(H.IrKind.REDUCE, 16, dst=(1, 0)),                            # a fold without operands
+                _ir(H.IrKind.COPY, 16, dst=(2, (1 << 62)), srcs=[(0, 0)]),       # beyond the staging
+                _ir(H.IrKind.COPY, 16, dst=(7, 0), srcs=[(0, 0)])]               # no such buffer
+        bad_kind = _ir(H.IrKind.COPY, 16, dst=(1, 0), srcs=[(0, 0)])
+        bad_kind.kind = 9
+        rejected = True
+        for bad in bads + [bad_kind]:
+            arr = (H.HcclAmdIrOp * 1)(bad)
+            try:
+                comm.execute(arr, 1, x, out, H.HcclReduceOp.SUM, False, s)
+                rejected = False
+            except H.HcclError as e:
+                rejected = rejected and e.code == H.HcclResult.HCCL_E_PARA
         comm.destroy()
         q.put(("ok", results, rejected))
     except Exception as e:  # noqa: BLE001
