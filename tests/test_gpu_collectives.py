@@ -487,6 +487,27 @@ def test_aiv_engine_orders(worlds, monkeypatch, op_type, n, count, core_limit, d
         assert O.equal_bits(dtype, outs[r], want[r]), (r, variant)
 
 
+@pytest.mark.parametrize("n,count", [(8, (1 << 20) + 7), (4, (3 << 19) + 5), (3, 700001)])
+def test_aiv_two_shot_slices_follow_its_loops(monkeypatch, n, count):
+    """The AIV large-core two-shot slices every executor loop of min(UB_MAX_DATA_SIZE, ccl/4) into groupSize * n
+    balanced slices on its own, so the loop boundaries decide which rank's copy each element's fold starts from. With
+    HCCL_BUFFSIZE = 1 MB the loops are 256 KiB: many loops, every one sliced afresh, bit-exact with the closed form."""
+    monkeypatch.setenv("HCCL_BUFFSIZE", "1")
+    comms = H.loopback_world(n)
+    try:
+        xs = [O.random_operands(O.FP32, count, seed=1600 + r, edge=False) for r in range(n)]
+        variant, want = aiv_expected(AR, O.FP32, O.SUM, xs, count, n, 48)
+        assert variant == R.AIV_AR_TWOSHOT_LARGE
+        used, outs = collective(comms, AR, H.Algo.AIV, O.FP32, O.SUM, xs, count)
+        assert used == H.Algo.AIV
+        for r in range(n):
+            assert O.equal_bits(O.FP32, outs[r], want[r]), r
+    finally:
+        torch.cuda.synchronize()
+        for c in comms:
+            c.destroy()
+
+
 def test_aiv_expansion_mode_env_and_fallback(worlds, monkeypatch):
     """HCCL_OP_EXPANSION_MODE=AIV on an auto communicator takes the AIV engine; what SelectAivAlgo does not match
     (PROD, FP64, 64 MiB at 8 ranks) runs the AICPU selection, as the reference falls back."""
