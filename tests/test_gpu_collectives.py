@@ -465,7 +465,7 @@ def aiv_expected(op_type, dtype, op, xs, count, n, core_limit):
 AIV_CASES = [(AR, 2, 5001, 48), (AR, 8, 30000, 48), (AR, 4, (1 << 20) + 3, 48), (AR, 8, (1 << 20) + 7, 48),
              (AR, 8, 100003, 48), (AR, 3, 400001, 56), (AR, 8, 70001, 9), (AR, 4, 300007, 8),
              (RS, 4, 1001, 48), (RS, 8, 30001, 48), (RS, 2, (1 << 17) + 5, 48), (RS, 8, (1 << 17) + 1, 48),
-             (RS, 8, (1 << 17) + 1, 16), (RS, 3, 200003, 6)]
+             (RS, 8, (1 << 17) + 1, 16), (RS, 3, 200003, 6), (RS, 8, 30001, 4), (AR, 8, 70001, 4)]
 
 
 @pytest.mark.parametrize("dtype,op", [(O.FP32, O.SUM), (O.FP16, O.SUM), (O.BFP16, O.MAX), (O.INT8, O.SUM),
