@@ -11,8 +11,10 @@ stream it waits for) for one rank's IR at the C3 shape, and replays it on a two-
 A unit starts when the previous unit of its stream and the unit it waits for have ended (every rank runs the same
 plan, so one rank's timeline stands for all). Reported per schedule: link and reduce totals, makespan, the reduce time
 that runs while a link unit is in flight (reduce_hidden_frac) and the makespan against the lower bound
-max(link total, reduce total); then the makespan again with an assumed launch cost per unit (15 us per transport
-group, 5 us per fold launch), which prices how many units the schedule issues.
+max(link total, reduce total); then the makespan again with a launch cost per unit, which prices how many units the
+schedule issues: 10 us per transport group plus 1 us per message in it (measured on RCCL self-loop programs,
+profiles/r02_rccl_selfloop_latency*.jsonl) and 5 us per fold launch (assumed); and the AllReduce bus bandwidth that
+makespan implies (busbw = bytes / makespan x 2(n-1)/n).
 
   python tools/executor_overlap_model.py > profiles/r02_executor_overlap_model.jsonl
 """
@@ -25,13 +27,14 @@ import hccl_amd as H  # noqa: E402
 
 B_LINK = 76.8e9
 B_HBM = 6.0e12
-# launch cost per unit for the second timeline (assumed, not measured here: an RCCL grouped send/recv launch and a
-# fold kernel launch); it prices the number of units a schedule issues
-OVH_LINK = 15e-6
+# launch cost per unit for the second timeline: a transport group (measured: ~10 us plus ~1 us per message) and a fold
+# kernel launch (assumed); it prices the number of units a schedule issues
+OVH_LINK = 10e-6
+OVH_MSG = 1e-6
 OVH_REDUCE = 5e-6
 
 
-def simulate(ops, nops, es, units, ovh_link=0.0, ovh_reduce=0.0):
+def simulate(ops, nops, es, units, ovh_link=0.0, ovh_reduce=0.0, ovh_msg=0.0):
     end = {0: 0.0, 1: 0.0}
     done = []
     spans = []
@@ -42,7 +45,7 @@ def simulate(ops, nops, es, units, ovh_link=0.0, ovh_reduce=0.0):
             for o in recs:
                 key = (o.peer, o.kind)
                 per_peer[key] = per_peer.get(key, 0) + o.count * es
-            dur = max(per_peer.values()) / B_LINK + ovh_link
+            dur = max(per_peer.values()) / B_LINK + ovh_link + ovh_msg * len(recs)
         else:
             hbm = 0
             for o in recs:
@@ -77,7 +80,10 @@ def model(op_type, algo, n, count, dtype, rank=0):
     units = H.executor_plan(ops, nops, es)
     row = {"op": H.OpType(op_type).name, "algo": H.Algo(used).name, "ranks": n, "bytes_per_rank": count * es}
     row.update(simulate(ops, nops, es, units))
-    row["makespan_with_launch_cost_ms"] = simulate(ops, nops, es, units, OVH_LINK, OVH_REDUCE)["makespan_ms"]
+    with_cost = simulate(ops, nops, es, units, OVH_LINK, OVH_REDUCE, OVH_MSG)["makespan_ms"]
+    row["makespan_with_launch_cost_ms"] = with_cost
+    if op_type == H.OpType.ALLREDUCE and with_cost:
+        row["allreduce_busbw_GBps_with_launch_cost"] = round(count * es / (with_cost * 1e-3) * 2 * (n - 1) / n / 1e9, 1)
     return row
 
 
