@@ -237,21 +237,85 @@ __global__ __launch_bounds__(kBlock) void k_reduceN(typename E::S* out, SrcPack 
     ReduceNBody<E, OP, U, NT, MODE, NS>(out, srcs, nsrc, nvec, edges, blockIdx.x, gridDim.x);
 }
 
-// A batch of independent folds: segment blockIdx.y, worked by the gridDim.x workgroups of its row.
+// A batch of independent folds (one schedule step's), in one of two layouts chosen by segment size (RunBatch):
+// * flat (k_reduceN_batch): the segments' full tiles are one concatenated tile space that the whole grid strides over,
+//   as a single fold would; at any moment the workgroups sit in a window of consecutive tiles, one or two segments
+//   wide, so the DRAM sees a few operand streams instead of every segment's at once; each segment's leftover vectors
+//   and scalar edges follow, spread over the grid;
+// * rows (k_reduceN_batch_rows): a grid row per segment.
+// Measured (tools/batch_fold_bench.py, 7 segments; profiles/r02_batch_fold_layout_ab.txt): at 4 and 16 MiB segments
+// flat runs 6.1-6.5 TB/s against rows' 5.5-6.1 (2 and 8 operands); at 1-2 MiB rows is as fast or faster, and beside the
+// RCCL kernels of a self-loop MeshChunk program (1.8 MiB sub-slices) rows' folds took 0.95-1.0 ms against flat's 1.4.
+constexpr uint64_t kBatchFlatSegBytes = 4ull << 20;  // segments this large (on average) take the flat layout
+
 struct BatchPack {
     void* out[kMaxBatchSegs];
     SrcPack srcs[kMaxBatchSegs];
     uint64_t nvec[kMaxBatchSegs];
     Edges edges[kMaxBatchSegs];
+    uint64_t tileStart[kMaxBatchSegs + 1];  // prefix sums of the segments' full tiles
+    int nseg;
     int nsrc;
 };
 
+// The other layout: one grid row (blockIdx.y) per segment, each row striding over its own segment.
 template <class E, int OP, int U, int NT>
-__global__ __launch_bounds__(kBlock) void k_reduceN_batch(BatchPack pk)
+__global__ __launch_bounds__(kBlock) void k_reduceN_batch_rows(BatchPack pk)
 {
     const uint32_t g = blockIdx.y;
     ReduceNBody<E, OP, U, NT>(static_cast<typename E::S*>(pk.out[g]), pk.srcs[g], pk.nsrc, pk.nvec[g], pk.edges[g],
                               blockIdx.x, gridDim.x);
+}
+
+template <class E, int OP, int U, int NT>
+__global__ __launch_bounds__(kBlock) void k_reduceN_batch(BatchPack pk)
+{
+    using S = typename E::S;
+    constexpr uint64_t kTile = uint64_t(kBlock) * U;
+    const uint32_t bid = blockIdx.x, nblocks = gridDim.x;
+    int g = 0;
+    for (uint64_t t = bid; t < pk.tileStart[pk.nseg]; t += nblocks) {
+        while (t >= pk.tileStart[g + 1]) ++g;  // t only grows: the segment index only moves forward
+        const uint64_t base = (t - pk.tileStart[g]) * kTile + threadIdx.x;
+        u32x4 acc[U];
+        FoldTile<E, OP, U, NT, 0, 0>(acc, pk.srcs[g], pk.nsrc, pk.edges[g], base);
+        u32x4* vout = reinterpret_cast<u32x4*>(static_cast<S*>(pk.out[g]) + pk.edges[g].head);
+#pragma unroll
+        for (int u = 0; u < U; ++u) st<NT>(vout + base + u * kBlock, acc[u]);
+    }
+    for (int h = 0; h < pk.nseg; ++h) {
+        S* out = static_cast<S*>(pk.out[h]);
+        const SrcPack& srcs = pk.srcs[h];
+        const Edges& edges = pk.edges[h];
+        u32x4* vout = reinterpret_cast<u32x4*>(out + edges.head);
+        const uint64_t nvec = pk.nvec[h];
+        for (uint64_t i = (pk.tileStart[h + 1] - pk.tileStart[h]) * kTile + uint64_t(bid) * kBlock + threadIdx.x;
+             i < nvec; i += uint64_t(nblocks) * kBlock) {
+            u32x4 acc = ld<NT>(reinterpret_cast<const u32x4*>(static_cast<const S*>(srcs.p[0]) + edges.head) + i);
+            for (int j = 1; j < pk.nsrc; ++j) {
+                acc = combine<E, OP>(
+                    ld<NT>(reinterpret_cast<const u32x4*>(static_cast<const S*>(srcs.p[j]) + edges.head) + i), acc);
+            }
+            st<NT>(vout + i, acc);
+        }
+        if (bid == uint32_t(h) % nblocks) {  // the scalar head and tail of segment h
+            const uint32_t tid = threadIdx.x;
+            uint64_t i = 0;
+            bool act = false;
+            if (tid < edges.head) {
+                i = tid;
+                act = true;
+            } else if (tid >= 64 && tid - 64 < edges.tail) {
+                i = edges.tailStart + (tid - 64);
+                act = true;
+            }
+            if (act) {
+                S acc = static_cast<const S*>(srcs.p[0])[i];
+                for (int j = 1; j < pk.nsrc; ++j) acc = E::template ap<OP>(static_cast<const S*>(srcs.p[j])[i], acc);
+                out[i] = acc;
+            }
+        }
+    }
 }
 
 template <class E, int OP>
@@ -629,18 +693,34 @@ namespace {
 template <class E, int OP>
 hipError_t RunBatch(const BatchPack& pk, uint32_t nseg, uint64_t maxVec, hipStream_t stream)
 {
-    // fill the chip once across the batch: the per-CU budget of the n-ary default, split over the segments
-    const LaunchCfg& cfg = DefaultFor(static_cast<uint32_t>(pk.nsrc));
-    const uint64_t cap = std::max<uint64_t>(1, uint64_t(CuCount()) * cfg.blocksPerCu / nseg);
-    const uint64_t need = std::max<uint64_t>(1, (maxVec + kBlock * cfg.unroll - 1) / (kBlock * cfg.unroll));
-    const uint32_t gx = static_cast<uint32_t>(std::min(cap, need));
-    if (pk.nsrc <= 2) {
-        hipLaunchKernelGGL((k_reduceN_batch<E, OP, kDefaultN2.unroll, kDefaultN2.nt>), dim3(gx, nseg), dim3(kBlock),
-                           0, stream, pk);
-    } else {
-        hipLaunchKernelGGL((k_reduceN_batch<E, OP, kDefaultN.unroll, kDefaultN.nt>), dim3(gx, nseg), dim3(kBlock), 0,
-                           stream, pk);
+    BatchPack p = pk;
+    p.nseg = int(nseg);
+    uint64_t totalVec = 0;
+    for (uint32_t g = 0; g < nseg; ++g) totalVec += pk.nvec[g];
+    if (totalVec * 16 / nseg < kBatchFlatSegBytes) {  // 16-B vectors: the average segment's bytes
+        // rows: the per-CU budget of the n-ary default split over the segments, each row sized for the longest
+        const LaunchCfg& c0 = DefaultFor(static_cast<uint32_t>(pk.nsrc));
+        const uint64_t cap = std::max<uint64_t>(1, uint64_t(CuCount()) * c0.blocksPerCu / nseg);
+        const uint64_t need = std::max<uint64_t>(1, (maxVec + kBlock * c0.unroll - 1) / (kBlock * c0.unroll));
+        const uint32_t gr = static_cast<uint32_t>(std::min(cap, need));
+        if (pk.nsrc <= 2) {
+            hipLaunchKernelGGL((k_reduceN_batch_rows<E, OP, kDefaultN2.unroll, kDefaultN2.nt>), dim3(gr, nseg),
+                               dim3(kBlock), 0, stream, p);
+        } else {
+            hipLaunchKernelGGL((k_reduceN_batch_rows<E, OP, kDefaultN.unroll, kDefaultN.nt>), dim3(gr, nseg),
+                               dim3(kBlock), 0, stream, p);
+        }
+        return hipGetLastError();
     }
+    // flat: one persistent grid over the concatenated tiles, sized like a single fold of the batch's bytes. U = 4 for
+    // every operand count: with two operands too the tile walk wants the larger tile (5.0 / 5.6 / 6.1 TB/s at U = 1 /
+    // 2 / 4 for 4 MiB segments, 5.7 / 6.3 / 6.4 at 16 MiB).
+    const LaunchCfg& cfg = kDefaultN;
+    const uint64_t tileVec = uint64_t(kBlock) * cfg.unroll;
+    p.tileStart[0] = 0;
+    for (uint32_t g = 0; g < nseg; ++g) p.tileStart[g + 1] = p.tileStart[g] + pk.nvec[g] / tileVec;
+    const uint32_t gx = GridFor(totalVec, static_cast<uint32_t>(tileVec), cfg);
+    hipLaunchKernelGGL((k_reduceN_batch<E, OP, kDefaultN.unroll, kDefaultN.nt>), dim3(gx), dim3(kBlock), 0, stream, p);
     return hipGetLastError();
 }
 
