@@ -1,0 +1,247 @@
+"""torch.distributed backend "hccl" over libhccl_amd.so — the position of torch_npu's ProcessGroupHCCL.
+
+The reference's Python caller (examples/03_ai_framework/01_pytorch/hccl_pytorch_allreduce_test.py:19-38) selects
+the backend by name, ``dist.init_process_group(backend="hccl", ...)``, and reduces with ``dist.all_reduce``. Importing
+this module registers that name, so the sample runs with only its device calls changed (``torch_npu.npu.set_device``
+-> ``torch.cuda.set_device``, ``device="npu"`` -> ``"cuda"``)::
+
+    import hccl_amd.process_group  # registers backend "hccl"
+    dist.init_process_group(backend="hccl", rank=rank, world_size=world_size, init_method=init_method)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+
+Every collective is one call of the C ABI (include/hccl.h) on the tensor's current HIP stream; nothing here computes.
+The mapping is the one ProcessGroupHCCL makes:
+
+* ``all_reduce`` -> HcclAllReduce (in place, as torch requires; the reference allows sendBuf == recvBuf,
+  all_reduce_auto_selector.cc:517-550);
+* ``reduce`` -> HcclReduce (root = the group rank ``dst``);
+* ``reduce_scatter_tensor`` / ``reduce_scatter`` -> HcclReduceScatter (input = rankSize blocks of the output's size,
+  reduce_scatter_op.cc:158-159; the list form is packed into one buffer first);
+* ``all_gather_into_tensor`` / ``all_gather`` -> HcclAllGather;
+* ``barrier`` -> a one-element HcclAllReduce, then the host waits for it.
+
+Reduce ops are HCCL's four (SUM, PRODUCT, MAX, MIN; hccl_types.h HcclReduceOp); AVG, PREMUL_SUM and the bitwise ops
+have no HCCL counterpart and raise ValueError, as does any dtype HCCL does not reduce (the entry answers
+HCCL_E_NOT_SUPPORT, which surfaces as HcclError).
+
+The communicator is created on first use, on the device of the first tensor (as ProcessGroupHCCL does): rank 0 calls
+HcclGetRootInfo and publishes the blob through the process group's store, every rank then calls
+HcclCommInitRootInfo (examples/02_collectives/01_allreduce/main.cc:122-136 with the store as the out-of-band channel).
+``HCCL_AMD_PG_TRANSPORT=ipc`` instead makes the IPC-only communicator (HcclAmdCommInitHostExchange) bootstrapped
+through the store; several ranks may then share one GPU (RCCL refuses that), which is how tests/ run the multi-rank
+form on a one-GPU box.
+
+Works complete in stream order: the call is enqueued on the caller's current stream and ``wait()`` makes the stream
+current at wait time wait for it (the NCCL backend's semantics), so the host never blocks except in ``barrier``.
+"""
+from __future__ import annotations
+
+import datetime
+import itertools
+import os
+import threading
+from typing import Callable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+import hccl_amd as H
+
+BACKEND_NAME = "hccl"
+
+_OPS = {
+    dist.ReduceOp.SUM: H.HcclReduceOp.SUM,
+    dist.ReduceOp.PRODUCT: H.HcclReduceOp.PROD,
+    dist.ReduceOp.MAX: H.HcclReduceOp.MAX,
+    dist.ReduceOp.MIN: H.HcclReduceOp.MIN,
+}
+
+
+def hccl_op(reduce_op) -> int:
+    """HcclReduceOp for a torch ReduceOp (SUM/PRODUCT/MAX/MIN); ValueError for the ones HCCL lacks."""
+    for k, v in _OPS.items():
+        if reduce_op == k:
+            return int(v)
+    raise ValueError(f"backend {BACKEND_NAME!r} supports ReduceOp SUM, PRODUCT, MAX and MIN (HcclReduceOp); "
+                     f"got {reduce_op}")
+
+
+class StoreAllGather:
+    """Host all-gather of byte strings through a c10d Store: the bootstrap channel of the IPC-only communicator
+    (HcclAmdHostAllGatherFn). Rounds are numbered, so every rank must call it the same number of times, which the
+    library guarantees (it calls it only inside collective set-up)."""
+
+    def __init__(self, store, rank: int, size: int, prefix: str):
+        self.store, self.rank, self.size, self.prefix = store, rank, size, prefix
+        self.round = 0
+
+    def __call__(self, mine: bytes) -> List[bytes]:
+        k = f"{self.prefix}/ag{self.round}"
+        self.round += 1
+        self.store.set(f"{k}/{self.rank}", mine)
+        return [self.store.get(f"{k}/{r}") for r in range(self.size)]
+
+
+class _Work(dist._Work):
+    """Completion of one enqueued collective: an event recorded on the stream it was enqueued on."""
+
+    def __init__(self, result: List[torch.Tensor], event: Optional[torch.cuda.Event]):
+        super().__init__()
+        self._result = result
+        self._event = event
+        self._future = torch.futures.Future()
+        self._future.set_result(result)
+
+    def wait(self, timeout: Optional[datetime.timedelta] = None) -> bool:
+        if self._event is not None:
+            torch.cuda.current_stream().wait_event(self._event)
+        return True
+
+    def is_completed(self) -> bool:
+        return self._event is None or self._event.query()
+
+    def is_success(self) -> bool:
+        return True
+
+    def result(self) -> List[torch.Tensor]:
+        return self._result
+
+    def get_future(self) -> torch.futures.Future:
+        return self._future
+
+
+class ProcessGroupHCCL(dist.ProcessGroup):
+    """One communicator per process group, created lazily on the first collective's device."""
+
+    _serial = itertools.count(1)  # every rank creates its groups in the same order, so the numbers agree
+
+    def __init__(self, store, rank: int, size: int, timeout: datetime.timedelta,
+                 comm_factory: Optional[Callable[[int], "H.Comm"]] = None):
+        super().__init__(rank, size)
+        self._store = store
+        self._timeout = timeout
+        self._comm = None
+        self._device: Optional[int] = None
+        self._lock = threading.Lock()
+        self._factory = comm_factory or self._make_comm
+        self._prefix = f"hccl_amd/pg{next(ProcessGroupHCCL._serial)}"
+
+    # ------------------------------------------------------------------------------------------------ communicator
+    def _make_comm(self, device: int) -> "H.Comm":
+        n, r = self.size(), self.rank()
+        if os.environ.get("HCCL_AMD_PG_TRANSPORT", "").lower() == "ipc":
+            return H.comm_init_host_exchange(n, r, StoreAllGather(self._store, r, n, self._prefix))
+        key = f"{self._prefix}/root_info"
+        if r == 0:
+            self._store.set(key, H.get_root_info())
+        blob = self._store.get(key)
+        return H.comm_init_root_info(n, bytes(blob), r)
+
+    def comm(self, device: Optional[torch.device] = None) -> "H.Comm":
+        """The group's communicator (created on `device`, default the current device, on first use)."""
+        with self._lock:
+            if self._comm is None:
+                idx = torch.cuda.current_device() if device is None or device.index is None else device.index
+                with torch.cuda.device(idx):
+                    self._comm = self._factory(idx)
+                self._device = idx
+            elif device is not None and device.index is not None and device.index != self._device:
+                raise ValueError(f"backend {BACKEND_NAME!r}: this process group's communicator is on cuda:"
+                                 f"{self._device}, got a tensor on {device}")
+            return self._comm
+
+    # ------------------------------------------------------------------------------------------------ helpers
+    @staticmethod
+    def _check(t: torch.Tensor, what: str) -> None:
+        if not t.is_cuda:
+            raise ValueError(f"backend {BACKEND_NAME!r}: {what} must be a GPU tensor, got {t.device}")
+        if not t.is_contiguous():
+            raise ValueError(f"backend {BACKEND_NAME!r}: {what} must be contiguous")
+
+    def _run(self, result: List[torch.Tensor], device: torch.device, fn) -> _Work:
+        comm = self.comm(device)
+        with torch.cuda.device(device):
+            stream = torch.cuda.current_stream()
+            fn(comm, stream)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        return _Work(result, ev)
+
+    # ------------------------------------------------------------------------------------------------ collectives
+    def allreduce(self, tensors: List[torch.Tensor], opts) -> _Work:
+        op = hccl_op(opts.reduceOp)
+        for t in tensors:
+            self._check(t, "all_reduce tensor")
+        return self._run(tensors, tensors[0].device,
+                         lambda c, s: [c.all_reduce(t, t, op, s) for t in tensors])
+
+    def reduce(self, tensors: List[torch.Tensor], opts) -> _Work:
+        op = hccl_op(opts.reduceOp)
+        t = tensors[opts.rootTensor]
+        self._check(t, "reduce tensor")
+        return self._run(tensors, t.device, lambda c, s: c.reduce(t, t, opts.rootRank, op, s))
+
+    def _reduce_scatter_base(self, output: torch.Tensor, input: torch.Tensor, opts) -> _Work:
+        op = hccl_op(opts.reduceOp)
+        self._check(output, "reduce_scatter output")
+        self._check(input, "reduce_scatter input")
+        if input.numel() != output.numel() * self.size() or input.dtype != output.dtype:
+            raise ValueError(f"backend {BACKEND_NAME!r}: reduce_scatter input must hold world_size x output "
+                             f"elements of the output's dtype")
+        return self._run([output], output.device, lambda c, s: c.reduce_scatter(input, output, op, s))
+
+    def reduce_scatter(self, outputs: List[torch.Tensor], inputs: List[List[torch.Tensor]], opts) -> _Work:
+        if len(outputs) != 1 or len(inputs) != 1 or len(inputs[0]) != self.size():
+            raise ValueError(f"backend {BACKEND_NAME!r}: reduce_scatter takes one output and world_size inputs")
+        packed = torch.cat([x.reshape(-1) for x in inputs[0]])
+        return self._reduce_scatter_base(outputs[0], packed, opts)
+
+    def _allgather_base(self, output: torch.Tensor, input: torch.Tensor, opts) -> _Work:
+        self._check(output, "all_gather output")
+        self._check(input, "all_gather input")
+        if output.numel() != input.numel() * self.size() or input.dtype != output.dtype:
+            raise ValueError(f"backend {BACKEND_NAME!r}: all_gather output must hold world_size x input elements")
+        return self._run([output], output.device, lambda c, s: c.all_gather(input, output, s))
+
+    def allgather(self, outputs: List[List[torch.Tensor]], inputs: List[torch.Tensor], opts) -> _Work:
+        if len(outputs) != 1 or len(inputs) != 1 or len(outputs[0]) != self.size():
+            raise ValueError(f"backend {BACKEND_NAME!r}: all_gather takes one input and world_size outputs")
+        inp = inputs[0]
+        self._check(inp, "all_gather input")
+        flat = torch.empty(inp.numel() * self.size(), dtype=inp.dtype, device=inp.device)
+        work = self._allgather_base(flat, inp, opts)
+        with torch.cuda.device(inp.device):  # unpack on the same stream, after the gather
+            for r, o in enumerate(outputs[0]):
+                o.copy_(flat[r * inp.numel():(r + 1) * inp.numel()].view_as(o))
+        return work
+
+    def barrier(self, opts) -> _Work:
+        dev = torch.device("cuda", self._device if self._device is not None else torch.cuda.current_device())
+        one = torch.ones(1, dtype=torch.int32, device=dev)
+        work = self._run([one], dev, lambda c, s: c.all_reduce(one, one, H.HcclReduceOp.SUM, s))
+        work._event.synchronize()  # a barrier returns to the host only when every rank has arrived
+        return work
+
+    def getBackendName(self) -> str:
+        return BACKEND_NAME
+
+    def shutdown(self) -> None:
+        """Called by dist.destroy_process_group: HcclCommDestroy (collective for IPC communicators)."""
+        with self._lock:
+            if self._comm is not None:
+                if self._device is not None:
+                    torch.cuda.synchronize(self._device)
+                self._comm.destroy()
+                self._comm = None
+
+
+def _create(store, rank: int, size: int, timeout: datetime.timedelta) -> ProcessGroupHCCL:
+    return ProcessGroupHCCL(store, rank, size, timeout)
+
+
+def register(name: str = BACKEND_NAME) -> None:
+    """Registers the backend under `name` for GPU tensors (registering again replaces the creator)."""
+    dist.Backend.register_backend(name, _create, devices=["cuda"])
+
+
+register()

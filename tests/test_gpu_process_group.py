@@ -1,0 +1,141 @@
+"""The reference's PyTorch caller through the "hccl" torch.distributed backend (hccl_amd/process_group.py).
+
+examples/03_ai_framework/01_pytorch/hccl_pytorch_allreduce_test.py:19-38 spawns one process per device, calls
+``dist.init_process_group(backend="hccl")`` and ``dist.all_reduce`` on ``torch.arange(world_size, float32)``; every
+rank must end with ``world_size * arange(world_size)`` (examples/02_collectives/01_allreduce/README_en.md:59-70 for
+8 ranks). Here the same body runs with its device calls changed (npu -> cuda):
+
+* world 1 over the RCCL transport, the root-info blob carried by the process group's store;
+* worlds 2 and 4 as separate processes sharing the one GPU over the IPC-only communicator
+  (HCCL_AMD_PG_TRANSPORT=ipc; RCCL refuses two ranks on one device), with the other collectives the backend maps
+  (reduce, reduce_scatter_tensor / list, all_gather_into_tensor / list, barrier, async work) checked exactly, and a
+  random fp32 all_reduce checked bit-exact against the reference's one-shot order O1 for its size
+  (ins_temp_all_reduce_mesh_1D_one_shot.cc:211-226: acc = x_me, then x_r for r ascending, r != me).
+"""
+import datetime
+import multiprocessing as mp
+import os
+import socket
+import time
+import traceback
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, n, port, transport, q):
+    os.environ["HCCL_AMD_IPC_TIMEOUT_MS"] = "20000"
+    if transport:
+        os.environ["HCCL_AMD_PG_TRANSPORT"] = transport
+    os.makedirs("gpurun_out", exist_ok=True)
+    progress = open(f"gpurun_out/process_group_n{n}_r{rank}.log", "w", buffering=1)
+    try:
+        import torch
+        import torch.distributed as dist
+        import hccl_amd.process_group  # noqa: F401  (registers backend "hccl")
+
+        torch.cuda.set_device(0)  # the sample: torch_npu.npu.set_device(rank); one GPU here
+        dist.init_process_group(backend="hccl", rank=rank, world_size=n, init_method=f"tcp://127.0.0.1:{port}",
+                                timeout=datetime.timedelta(seconds=120))
+        checks = {}
+        # --- the reference sample's body
+        t = torch.arange(n, dtype=torch.float32, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        checks["sample_all_reduce"] = t.cpu().tolist() == [float(n * i) for i in range(n)]
+        progress.write(f"sample {t.cpu().tolist()}\n")
+        # --- random fp32 all_reduce, bit-exact against order O1 (one-shot at this size)
+        count = 4099
+        g = np.random.default_rng(1234)
+        xs = [g.uniform(-1, 1, count).astype(np.float32) for _ in range(n)]
+        x = torch.from_numpy(xs[rank]).cuda()
+        dist.all_reduce(x)
+        acc = xs[rank].copy()
+        for r in range(n):
+            if r != rank:
+                acc = (xs[r] + acc).astype(np.float32)
+        checks["o1_bits"] = np.array_equal(x.cpu().numpy().view(np.uint32), acc.view(np.uint32))
+        # --- MAX / MIN / PRODUCT on integers
+        v = torch.full((1000,), rank + 2, dtype=torch.int32, device="cuda")
+        for op, want in ((dist.ReduceOp.MAX, n + 1), (dist.ReduceOp.MIN, 2),
+                         (dist.ReduceOp.PRODUCT, int(np.prod(np.arange(2, n + 2))))):
+            y = v.clone()
+            dist.all_reduce(y, op=op)
+            checks[f"op_{op}"] = bool(torch.all(y == want).item())
+        # --- reduce to root 1 % n
+        root = 1 % n
+        y = torch.full((5001,), float(rank + 1), device="cuda")
+        dist.reduce(y, dst=root)
+        checks["reduce"] = (not rank == root) or bool(torch.all(y == n * (n + 1) / 2).item())
+        # --- reduce_scatter_tensor and the list form
+        rc = 3001
+        inp = torch.arange(n * rc, dtype=torch.float32, device="cuda") % 113 + rank
+        out = torch.empty(rc, device="cuda")
+        dist.reduce_scatter_tensor(out, inp)
+        want = n * (torch.arange(rank * rc, (rank + 1) * rc, device="cuda", dtype=torch.float32) % 113) + n * (n - 1) / 2
+        checks["reduce_scatter_tensor"] = bool(torch.equal(out, want))
+        out2 = torch.empty(rc, device="cuda")
+        dist.reduce_scatter(out2, list(inp.chunk(n)))
+        checks["reduce_scatter_list"] = bool(torch.equal(out2, want))
+        # --- all_gather_into_tensor and the list form (bf16: data movement, any dtype)
+        a = torch.full((777,), float(rank), dtype=torch.bfloat16, device="cuda")
+        full = torch.empty(777 * n, dtype=torch.bfloat16, device="cuda")
+        dist.all_gather_into_tensor(full, a)
+        checks["all_gather_into_tensor"] = bool(torch.equal(
+            full, torch.arange(n, device="cuda").repeat_interleave(777).to(torch.bfloat16)))
+        parts = [torch.empty(777, dtype=torch.bfloat16, device="cuda") for _ in range(n)]
+        dist.all_gather(parts, a)
+        checks["all_gather_list"] = all(bool(torch.all(p == q).item()) for q, p in enumerate(parts))
+        # --- async work on a side stream, then wait() orders the current stream after it
+        s = torch.cuda.Stream()
+        z = torch.full((1 << 20,), 1.0, device="cuda")
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s):
+            work = dist.all_reduce(z, async_op=True)
+        work.wait()
+        checks["async_wait"] = bool(torch.all(z == n).item())
+        # --- unsupported op and dtype surface as errors, not wrong data
+        try:
+            dist.all_reduce(torch.ones(4, device="cuda"), op=dist.ReduceOp.AVG)
+            checks["avg_refused"] = False
+        except ValueError:
+            checks["avg_refused"] = True
+        dist.barrier()
+        dist.destroy_process_group()  # ProcessGroupHCCL.shutdown -> HcclCommDestroy
+        progress.write(f"checks {checks}\n")
+        q.put((rank, "ok", checks))
+    except Exception:  # noqa: BLE001
+        progress.write(traceback.format_exc())
+        q.put((rank, traceback.format_exc(), None))
+        time.sleep(10)
+
+
+@pytest.mark.parametrize("n,transport", [(1, ""), (2, "ipc"), (4, "ipc")])
+def test_reference_pytorch_sample(n, transport):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, n, port, transport, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    try:
+        got = {}
+        for _ in procs:
+            rank, msg, res = q.get(timeout=240)
+            got[rank] = (msg, res)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(n):
+        msg, res = got[r]
+        assert msg == "ok", f"rank {r}: {msg}"
+        assert all(res.values()), f"rank {r}: {res}"
