@@ -9,7 +9,7 @@ this module registers that name, so the sample runs with only its device calls c
     dist.init_process_group(backend="hccl", rank=rank, world_size=world_size, init_method=init_method)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
 
-Every collective is one call of the C ABI (include/hccl.h) on the tensor's current HIP stream; nothing here computes.
+Every collective is one call of the C ABI (include/hccl.h) on a HIP stream; nothing here computes.
 The mapping is the one ProcessGroupHCCL makes:
 
 * ``all_reduce`` -> HcclAllReduce (in place, as torch requires; the reference allows sendBuf == recvBuf,
@@ -31,8 +31,10 @@ HcclCommInitRootInfo (examples/02_collectives/01_allreduce/main.cc:122-136 with 
 through the store; several ranks may then share one GPU (RCCL refuses that), which is how tests/ run the multi-rank
 form on a one-GPU box.
 
-Works complete in stream order: the call is enqueued on the caller's current stream and ``wait()`` makes the stream
-current at wait time wait for it (the NCCL backend's semantics), so the host never blocks except in ``barrier``.
+Streams are the NCCL backend's: each group owns one stream per device (the HCCL entries reject the null stream,
+as the reference's do, and torch's default stream is the null stream). A collective waits there for the caller's
+current stream, runs, and marks its tensors as used on that stream for the caching allocator; ``wait()`` makes the
+then-current stream wait for it. The host never blocks except in ``barrier``.
 """
 from __future__ import annotations
 
@@ -64,6 +66,10 @@ def hccl_op(reduce_op) -> int:
             return int(v)
     raise ValueError(f"backend {BACKEND_NAME!r} supports ReduceOp SUM, PRODUCT, MAX and MIN (HcclReduceOp); "
                      f"got {reduce_op}")
+
+
+def output_dtype_mismatch(outputs: List[torch.Tensor], inp: torch.Tensor) -> bool:
+    return any(o.numel() != inp.numel() or o.dtype != inp.dtype or o.device != inp.device for o in outputs)
 
 
 class StoreAllGather:
@@ -122,6 +128,7 @@ class ProcessGroupHCCL(dist.ProcessGroup):
         self._timeout = timeout
         self._comm = None
         self._device: Optional[int] = None
+        self._stream: Optional[torch.cuda.Stream] = None
         self._lock = threading.Lock()
         self._factory = comm_factory or self._make_comm
         self._prefix = f"hccl_amd/pg{next(ProcessGroupHCCL._serial)}"
@@ -130,7 +137,9 @@ class ProcessGroupHCCL(dist.ProcessGroup):
     def _make_comm(self, device: int) -> "H.Comm":
         n, r = self.size(), self.rank()
         if os.environ.get("HCCL_AMD_PG_TRANSPORT", "").lower() == "ipc":
-            return H.comm_init_host_exchange(n, r, StoreAllGather(self._store, r, n, self._prefix))
+            c = H.comm_init_host_exchange(n, r, StoreAllGather(self._store, r, n, self._prefix))
+            c.set_algo(H.Algo.IPC)  # the reference's default selection, so the bits are those of the RCCL path
+            return c
         key = f"{self._prefix}/root_info"
         if r == 0:
             self._store.set(key, H.get_root_info())
@@ -158,13 +167,18 @@ class ProcessGroupHCCL(dist.ProcessGroup):
         if not t.is_contiguous():
             raise ValueError(f"backend {BACKEND_NAME!r}: {what} must be contiguous")
 
-    def _run(self, result: List[torch.Tensor], device: torch.device, fn) -> _Work:
+    def _run(self, result: List[torch.Tensor], device: torch.device, fn, used: List[torch.Tensor]) -> _Work:
         comm = self.comm(device)
         with torch.cuda.device(device):
-            stream = torch.cuda.current_stream()
-            fn(comm, stream)
+            if self._stream is None:
+                self._stream = torch.cuda.Stream()
+            side = self._stream
+            side.wait_stream(torch.cuda.current_stream())
+            fn(comm, side)
+            for t in used:
+                t.record_stream(side)
             ev = torch.cuda.Event()
-            ev.record(stream)
+            ev.record(side)
         return _Work(result, ev)
 
     # ------------------------------------------------------------------------------------------------ collectives
@@ -173,13 +187,13 @@ class ProcessGroupHCCL(dist.ProcessGroup):
         for t in tensors:
             self._check(t, "all_reduce tensor")
         return self._run(tensors, tensors[0].device,
-                         lambda c, s: [c.all_reduce(t, t, op, s) for t in tensors])
+                         lambda c, s: [c.all_reduce(t, t, op, s) for t in tensors], tensors)
 
     def reduce(self, tensors: List[torch.Tensor], opts) -> _Work:
         op = hccl_op(opts.reduceOp)
         t = tensors[opts.rootTensor]
         self._check(t, "reduce tensor")
-        return self._run(tensors, t.device, lambda c, s: c.reduce(t, t, opts.rootRank, op, s))
+        return self._run(tensors, t.device, lambda c, s: c.reduce(t, t, opts.rootRank, op, s), [t])
 
     def _reduce_scatter_base(self, output: torch.Tensor, input: torch.Tensor, opts) -> _Work:
         op = hccl_op(opts.reduceOp)
@@ -188,7 +202,8 @@ class ProcessGroupHCCL(dist.ProcessGroup):
         if input.numel() != output.numel() * self.size() or input.dtype != output.dtype:
             raise ValueError(f"backend {BACKEND_NAME!r}: reduce_scatter input must hold world_size x output "
                              f"elements of the output's dtype")
-        return self._run([output], output.device, lambda c, s: c.reduce_scatter(input, output, op, s))
+        return self._run([output], output.device, lambda c, s: c.reduce_scatter(input, output, op, s),
+                         [input, output])
 
     def reduce_scatter(self, outputs: List[torch.Tensor], inputs: List[List[torch.Tensor]], opts) -> _Work:
         if len(outputs) != 1 or len(inputs) != 1 or len(inputs[0]) != self.size():
@@ -201,24 +216,32 @@ class ProcessGroupHCCL(dist.ProcessGroup):
         self._check(input, "all_gather input")
         if output.numel() != input.numel() * self.size() or input.dtype != output.dtype:
             raise ValueError(f"backend {BACKEND_NAME!r}: all_gather output must hold world_size x input elements")
-        return self._run([output], output.device, lambda c, s: c.all_gather(input, output, s))
+        return self._run([output], output.device, lambda c, s: c.all_gather(input, output, s),
+                         [input, output])
 
     def allgather(self, outputs: List[List[torch.Tensor]], inputs: List[torch.Tensor], opts) -> _Work:
         if len(outputs) != 1 or len(inputs) != 1 or len(outputs[0]) != self.size():
             raise ValueError(f"backend {BACKEND_NAME!r}: all_gather takes one input and world_size outputs")
         inp = inputs[0]
         self._check(inp, "all_gather input")
-        flat = torch.empty(inp.numel() * self.size(), dtype=inp.dtype, device=inp.device)
-        work = self._allgather_base(flat, inp, opts)
-        with torch.cuda.device(inp.device):  # unpack on the same stream, after the gather
-            for r, o in enumerate(outputs[0]):
-                o.copy_(flat[r * inp.numel():(r + 1) * inp.numel()].view_as(o))
-        return work
+        if output_dtype_mismatch(outputs[0], inp):
+            raise ValueError(f"backend {BACKEND_NAME!r}: all_gather outputs must match the input's size and dtype")
+        m = inp.numel()
+        flat = torch.empty(m * self.size(), dtype=inp.dtype, device=inp.device)
+
+        def gather_and_unpack(c, s):
+            c.all_gather(inp, flat, s)
+            with torch.cuda.stream(s):  # unpacked on the group's stream, after the gather
+                for r, o in enumerate(outputs[0]):
+                    o.copy_(flat[r * m:(r + 1) * m].view_as(o))
+
+        return self._run(outputs[0], inp.device, gather_and_unpack, [inp, flat] + list(outputs[0]))
 
     def barrier(self, opts) -> _Work:
         dev = torch.device("cuda", self._device if self._device is not None else torch.cuda.current_device())
         one = torch.ones(1, dtype=torch.int32, device=dev)
-        work = self._run([one], dev, lambda c, s: c.all_reduce(one, one, H.HcclReduceOp.SUM, s))
+        work = self._run([one], dev, lambda c, s: c.all_reduce(one, one, H.HcclReduceOp.SUM, s),
+                         [one])
         work._event.synchronize()  # a barrier returns to the host only when every rank has arrived
         return work
 
