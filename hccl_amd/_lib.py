@@ -84,6 +84,7 @@ class Algo(enum.IntEnum):
     IPC = 9
     AIV = 10
     AIV_ONLY = 11
+    IPC_RHD = 12
 
 
 class AivVariant(enum.IntEnum):

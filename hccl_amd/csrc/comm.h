@@ -146,6 +146,7 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
 // The same for an explicit plan (the AIV engine's variants, SelectAivPlan).
 HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* sendBuf, void* recvBuf, uint64_t count,
                       HcclDataType dt, HcclReduceOp op, uint32_t root, hipStream_t stream);
+HcclResult IpcPlanRhd(uint32_t n, IpcPlan* pl);
 HcclResult IpcPlanForFamily(int32_t opType, int32_t family, uint32_t n, uint64_t es, uint64_t cclBytes, IpcPlan* pl);
 
 // The reference's AIV engine (HCCL_OP_EXPANSION_MODE=AIV): SelectAivAlgo's rules and the variant its kernel takes

@@ -294,6 +294,20 @@ HcclResult IpcPlanForFamily(int32_t opType, int32_t family, uint32_t n, uint64_t
     return HCCL_SUCCESS;
 }
 
+// RHD's bits on the one-sided kernel (HCCL_AMD_ALGO_IPC_RHD): the one-shot kind in order kIpcRhd over the whole
+// range. AllReduceRhd has no executor loops (it is not a reference template), so neither does this: its slicing is
+// a function of the count alone.
+HcclResult IpcPlanRhd(uint32_t n, IpcPlan* pl)
+{
+    if (RhdTable(n).empty() || n < 2) return HCCL_E_NOT_SUPPORT;
+    IpcPlan p{};
+    p.kind = kIpcAllReduceOneShot;
+    p.order = kIpcRhd;
+    p.geom = kIpcGeomWhole;
+    *pl = p;
+    return HCCL_SUCCESS;
+}
+
 uint32_t AivCoreLimit()
 {
     // The reference takes the vector-core count from the comm config (aivCoreLimit) or the device
@@ -447,6 +461,14 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
     const uint64_t callBytes = (blockLayout ? uint64_t(c.nRanks) : 1u) * count * es;  // RS input / AG output
     s.blocks = c.ipcBlocks != 0 ? c.ipcBlocks : DefaultIpcBlocks(callBytes);
     if (c.transport->SharedDevice()) s.blocks = std::min(s.blocks, kIpcBlocks);
+    // Co-residency: every block waits at barriers for its peers' blocks, so all blocks on this device must be resident
+    // at once (a loopback world puts every rank's blocks on it). The count depends only on the kernel and the device,
+    // so ranks of a node agree on it.
+    {
+        const uint32_t here = c.transport->SharedDevice() ? n : 1u;
+        const uint32_t resident = IpcResidentBlocks(dt, op, plan.order == kIpcRhd);
+        if (resident != 0) s.blocks = std::max<uint32_t>(1, std::min(s.blocks, resident / here));
+    }
     const uint64_t V = 16 / es;
 
     IpcArgs a{};
@@ -467,6 +489,19 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
     a.outStride = count;
     a.altOff = s.stgInBytes + s.stgResBytes;
     a.altBytes = s.stgAltBytes;
+    if (plan.order == kIpcRhd) {
+        // the RHD schedule's parts and relabelling (AllReduceRhd): R instances over Chunk(count, R, j) parts
+        const std::vector<std::vector<uint32_t>> table = RhdTable(n);
+        const uint32_t parts = std::min<uint32_t>(static_cast<uint32_t>(table.size()), RhdInstances(n, count * es));
+        if (parts == 0 || loopElems != 0) return HCCL_E_INTERNAL;
+        a.rhdParts = parts;
+        a.alignElems = static_cast<uint32_t>(std::max<uint64_t>(1, 128 / es));
+        const uint64_t stride = (count + parts - 1) / parts;
+        a.rhdPartStride = std::max<uint64_t>(1, (stride + a.alignElems - 1) / a.alignElems * a.alignElems);
+        for (uint32_t j = 0; j < parts; ++j) {
+            for (uint32_t v = 0; v < n; ++v) a.rhdReal[j][v] = static_cast<uint8_t>(table[j][v]);
+        }
+    }
     const bool single = SingleBarrierKind(kind);
     const uint64_t slotCap = ((single ? s.stgAltBytes : s.stgInBytes) / es / n) / V * V;
 

@@ -30,6 +30,8 @@ enum IpcOrder : uint32_t {
     kIpcO4 = 3,  // pow-2 tree over the source ranks (rank-independent): M = largest power of two below n,
                  // x_j = x_{j+M} (op) x_j for j + M < n, then pairwise halving  AIV local-tree ReduceScatter
                  // (aiv_reduce_scatter_local_tree.h:138-172) = the STRICT order-preserved tree
+    kIpcRhd = 4,  // one-shot kind only: the RHD AllReduce's bits (schedule.cc AllReduceRhd), per element the O4 tree
+                  // over virtual ranks v ^ q of its RHD instance, v = the owner of its chunk (RhdFold)
 };
 
 // Chunk layout of one launch (input coordinates, elements; rank c owns chunk c).
@@ -117,10 +119,18 @@ struct IpcArgs {
                        // [5]: blocks of the running launch that have finished (kIpcEpochWord, kIpcDoneWord)
     uint32_t callSeq;  // this call's sequence number on the communicator
     bool aligned;      // every in[] / out[] is 16-B aligned (chunks whose start is not are still element-wise)
+    uint32_t rhdParts;       // kIpcRhd: RHD instances R (parts of the launch's range)
+    uint32_t alignElems;     // kIpcRhd: HCCL_MIN_SLICE_ALIGN (128 B) in elements
+    uint64_t rhdPartStride;  // kIpcRhd: elements per part (the last part may be shorter)
+    uint8_t rhdReal[kIpcMaxRanks - 1][kIpcMaxRanks];  // kIpcRhd: per instance j, virtual rank -> real rank
 };
 
 HcclResult LaunchIpcCollective(const IpcArgs& a, uint32_t blocks, uint32_t worldRanks, HcclDataType dt,
                               HcclReduceOp op, hipStream_t stream);
+
+// Workgroups of the IPC kernel for (dt, op) that the device holds at once (occupancy x CUs; 0 if unknown). Every
+// block of a launch waits at barriers for its peers' blocks, so the blocks that share a device must all be resident.
+uint32_t IpcResidentBlocks(HcclDataType dt, HcclReduceOp op, bool rhd);
 
 // Writes back and invalidates every XCD's L2 at system scope (one maintenance block per CU); synchronous on `stream`.
 HcclResult ScrubL2(hipStream_t stream);

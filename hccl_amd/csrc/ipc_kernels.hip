@@ -33,6 +33,8 @@
 // sharing the GPU.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "internal.h"
 #include "ipc.h"
 #include "reduce_elem.h"
@@ -311,6 +313,34 @@ __device__ __forceinline__ auto TreeFoldN(uint32_t n, const Leaf& leaf)
     return TreeFold<E, OP, 1>(n, leaf);
 }
 
+// Order O4 over the piece range r: operand q of the tree is rank rankOf(q)'s (rankSrc gives a rank's operand in piece
+// coordinates). One vector (or element) per lane and step keeps the register stack small.
+template <class E, int OP, class Dst, class RankSrc, class RankOf>
+__device__ __forceinline__ void TreeSeg(uint32_t n, const RankSrc& rankSrc, const RankOf& rankOf, Dst dsts,
+                                        uint32_t ndst, Range r, bool vec)
+{
+    using S = typename E::S;
+    constexpr uint64_t V = 16 / sizeof(S);
+    const uint64_t vb = (r.lo + V - 1) / V, ve = r.hi / V;
+    auto scalarTree = [&](uint64_t lo, uint64_t hi) {
+        for (uint64_t e = lo + threadIdx.x; e < hi; e += kIpcBlock) {
+            const S acc = TreeFoldN<E, OP>(n, [&](uint32_t q) { return rankSrc(rankOf(q))[e]; });
+            for (uint32_t d = 0; d < ndst; ++d) dsts(d)[e] = acc;
+        }
+    };
+    if (!vec || vb >= ve) {
+        scalarTree(r.lo, r.hi);
+        return;
+    }
+    scalarTree(r.lo, vb * V);
+    for (uint64_t v = vb + threadIdx.x; v < ve; v += kIpcBlock) {
+        const u32x4 acc = TreeFoldN<E, OP>(
+            n, [&](uint32_t q) { return reinterpret_cast<const u32x4*>(rankSrc(rankOf(q)))[v]; });
+        for (uint32_t d = 0; d < ndst; ++d) reinterpret_cast<u32x4*>(dsts(d))[v] = acc;
+    }
+    scalarTree(ve * V, r.hi);
+}
+
 // Fold of the piece range r (piece coordinates) of chunk `me` over the n operands, operand i being rank
 // OperandRank(order, n, me, j, i) (order O4: the tree over the ranks), written to ndst destinations. own = this rank's
 // operand, slots = its staging (slot q at q * piece). vec: the chunk's operands are 16-B aligned at piece coordinate
@@ -324,25 +354,8 @@ __device__ __forceinline__ void FoldSeg(const IpcArgs& a, uint32_t me, uint32_t 
     const uint32_t n = a.n;
     auto rankSrc = [&](uint32_t q) { return q == me ? own : slots + uint64_t(q) * a.piece; };
     if (a.order == kIpcO4) {
-        // rank-independent tree: one vector (or element) per lane and step keeps the register stack small
-        const uint64_t vb = (r.lo + V - 1) / V, ve = r.hi / V;
-        auto scalarTree = [&](uint64_t lo, uint64_t hi) {
-            for (uint64_t e = lo + threadIdx.x; e < hi; e += kIpcBlock) {
-                const S acc = TreeFoldN<E, OP>(n, [&](uint32_t q) { return rankSrc(q)[e]; });
-                for (uint32_t d = 0; d < ndst; ++d) dsts(d)[e] = acc;
-            }
-        };
-        if (!vec || vb >= ve) {
-            scalarTree(r.lo, r.hi);
-            return;
-        }
-        scalarTree(r.lo, vb * V);
-        for (uint64_t v = vb + threadIdx.x; v < ve; v += kIpcBlock) {
-            const u32x4 acc = TreeFoldN<E, OP>(
-                n, [&](uint32_t q) { return reinterpret_cast<const u32x4*>(rankSrc(q))[v]; });
-            for (uint32_t d = 0; d < ndst; ++d) reinterpret_cast<u32x4*>(dsts(d))[v] = acc;
-        }
-        scalarTree(ve * V, r.hi);
+        // rank-independent tree
+        TreeSeg<E, OP>(n, rankSrc, [](uint32_t q) { return q; }, dsts, ndst, r, vec);
         return;
     }
     auto src = [&](uint32_t i) { return rankSrc(OperandRank(a.order, n, me, j, i)); };
@@ -384,13 +397,49 @@ __device__ __forceinline__ void FoldSeg(const IpcArgs& a, uint32_t me, uint32_t 
     scalar(ve * V, r.hi);
 }
 
-// The block's window r of round k (piece coordinates, chunk offset kP) of chunk `me`: one FoldSeg, or, in order O6,
-// one per sub-slice the window meets.
+// Order kIpcRhd (one-shot kind, whole range: piece coordinate e is element kP + e of the launch). The RHD AllReduce
+// (schedule.cc AllReduceRhd) splits the buffer into R parts, instance j running the classic recursive halving on
+// virtual ranks (virtual v = real rhdReal[j][v]) over n chunks of its part, each fold dst = partner (op) mine. The
+// element's value is then the O4 tree over the operands of virtual ranks v ^ q, q = 0 .. n-1, v its chunk's owner:
+// round M of O4 folds leaf q + M into leaf q, which is exactly the step at distance M folding partner v ^ q ^ M into
+// v ^ q (tests/test_ipc_rhd_order.py checks the identity against the schedule's closed form). Split the window at
+// part and chunk boundaries (Chunk() of schedule.cc: ceil splits rounded up to HCCL_MIN_SLICE_ALIGN).
 template <class E, int OP, class Dst>
+__device__ __forceinline__ void RhdFold(const IpcArgs& a, uint32_t me, uint64_t kP, const typename E::S* own,
+                                        const typename E::S* slots, Dst dsts, uint32_t ndst, Range r, bool vec)
+{
+    const uint32_t n = a.n;
+    auto rankSrc = [&](uint32_t q) { return q == me ? own : slots + uint64_t(q) * a.piece; };
+    uint64_t g = kP + r.lo;
+    const uint64_t g1 = kP + r.hi;
+    while (g < g1) {
+        const uint32_t j = static_cast<uint32_t>(g / a.rhdPartStride);
+        const uint64_t pb = uint64_t(j) * a.rhdPartStride;
+        const uint64_t plen = min(a.total, pb + a.rhdPartStride) - pb;
+        const uint64_t sc = ((plen + n - 1) / n + a.alignElems - 1) / a.alignElems * a.alignElems;
+        const uint32_t v = static_cast<uint32_t>((g - pb) / sc);
+        const uint64_t end = min(g1, pb + min(plen, uint64_t(v + 1) * sc));
+        // operand q of the tree is real rank rhdReal[j][v ^ q], packed 4 bits per operand (n <= 16) so the tree's
+        // compile-time operand numbers select it with a shift
+        uint64_t packed = 0;
+        for (uint32_t q = 0; q < n; ++q) packed |= uint64_t(a.rhdReal[j][v ^ q]) << (4 * q);
+        TreeSeg<E, OP>(n, rankSrc, [packed](uint32_t q) { return uint32_t(packed >> (4 * q)) & 15u; }, dsts, ndst,
+                       Range{g - kP, end - kP}, vec);
+        g = end;
+    }
+}
+
+// The block's window r of round k (piece coordinates, chunk offset kP) of chunk `me`: one FoldSeg, or, in order O6,
+// one per sub-slice the window meets (kIpcRhd: one tree per RHD chunk the window meets).
+template <class E, int OP, bool kRhd, class Dst>
 __device__ __forceinline__ void FoldRange(const IpcArgs& a, uint32_t me, uint64_t kP, const typename E::S* own,
                                           const typename E::S* slots, Dst dsts, uint32_t ndst, Range r, bool vec)
 {
     using S = typename E::S;
+    if constexpr (kRhd) {
+        RhdFold<E, OP>(a, me, kP, own, slots, dsts, ndst, r, vec);
+        return;
+    }
     if (a.order != kIpcO6) {
         FoldSeg<E, OP>(a, me, 0, own, slots, dsts, ndst, r, vec);
         return;
@@ -403,16 +452,20 @@ __device__ __forceinline__ void FoldRange(const IpcArgs& a, uint32_t me, uint64_
     }
 }
 
-template <class E, int OP>
+// kRhd: the kIpcRhd instantiation (one-shot AllReduce only, kind and order fixed at compile time). It is a kernel of
+// its own so that the RHD tree's register use never lowers the occupancy of the others: a loopback world needs every
+// rank's blocks resident at once.
+template <class E, int OP, bool kRhd>
 __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
 {
+    const uint32_t kind = kRhd ? uint32_t(kIpcAllReduceOneShot) : a.kind;
     using S = typename E::S;
     const uint32_t n = a.n;
     const uint32_t me = a.me >= 0 ? static_cast<uint32_t>(a.me) : blockIdx.y;
     const S* in = static_cast<const S*>(a.in[me]);
     S* out = static_cast<S*>(a.out[me]);
-    const bool oneShot = a.kind == kIpcAllReduceOneShot || a.kind == kIpcReduceOneShot;
-    const bool reduceKind = a.kind == kIpcReduce || a.kind == kIpcReduceOneShot;
+    const bool oneShot = kind == kIpcAllReduceOneShot || kind == kIpcReduceOneShot;
+    const bool reduceKind = kind == kIpcReduce || kind == kIpcReduceOneShot;
     // a communicator whose IPC barrier ever timed out stays failed (sticky bit): never wait on its peers again
     if ((__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 1u) != 0) return;
     // Slots: the two-barrier kinds use stgIn. The single-barrier kinds alternate between two areas by the parity of
@@ -427,7 +480,7 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
     //     started only after the launch with round k had ended.
     // No two-barrier kind touches these areas, so a peer still in phase 2 of an earlier call is never disturbed, and a
     // later two-shot call never stores over a fold that runs after the last barrier.
-    const bool single = SingleBarrierKind(a.kind);
+    const bool single = SingleBarrierKind(kind);
     auto slotArea = [&](uint32_t c, uint32_t e) -> char* {
         char* base = static_cast<char*>(a.stgIn[c]);
         return single ? base + a.altOff + (e & 1u) * a.altBytes : base;
@@ -445,13 +498,13 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
         // moment the blocks of a rank spread their stores over all n-1 xGMI links instead of all feeding one peer.
         for (uint32_t i = 0; i + 1 < n; ++i) {
             const uint32_t c = (me + 1 + (i + blockIdx.x) % (n - 1)) % n;
-            if (a.kind == kIpcReduceOneShot && c != a.root) continue;
+            if (kind == kIpcReduceOneShot && c != a.root) continue;
             const Range r = BlockWindow(a, PieceLen(a, c, kP));
             S* slot = reinterpret_cast<S*>(slotArea(c, epoch + 1)) + uint64_t(me) * a.piece;
             CopyRange<S>(slot, in + ChunkStart(a, c) + kP, r, ChunkVec<S>(a, c));
         }
         if (!Barrier(a, fl, ++epoch, waitMax)) break;
-        if (a.kind == kIpcAllGather) {
+        if (kind == kIpcAllGather) {
             // phase 1 of an AllGather: rank q's piece, from my slot q (mine from my input), to output block q
             const Range r = BlockWindow(a, PieceLen(a, me, kP));
             const S* slots = reinterpret_cast<const S*>(slotArea(me, epoch));
@@ -461,7 +514,7 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
                 S* dst = out + uint64_t(q) * a.outStride + kP;
                 if (src != dst) CopyRange<S>(dst, src, r, a.aligned && (uint64_t(q) * a.outStride) % V == 0);
             }
-        } else if (!(a.kind == kIpcReduceOneShot && me != a.root)) {
+        } else if (!(kind == kIpcReduceOneShot && me != a.root)) {
             // phase 1: fold my chunk's piece over the slots (my own operand straight from my input)
             const Range r = BlockWindow(a, PieceLen(a, me, kP));
             const S* own = in + ChunkStart(a, me) + kP;
@@ -469,8 +522,8 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
             // destination 0: my output (or, for a non-root two-shot Reduce rank, the root's result area); the
             // two-shot AllReduce also pushes to every peer's result area (destinations 1 .. n-1 = the peers in
             // ascending order)
-            S* first = a.kind == kIpcReduceScatter ? out + kP
-                     : (a.kind == kIpcReduce && me != a.root)
+            S* first = kind == kIpcReduceScatter ? out + kP
+                     : (kind == kIpcReduce && me != a.root)
                          ? static_cast<S*>(a.stgRes[a.root]) + uint64_t(me) * a.piece
                          : out + ChunkStart(a, me) + kP;
             auto dst = [&](uint32_t d) {
@@ -478,12 +531,12 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
                 const uint32_t p = d - 1 < me ? d - 1 : d;
                 return static_cast<S*>(a.stgRes[p]) + uint64_t(me) * a.piece;
             };
-            FoldRange<E, OP>(a, me, kP, own, slots, dst, a.kind == kIpcAllReduce ? n : 1u, r, ChunkVec<S>(a, me));
+            FoldRange<E, OP, kRhd>(a, me, kP, own, slots, dst, kind == kIpcAllReduce ? n : 1u, r, ChunkVec<S>(a, me));
         }
         if (!single && !Barrier(a, fl, ++epoch, waitMax)) break;
         // phase 2: the other chunks' results from my own result area (two-shot AllReduce: every rank; two-shot
         // Reduce: the root)
-        if (!oneShot && (a.kind == kIpcAllReduce || (reduceKind && me == a.root))) {
+        if (!oneShot && (kind == kIpcAllReduce || (reduceKind && me == a.root))) {
             for (uint32_t c = 0; c < n; ++c) {
                 if (c == me) continue;
                 const Range r = BlockWindow(a, PieceLen(a, c, kP));
@@ -499,11 +552,20 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
 template <class E>
 hipError_t LaunchIpcT(int op, const IpcArgs& a, dim3 grid, hipStream_t s)
 {
+    if (a.order == kIpcRhd) {
+        switch (op) {
+            case R_SUM: hipLaunchKernelGGL((k_ipc_collective<E, R_SUM, true>), grid, dim3(kIpcBlock), 0, s, a); break;
+            case R_PROD: hipLaunchKernelGGL((k_ipc_collective<E, R_PROD, true>), grid, dim3(kIpcBlock), 0, s, a); break;
+            case R_MAX: hipLaunchKernelGGL((k_ipc_collective<E, R_MAX, true>), grid, dim3(kIpcBlock), 0, s, a); break;
+            default: hipLaunchKernelGGL((k_ipc_collective<E, R_MIN, true>), grid, dim3(kIpcBlock), 0, s, a); break;
+        }
+        return hipGetLastError();
+    }
     switch (op) {
-        case R_SUM: hipLaunchKernelGGL((k_ipc_collective<E, R_SUM>), grid, dim3(kIpcBlock), 0, s, a); break;
-        case R_PROD: hipLaunchKernelGGL((k_ipc_collective<E, R_PROD>), grid, dim3(kIpcBlock), 0, s, a); break;
-        case R_MAX: hipLaunchKernelGGL((k_ipc_collective<E, R_MAX>), grid, dim3(kIpcBlock), 0, s, a); break;
-        default: hipLaunchKernelGGL((k_ipc_collective<E, R_MIN>), grid, dim3(kIpcBlock), 0, s, a); break;
+        case R_SUM: hipLaunchKernelGGL((k_ipc_collective<E, R_SUM, false>), grid, dim3(kIpcBlock), 0, s, a); break;
+        case R_PROD: hipLaunchKernelGGL((k_ipc_collective<E, R_PROD, false>), grid, dim3(kIpcBlock), 0, s, a); break;
+        case R_MAX: hipLaunchKernelGGL((k_ipc_collective<E, R_MAX, false>), grid, dim3(kIpcBlock), 0, s, a); break;
+        default: hipLaunchKernelGGL((k_ipc_collective<E, R_MIN, false>), grid, dim3(kIpcBlock), 0, s, a); break;
     }
     return hipGetLastError();
 }
@@ -538,6 +600,62 @@ HcclResult ScrubL2(hipStream_t stream)
         return HCCL_E_RUNTIME;
     }
     return HCCL_SUCCESS;
+}
+
+namespace {
+
+template <class E>
+const void* IpcKernelT(int op, bool rhd)
+{
+    if (rhd) {
+        switch (op) {
+            case R_SUM: return reinterpret_cast<const void*>(&k_ipc_collective<E, R_SUM, true>);
+            case R_PROD: return reinterpret_cast<const void*>(&k_ipc_collective<E, R_PROD, true>);
+            case R_MAX: return reinterpret_cast<const void*>(&k_ipc_collective<E, R_MAX, true>);
+            default: return reinterpret_cast<const void*>(&k_ipc_collective<E, R_MIN, true>);
+        }
+    }
+    switch (op) {
+        case R_SUM: return reinterpret_cast<const void*>(&k_ipc_collective<E, R_SUM, false>);
+        case R_PROD: return reinterpret_cast<const void*>(&k_ipc_collective<E, R_PROD, false>);
+        case R_MAX: return reinterpret_cast<const void*>(&k_ipc_collective<E, R_MAX, false>);
+        default: return reinterpret_cast<const void*>(&k_ipc_collective<E, R_MIN, false>);
+    }
+}
+
+}  // namespace
+
+uint32_t IpcResidentBlocks(HcclDataType dt, HcclReduceOp op, bool rhd)
+{
+    // per process and (dtype, op, kind of kernel); one device model per node (0 = not yet asked)
+    static std::atomic<uint32_t> cache[32][4][2];
+    const uint32_t di = static_cast<uint32_t>(dt), oi = static_cast<uint32_t>(op);
+    if (di < 32 && oi < 4) {
+        const uint32_t v = cache[di][oi][rhd ? 1 : 0].load(std::memory_order_relaxed);
+        if (v != 0) return v;
+    }
+    const void* k = nullptr;
+    switch (dt) {
+        case HCCL_DATA_TYPE_INT8: k = IpcKernelT<EInt<int8_t, uint32_t>>(op, rhd); break;
+        case HCCL_DATA_TYPE_INT16: k = IpcKernelT<EInt<int16_t, uint32_t>>(op, rhd); break;
+        case HCCL_DATA_TYPE_INT32: k = IpcKernelT<EInt<int32_t, uint32_t>>(op, rhd); break;
+        case HCCL_DATA_TYPE_INT64: k = IpcKernelT<EInt<int64_t, uint64_t>>(op, rhd); break;
+        case HCCL_DATA_TYPE_UINT64: k = IpcKernelT<EInt<uint64_t, uint64_t>>(op, rhd); break;
+        case HCCL_DATA_TYPE_FP16: k = IpcKernelT<EF16>(op, rhd); break;
+        case HCCL_DATA_TYPE_BFP16: k = IpcKernelT<EBF16>(op, rhd); break;
+        case HCCL_DATA_TYPE_FP32: k = IpcKernelT<EFp<float>>(op, rhd); break;
+        case HCCL_DATA_TYPE_FP64: k = IpcKernelT<EFp<double>>(op, rhd); break;
+        default: return 0;
+    }
+    int perCu = 0, cus = 0, dev = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCu, k, kIpcBlock, 0) != hipSuccess || perCu <= 0) return 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+        return 0;
+    }
+    const uint32_t v = static_cast<uint32_t>(perCu) * static_cast<uint32_t>(cus);
+    if (di < 32 && oi < 4) cache[di][oi][rhd ? 1 : 0].store(v, std::memory_order_relaxed);
+    return v;
 }
 
 HcclResult LaunchIpcCollective(const IpcArgs& a, uint32_t blocks, uint32_t worldRanks, HcclDataType dt,

@@ -115,6 +115,20 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
         if (aivOnly) return HCCL_E_NOT_SUPPORT;
         p.algo = HCCL_AMD_ALGO_AUTO;
     }
+    // RHD's bits from one launch of the one-sided kernel (AllReduce, power-of-two n). An IPC-only communicator asked for
+    // RHD takes it too, so it keeps RHD's order. Anything else runs the RHD schedule (or its own fallbacks).
+    if (p.algo == HCCL_AMD_ALGO_RHD && !c.transport->HasSendRecv()) p.algo = HCCL_AMD_ALGO_IPC_RHD;
+    if (p.algo == HCCL_AMD_ALGO_IPC_RHD) {
+        IpcPlan plan{};
+        if (opType == HCCL_AMD_OP_ALLREDUCE && IpcPlanRhd(c.nRanks, &plan) == HCCL_SUCCESS) {
+            const HcclResult r = RunIpcPlan(c, opType, plan, sendBuf, recvBuf, count, dt, op, root, stream);
+            if (r != HCCL_E_NOT_SUPPORT) {
+                c.lastAlgo = HCCL_AMD_ALGO_IPC_RHD;
+                return r;
+            }
+        }
+        p.algo = HCCL_AMD_ALGO_RHD;
+    }
     // an IPC-only communicator (bootstrap transport without send/recv) runs every reducing op on the IPC kernel in
     // the auto family, whatever schedule family was asked for
     if (!c.transport->HasSendRecv() && p.algo != HCCL_AMD_ALGO_IPC_TWOSHOT) p.algo = HCCL_AMD_ALGO_IPC;
@@ -411,7 +425,7 @@ HcclResult HcclAmdCommSetAlgo(HcclComm comm, int32_t algo)
 {
     Comm* c = AsComm(comm);
     if (c == nullptr) return HCCL_E_PTR;
-    if (algo < HCCL_AMD_ALGO_AUTO || algo > HCCL_AMD_ALGO_AIV_ONLY) return HCCL_E_PARA;
+    if (algo < HCCL_AMD_ALGO_AUTO || algo > HCCL_AMD_ALGO_IPC_RHD) return HCCL_E_PARA;
     c->algoOverride = algo;
     return HCCL_SUCCESS;
 }

@@ -665,8 +665,6 @@ std::vector<std::vector<uint32_t>> RhdTable(uint32_t n)
     return t;
 }
 
-namespace {
-
 // How many of the n-1 instances a call of `bytes` per rank runs. Every instance adds one message per rank and step
 // (6 steps at n = 8), and on the executor each message costs host time whatever its size: about 10 us per transport
 // group plus 1 us per message (RCCL self-loop programs, profiles/r02_rccl_selfloop_latency.jsonl). What an instance
@@ -680,6 +678,8 @@ uint32_t RhdInstances(uint32_t n, uint64_t bytes)
     while (r < most && uint64_t(r + 1) * (r + 1) * (1ull << 20) <= 2 * bytes) ++r;
     return r;
 }
+
+namespace {
 
 void AllReduceRhd(const ScheduleParams& p, Builder& b)
 {

@@ -51,6 +51,9 @@ std::vector<std::vector<uint32_t>> RingTable(uint32_t n);
 // The RHD instances for a power-of-two n (empty otherwise): per instance, the real rank of every virtual rank.
 std::vector<std::vector<uint32_t>> RhdTable(uint32_t n);
 
+// How many RHD instances (parts of the buffer) an AllReduce of `bytes` per rank runs (AllReduceRhd).
+uint32_t RhdInstances(uint32_t n, uint64_t bytes);
+
 // Returns HCCL_E_PARA for an invalid combination, HCCL_SUCCESS otherwise.
 int BuildSchedule(const ScheduleParams& p, Schedule* out);
 

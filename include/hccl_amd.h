@@ -114,8 +114,11 @@ typedef enum {
     HCCL_AMD_ALGO_AIV = 10,            /* the reference's AIV engine (HCCL_OP_EXPANSION_MODE=AIV): SelectAivAlgo's
                                           choice and orders on the one-sided kernel; what it does not match runs
                                           the auto (AICPU) selection, as the reference falls back */
-    HCCL_AMD_ALGO_AIV_ONLY = 11        /* the AIV engine with no fallback (OpExecuteConfig::AIV_ONLY): no 8 MiB x n
+    HCCL_AMD_ALGO_AIV_ONLY = 11,       /* the AIV engine with no fallback (OpExecuteConfig::AIV_ONLY): no 8 MiB x n
                                           bound, and what SelectAivAlgo does not match returns HCCL_E_NOT_SUPPORT */
+    HCCL_AMD_ALGO_IPC_RHD = 12         /* AllReduce, power-of-two n: HCCL_AMD_ALGO_RHD's bits from one one-shot launch
+                                          of the one-sided kernel (one barrier instead of 2 log2 n transport steps);
+                                          anything else, or no peer mappings, runs HCCL_AMD_ALGO_RHD */
 } HcclAmdAlgo;
 
 /* Variant of the reference's AIV engine a call takes (HcclAmdSelectAivAlgo). */

@@ -450,6 +450,30 @@ def test_c5_rhd_fp16_random_bit_exact(worlds, nbytes):
             assert O.equal_bits(O.FP16, outs[r], want_cf[r]), ("vs closed form", r)
 
 
+@pytest.mark.parametrize("n,dtype,op,count", [
+    (8, O.FP16, O.SUM, 512), (8, O.FP16, O.SUM, 32 << 10), (8, O.FP16, O.SUM, 1 << 19),
+    (8, O.FP16, O.SUM, (1 << 20) + 77),  # 2 MiB: two RHD instances, ragged chunks
+    (8, O.FP16, O.SUM, 8 << 20),  # 16 MiB: five instances
+    (8, O.FP16, O.SUM, 32 << 20),  # 64 MiB: all seven instances, four staging rounds
+    (4, O.FP32, O.SUM, 1000003), (2, O.BFP16, O.SUM, 70001), (8, O.FP32, O.MAX, 300007), (4, O.FP32, O.MIN, 4099),
+    (8, O.INT32, O.PROD, 9999), (8, O.FP32, O.SUM, (3 << 20) + 5),
+])
+def test_ipc_rhd_is_rhd_bit_exact(worlds, monkeypatch, n, dtype, op, count):
+    """HCCL_AMD_ALGO_IPC_RHD: RHD's bits (the RHD schedule's IR replayed by the oracle) from one one-shot launch of the
+    one-sided kernel, across one to seven RHD instances, ragged chunks, several staging rounds, the src/dst roles of
+    MAX/MIN on ties and NaN (edge operands)."""
+    monkeypatch.setenv("HCCL_AMD_IPC_TIMEOUT_MS", "20000")  # a stuck barrier fails the test, never hangs the box
+    comms = worlds(n)
+    edge = op in (O.MAX, O.MIN)
+    xs = [O.random_operands(dtype, count, seed=950 + r, edge=edge) for r in range(n)]
+    used, outs = collective(comms, AR, H.Algo.IPC_RHD, dtype, op, xs, count)
+    assert used == H.Algo.IPC_RHD
+    assert ipc_status(comms[0]) & 1 == 0
+    want = oracle_replay(AR, R.ALGO_RHD, n, count, dtype, op, xs, 0, 0)
+    for r in range(n):
+        assert O.equal_bits(dtype, outs[r], want[r]), r
+
+
 def aiv_expected(op_type, dtype, op, xs, count, n, core_limit):
     es = np.dtype(O.NP_STORAGE[dtype]).itemsize
     variant, group = R.aiv_select(op_type, n, count, es, dtype in (O.UINT64, O.FP64), op == O.PROD,

@@ -1,0 +1,69 @@
+"""The identity the one-sided RHD kernel (HCCL_AMD_ALGO_IPC_RHD, ipc_kernels.hip RhdFold) rests on — host only.
+
+The RHD AllReduce (schedule.cc AllReduceRhd) gives element e of part j, virtual chunk v the value the classic recursive
+halving builds on virtual ranks (each step: dst = partner (op) mine). RhdFold computes it from all n inputs at once as
+the O4 tree over the operands of virtual ranks v ^ q, q = 0 .. n-1 (tests/sched_ref.py tree_fold), locating (j, v)
+with the kernel's own arithmetic (Chunk(): ceil splits rounded up to 128 B). Checked bit-exact against the schedule's
+closed form (sched_ref.allreduce_rhd), which tests/test_schedules.py pins against the IR replay.
+"""
+import numpy as np
+import pytest
+
+import hccl_amd as H
+from oracle import oracle as O
+from tests import sched_ref as R
+
+
+def rhd_by_tree(dtype, op, xs):
+    """RhdFold's restatement: per (part, chunk) segment, the O4 tree over relabelled operands."""
+    n = len(xs)
+    count = xs[0].size
+    es = xs[0].itemsize
+    align = max(1, 128 // es)
+    parts = min(len(H.rhd_table(n)), R.rhd_instances(n, count * es))
+    table = H.rhd_table(n)[:parts]
+    stride = max(1, -(-(-(-count // parts)) // align) * align)
+    out = np.empty_like(xs[0])
+    g = 0
+    while g < count:
+        j = g // stride
+        pb = j * stride
+        plen = min(count, pb + stride) - pb
+        sc = -(-(-(-plen // n)) // align) * align
+        v = (g - pb) // sc
+        end = min(count, pb + min(plen, (v + 1) * sc))
+        real = table[j]
+        out[g:end] = R.tree_fold(dtype, op, [xs[real[v ^ q]][g:end] for q in range(n)])
+        g = end
+    return out
+
+
+@pytest.mark.parametrize("n", [2, 4, 8, 16])
+@pytest.mark.parametrize("nbytes", [2, 1000, 64 << 10, 1 << 20, (2 << 20) + 6, 9 << 20])
+def test_tree_over_relabelled_ranks_is_rhd(n, nbytes):
+    dtype = O.FP16
+    count = nbytes // 2
+    if n == 16 and nbytes > (2 << 20) + 6:
+        pytest.skip("covered at 8 ranks; the closed form is slow at 16 x 9 MiB")
+    xs = [O.random_operands(dtype, count, seed=70 + r, edge=False) for r in range(n)]
+    want = R.allreduce_rhd(dtype, O.SUM, xs)[0]
+    got = rhd_by_tree(dtype, O.SUM, xs)
+    assert O.equal_bits(dtype, got, want)
+
+
+@pytest.mark.parametrize("dtype,op", [(O.FP32, O.MAX), (O.FP32, O.MIN), (O.FP32, O.SUM), (O.BFP16, O.SUM),
+                                      (O.INT32, O.PROD)])
+def test_identity_keeps_src_dst_roles(dtype, op):
+    """MAX/MIN return src on ties and NaN: the tree must keep the schedule's (partner = src, mine = dst) roles.
+    Edge operands at shared positions make the roles visible."""
+    n, count = 8, 30011
+    rng = np.random.default_rng(5)
+    xs = [O.random_operands(dtype, count, seed=90 + r, edge=False) for r in range(n)]
+    edges = O.edge_values(dtype)
+    pos = rng.choice(count, size=len(edges) * n, replace=False).reshape(n, -1)
+    for r in range(n):
+        for k in range(n):  # every rank gets every edge value at rank-rotated positions: ties across ranks
+            xs[r][pos[k]] = np.roll(edges, r + k)
+    want = R.allreduce_rhd(dtype, op, xs)[0]
+    got = rhd_by_tree(dtype, op, xs)
+    assert O.equal_bits(dtype, got, want)
