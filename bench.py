@@ -481,9 +481,10 @@ def bench_c4(comm, send, recv, world) -> dict:
 
 def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
     """C5: AllReduce fp16 SUM, 1 KiB .. 4 GiB: latency at small sizes, busbw at large. Each size runs the RHD schedule
-    (the config's algorithm), the auto selection (what the reference would run: one-shot / two-shot / MeshChunk) and,
-    up to 256 MiB, the one-sided IPC kernel in the same order family (one launch per call: the latency end). The RCCL
-    rows of every size run before the IPC rows: an IPC barrier timeout fails the communicator."""
+    (the config's algorithm), the auto selection (what the reference would run: one-shot / two-shot / MeshChunk),
+    up to 256 MiB the one-sided IPC kernel in the same order family (one launch per call: the latency end), and up to
+    64 MiB IPC_RHD (the RHD schedule's bits from one one-sided launch, compared with them). The RCCL rows of every size
+    run before the IPC rows: an IPC barrier timeout fails the communicator."""
     s = torch.cuda.current_stream()
     sizes = []
     nbytes = 1 << 10
@@ -492,12 +493,15 @@ def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
         nbytes *= 2
     rows = {b: {"bytes": b} for b in sizes}
     f = 2 * (world - 1) / world
-    key = {H.Algo.RHD: "rhd", H.Algo.AUTO: "auto", H.Algo.IPC: "ipc"}
+    key = {H.Algo.RHD: "rhd", H.Algo.AUTO: "auto", H.Algo.IPC: "ipc", H.Algo.IPC_RHD: "ipc_rhd"}
+    rhd_digest = {}
     try:
-        for algo in (H.Algo.RHD, H.Algo.AUTO, H.Algo.IPC):
+        for algo in (H.Algo.RHD, H.Algo.AUTO, H.Algo.IPC, H.Algo.IPC_RHD):
             comm.set_algo(algo)
             for nbytes in sizes:
                 if algo == H.Algo.IPC and nbytes > (256 << 20):
+                    break
+                if algo == H.Algo.IPC_RHD and nbytes > (64 << 20):  # one-shot: (n-1) x S arrive at every rank
                     break
                 row = rows[nbytes]
                 a = send.view(torch.float16)[: nbytes // 2]
@@ -510,6 +514,13 @@ def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
                     continue
                 row[f"{key[algo]}_us"] = round(t * 1e6, 1)
                 row[f"{key[algo]}_busbw_GBps"] = round(nbytes / t / 1e9 * f, 2)
+                # RHD's bits from the one-sided kernel: the IPC_RHD output must equal the RHD schedule's, bit for bit
+                sample = b.view(torch.int16)[:: 1 << 10].clone()
+                if algo == H.Algo.RHD:
+                    rhd_digest[nbytes] = sample
+                elif algo == H.Algo.IPC_RHD and nbytes in rhd_digest:
+                    row["ipc_rhd_ran"] = H.Algo(comm.last_algo).name
+                    row["ipc_rhd_matches_rhd"] = bool(torch.equal(sample, rhd_digest[nbytes]))
                 if algo == H.Algo.AUTO:
                     row["auto_algo"] = H.Algo(comm.last_algo).name
                 if algo == H.Algo.IPC:

@@ -1,8 +1,9 @@
 """Per-call latency of the IPC AllReduce, eager vs captured in a HIP graph (K calls per graph, one replay), in rank
 mode on the one-GPU box (n processes share the GPU over the IPC-only communicator; not an xGMI measurement).
   python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29541 \\
-      tools/graph_latency.py > gpurun_out/graph_latency.jsonl
+      tools/graph_latency.py [--algo IPC|IPC_RHD|IPC_TWOSHOT] > gpurun_out/graph_latency.jsonl
 """
+import argparse
 import json
 import os
 import sys
@@ -17,6 +18,10 @@ K = 100
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--algo", default="IPC")
+    ap.add_argument("--sizes", default="1024,65536,1048576")
+    args = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     os.environ.setdefault("HCCL_AMD_IPC_TIMEOUT_MS", "10000")
     torch.cuda.set_device(0)
@@ -28,9 +33,9 @@ def main():
         return out
 
     comm = H.comm_init_host_exchange(world, rank, all_gather)
-    comm.set_algo(H.Algo.IPC)
+    comm.set_algo(H.Algo[args.algo])
     s = torch.cuda.Stream()
-    for nbytes in (1 << 10, 64 << 10, 1 << 20):
+    for nbytes in [int(v) for v in args.sizes.split(",")]:
         x = torch.ones(nbytes // 2, dtype=torch.float16, device="cuda")
         y = torch.empty_like(x)
         for _ in range(10):
@@ -65,7 +70,7 @@ def main():
         t = torch.tensor([eager, graph])
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         if rank == 0:
-            print(json.dumps({"n": world, "bytes": nbytes, "eager_us": round(float(t[0]) * 1e3, 2),
+            print(json.dumps({"algo": H.Algo(comm.last_algo).name, "n": world, "bytes": nbytes, "eager_us": round(float(t[0]) * 1e3, 2),
                               "graph_us": round(float(t[1]) * 1e3, 2), "ok": ok,
                               "ipc_status_bit0": comm.ipc_status() & 1}), flush=True)
         del g
