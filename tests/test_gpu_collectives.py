@@ -299,6 +299,34 @@ def test_ipc_allgather(worlds, dtype, n, count, inplace):
             c.set_algo(0)
 
 
+@pytest.mark.parametrize("dtype,algo", [(O.INT8, 7), (O.INT8, 9), (O.FP16, int(H.Algo.IPC_RHD))])
+def test_ipc_blocks_capped_at_resident(worlds, monkeypatch, dtype, algo):
+    """Co-residency guard (ipc.cc RunIpcPlan, IpcResidentBlocks): the int8 IPC kernel uses 191 VGPRs, so the GPU holds
+    2 of its workgroups per CU; an 8-rank loopback world asking for 256 blocks per rank (2,048) would wait forever
+    for blocks that cannot start. The launch is capped at the resident count, and the result is exact."""
+    monkeypatch.setenv("HCCL_AMD_IPC_TIMEOUT_MS", "20000")  # a stuck barrier fails the test, never hangs the box
+    n, count = 8, (24 << 20) + 3
+    comms = worlds(n)
+    xs = [O.random_operands(dtype, count, seed=990 + r, edge=False, small_ints=True) for r in range(n)]
+    for c in comms:
+        c.set_ipc_blocks(256)
+    try:
+        used, outs = collective(comms, AR, algo, dtype, O.SUM, xs, count)
+    finally:
+        for c in comms:
+            c.set_ipc_blocks(0)
+    assert used == algo
+    assert ipc_status(comms[0]) & 1 == 0
+    if dtype == O.INT8:
+        want = R.fold(dtype, O.SUM, xs)  # wrap-around integer sums: every order gives these bits
+        for r in range(n):
+            assert O.equal_bits(dtype, outs[r], want), r
+    else:
+        want = oracle_replay(AR, R.ALGO_RHD, n, count, dtype, O.SUM, xs, 0, 0)
+        for r in range(n):
+            assert O.equal_bits(dtype, outs[r], want[r]), r
+
+
 @pytest.mark.parametrize("shift", [(1, 1), (0, 3), (2, 0)])
 def test_ipc_unaligned_buffers(worlds, shift):
     """Buffers not 16-B aligned still run the IPC kernel (element-wise accesses to the user buffers; the path choice
