@@ -292,12 +292,19 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
 {
     if (singleStream) return ExecuteSingleStream(c, ops, bufs, dt, op, user);
     const uint64_t es = DataTypeSize(dt);
-    hipStream_t streams[2] = {c.commStream, c.reduceStream};
+    // Under stream capture the transport groups go on the capturing stream itself and only the folds on a forked
+    // stream: an RCCL group captured on a stream joined to the capture (rather than its origin) brought down graph
+    // instantiation (hipStreamEndCapture segfaulted; tools/rccl_capture_probe.py), while the same group on the origin
+    // stream captures and replays. The plan and its waits are the same; only the link stream's identity changes.
+    hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
+    HIP_CHK(hipStreamIsCapturing(user, &capture));
+    const bool captured = capture != hipStreamCaptureStatusNone;
+    hipStream_t streams[2] = {captured ? user : c.commStream, c.reduceStream};
     c.nextEvent = 0;
     hipEvent_t start;
     HCCL_CHK(c.NextEvent(&start));
     HIP_CHK(hipEventRecord(start, user));
-    HIP_CHK(hipStreamWaitEvent(c.commStream, start, 0));
+    if (!captured) HIP_CHK(hipStreamWaitEvent(c.commStream, start, 0));
     HIP_CHK(hipStreamWaitEvent(c.reduceStream, start, 0));
 
     auto addr = [&](int32_t buf, uint64_t off) -> uintptr_t {
@@ -343,7 +350,8 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
     }
 
     for (int s = 0; s < 2; ++s) {
-        if (!used[s]) continue;
+        // an unused stream needs no join, except under capture, where every stream forked into it must rejoin
+        if ((!used[s] && !captured) || streams[s] == user) continue;
         hipEvent_t end;
         HCCL_CHK(c.NextEvent(&end));
         HIP_CHK(hipEventRecord(end, streams[s]));

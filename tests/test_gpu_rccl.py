@@ -7,6 +7,7 @@ RCCL's reason (the 8-GPU path is exercised by bench.py on the driver's node). Th
 """
 import multiprocessing as mp
 import os
+import time
 import traceback
 
 import numpy as np
@@ -305,3 +306,85 @@ def test_rccl_runs_the_schedules_over_a_self_loop():
     bad = [r for r in results if r[2] not in ("ok", "unpaired")]
     assert not bad, bad
     assert sum(r[2] == "ok" for r in results) >= 2 * len(SELF_LOOP_CASES), results
+
+
+CAPTURE_CASES = [SELF_LOOP_CASES[i] for i in (0, 4, 5, 6, 7, 11, 13)]
+
+
+def _capture_worker(q):
+    """Each program captured once into a HIP graph (torch.cuda.graph) per executor mode, then replayed on two fresh
+    inputs; every replay's output bit-exact against the oracle replaying the program on that input."""
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        import torch
+        import hccl_amd as H
+        from oracle import oracle as O
+        from tests._util import to_device, to_host
+        torch.cuda.set_device(0)
+        comm = H.comm_init_root_info(1, H.get_root_info(), 0)
+        s = torch.cuda.Stream()
+        results = []
+        dtype, op = O.FP32, O.SUM
+        for k, (op_type, algo, n, rank, count) in enumerate(CAPTURE_CASES):
+            prog = self_looped(op_type, algo, n, rank, count, dtype)
+            if prog is None:
+                results.append((k, "unpaired"))
+                continue
+            arr, nops, scratch = prog
+            in_len = count * n if op_type == 1 else count
+            out_len = count * n if op_type == 3 else count
+            st = O.NP_STORAGE[dtype]
+            for single in (False, True):
+                xd = to_device(dtype, O.random_operands(dtype, in_len, seed=5000 + k, edge=False))
+                od = to_device(dtype, np.zeros(out_len, st))
+                comm.execute(arr, nops, xd, od, op, single, s, dtype=dtype)  # eager first (RCCL connections)
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    comm.execute(arr, nops, xd, od, op, single, torch.cuda.current_stream(), dtype=dtype)
+                for rep in range(2):
+                    x = O.random_operands(dtype, in_len, seed=6000 + 10 * k + rep, edge=False)
+                    bufs = [[x.copy(), np.zeros(out_len, st), np.zeros(max(scratch, 1), st)]]
+                    assert O.replay(1, dtype, op, [(arr, nops)], bufs) == 0
+                    xd.copy_(to_device(dtype, x))
+                    od.zero_()
+                    torch.cuda.synchronize()
+                    g.replay()
+                    torch.cuda.synchronize()
+                    same = O.equal_bits(dtype, to_host(dtype, od), bufs[0][1])
+                    results.append((k, single, rep, "ok" if same else "mismatch"))
+                del g
+        comm.destroy()
+        q.put(("ok", results))
+    except Exception as e:  # noqa: BLE001
+        q.put(("err", f"{type(e).__name__}: {e}\n{traceback.format_exc()}"))
+
+
+def test_rccl_path_graph_capture_replays():
+    """HIP-graph capture of the RCCL path (executor + RCCL send/recv groups + folds): the schedules' programs over a
+    one-rank self loop, captured in both executor modes and replayed on fresh inputs, bit-exact. Under capture the
+    transport groups run on the capturing stream itself: RCCL groups captured on a forked stream brought down graph
+    instantiation (hipStreamEndCapture segfault, reproduced with RCCL alone by tools/rccl_capture_probe.py)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_capture_worker, args=(q,))
+    p.start()
+    got = None
+    try:
+        deadline = time.time() + 300
+        while got is None and time.time() < deadline:
+            try:
+                got = q.get(timeout=5)
+            except Exception:  # noqa: BLE001  (queue.Empty)
+                if not p.is_alive():
+                    break
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert got is not None, f"capture worker died (exit code {p.exitcode})"
+    status, results = got
+    assert status == "ok", results
+    assert not [r for r in results if r[-1] not in ("ok", "unpaired")], results
+    assert sum(r[-1] == "ok" for r in results) >= 8, results
