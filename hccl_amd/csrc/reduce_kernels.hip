@@ -549,10 +549,16 @@ hipError_t RunN(void* out, const void* const* srcs, uint32_t n, uint64_t count, 
         }
         switch (cfg.unroll * 4 + cfg.nt) {
             case 4 + 0: return RunNVariant<E, OP, 1, 0>(out, pk, int(n), nvec, edges, grid, stream);
+            case 4 + 1: return RunNVariant<E, OP, 1, 1>(out, pk, int(n), nvec, edges, grid, stream);
+            case 4 + 2: return RunNVariant<E, OP, 1, 2>(out, pk, int(n), nvec, edges, grid, stream);
             case 4 + 3: return RunNVariant<E, OP, 1, 3>(out, pk, int(n), nvec, edges, grid, stream);
             case 8 + 0: return RunNVariant<E, OP, 2, 0>(out, pk, int(n), nvec, edges, grid, stream);
+            case 8 + 1: return RunNVariant<E, OP, 2, 1>(out, pk, int(n), nvec, edges, grid, stream);
+            case 8 + 2: return RunNVariant<E, OP, 2, 2>(out, pk, int(n), nvec, edges, grid, stream);
             case 8 + 3: return RunNVariant<E, OP, 2, 3>(out, pk, int(n), nvec, edges, grid, stream);
             case 16 + 0: return RunNVariant<E, OP, 4, 0>(out, pk, int(n), nvec, edges, grid, stream);
+            case 16 + 1: return RunNVariant<E, OP, 4, 1>(out, pk, int(n), nvec, edges, grid, stream);
+            case 16 + 2: return RunNVariant<E, OP, 4, 2>(out, pk, int(n), nvec, edges, grid, stream);
             case 16 + 3: return RunNVariant<E, OP, 4, 3>(out, pk, int(n), nvec, edges, grid, stream);
             default: return hipErrorInvalidValue;
         }

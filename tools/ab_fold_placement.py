@@ -14,8 +14,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import hccl_amd as H  # noqa: E402
 
 GIB = 1 << 30
-# bpc x unroll [x fold mode]: HcclAmdSetFoldMode (0 default, 1 serial, 2 prefetch, 3 every operand first)
-SHAPES = [tuple(int(v) for v in (x + "x0").split("x")[:3]) if x.count("x") == 1 else tuple(int(v) for v in x.split("x"))
+# bpc x unroll [x fold mode [x cache policy]]: HcclAmdSetFoldMode (0 default, 1 serial, 2 prefetch, 3 every operand
+# first); HcclAmdSetReduceLaunch's cachePolicy (0 default, 1 plain, 2 nt loads, 3 nt stores, 4 nt loads + stores)
+SHAPES = [tuple(int(v) for v in (x + "x0x0x0").split("x")[:4])
           for x in os.environ.get("AB_SHAPES", "2x2,2x4,4x2,2x1").split(",")]
 NS = tuple(int(x) for x in os.environ.get("AB_NS", "8").split(","))
 TRIALS = int(os.environ.get("AB_TRIALS", "12"))
@@ -47,23 +48,23 @@ def main():
             order = SHAPES[:]
             rng.shuffle(order)
             ref = None
-            for bpc, u, fm in order:
-                H.set_reduce_launch(bpc, u, 0)
+            for bpc, u, fm, pol in order:
+                H.set_reduce_launch(bpc, u, pol)
                 H.set_fold_mode(fm)
-                res.setdefault((n, bpc, u, fm), []).append(timeit(lambda: H.local_reduce_n(out, ins)))
+                res.setdefault((n, bpc, u, fm, pol), []).append(timeit(lambda: H.local_reduce_n(out, ins)))
                 # every shape and mode folds in the same order: the outputs must be identical bits
                 digest = out.view(torch.int32)[:: 1 << 10].clone()
                 if ref is None:
                     ref = digest
                 elif not torch.equal(ref, digest):
-                    mismatch.add((n, bpc, u, fm))
+                    mismatch.add((n, bpc, u, fm, pol))
     H.set_reduce_launch(0, 0, 0)
     H.set_fold_mode(0)
-    for (n, bpc, u, fm), ts in sorted(res.items()):
+    for (n, bpc, u, fm, pol), ts in sorted(res.items()):
         ts = sorted(ts)
         med = ts[len(ts) // 2]
-        print(json.dumps({"n": n, "blocks_per_cu": bpc, "unroll": u, "fold_mode": fm,
-                          "bits_match": (n, bpc, u, fm) not in mismatch, "median_us": round(med * 1e6, 1),
+        print(json.dumps({"n": n, "blocks_per_cu": bpc, "unroll": u, "fold_mode": fm, "cache_policy": pol,
+                          "bits_match": (n, bpc, u, fm, pol) not in mismatch, "median_us": round(med * 1e6, 1),
                           "min_us": round(ts[0] * 1e6, 1), "max_us": round(ts[-1] * 1e6, 1),
                           "mean_us": round(sum(ts) / len(ts) * 1e6, 1),
                           "median_GBps": round((n + 1) * GIB / med / 1e9, 1)}), flush=True)
