@@ -18,7 +18,9 @@ The mapping is the one ProcessGroupHCCL makes:
 * ``reduce_scatter_tensor`` / ``reduce_scatter`` -> HcclReduceScatter (input = rankSize blocks of the output's size,
   reduce_scatter_op.cc:158-159; the list form is packed into one buffer first);
 * ``all_gather_into_tensor`` / ``all_gather`` -> HcclAllGather;
-* ``barrier`` -> a one-element HcclAllReduce, then the host waits for it.
+* ``barrier`` -> a one-element HcclAllReduce, then the host waits for it;
+* ``broadcast`` -> HcclAllGather of the tensor's bytes, keeping the root's block (for DDP's start-up sync; the reduce
+  path has no broadcast of its own).
 
 Reduce ops are HCCL's four (SUM, PRODUCT, MAX, MIN; hccl_types.h HcclReduceOp); AVG, PREMUL_SUM and the bitwise ops
 have no HCCL counterpart and raise ValueError, as does any dtype HCCL does not reduce (the entry answers
@@ -89,14 +91,19 @@ class StoreAllGather:
 
 
 class _Work(dist._Work):
-    """Completion of one enqueued collective: an event recorded on the stream it was enqueued on."""
+    """Completion of one enqueued collective: an event recorded on the stream it was enqueued on, and a CUDA-aware
+    future completed on that stream (its consumers' streams wait for it, as with the NCCL backend's futures; DDP's
+    gradient hooks chain on it)."""
 
-    def __init__(self, result: List[torch.Tensor], event: Optional[torch.cuda.Event]):
+    def __init__(self, result: List[torch.Tensor], event: Optional[torch.cuda.Event],
+                 future: Optional[torch.futures.Future] = None):
         super().__init__()
         self._result = result
         self._event = event
-        self._future = torch.futures.Future()
-        self._future.set_result(result)
+        if future is None:
+            future = torch.futures.Future()
+            future.set_result(result)
+        self._future = future
 
     def wait(self, timeout: Optional[datetime.timedelta] = None) -> bool:
         if self._event is not None:
@@ -179,7 +186,10 @@ class ProcessGroupHCCL(dist.ProcessGroup):
                 t.record_stream(side)
             ev = torch.cuda.Event()
             ev.record(side)
-        return _Work(result, ev)
+            fut = torch.futures.Future(devices=[torch.device("cuda", torch.cuda.current_device())])
+            with torch.cuda.stream(side):
+                fut.set_result(result)  # marks the result ready on the group's stream
+        return _Work(result, ev, fut)
 
     # ------------------------------------------------------------------------------------------------ collectives
     def allreduce(self, tensors: List[torch.Tensor], opts) -> _Work:
@@ -236,6 +246,24 @@ class ProcessGroupHCCL(dist.ProcessGroup):
                     o.copy_(flat[r * m:(r + 1) * m].view_as(o))
 
         return self._run(outputs[0], inp.device, gather_and_unpack, [inp, flat] + list(outputs[0]))
+
+    def broadcast(self, tensors: List[torch.Tensor], opts) -> _Work:
+        """Broadcast from opts.rootRank, built on HcclAllGather of the tensor's bytes (the reduce path has no
+        broadcast of its own; DDP needs one at construction to sync module states): every rank gathers every rank's
+        bytes and keeps the root's block, so the root's bits arrive unchanged whatever the dtype."""
+        t = tensors[opts.rootTensor]
+        self._check(t, "broadcast tensor")
+        root = opts.rootRank
+        raw = t.view(torch.uint8)
+        m = raw.numel()
+        flat = torch.empty(m * self.size(), dtype=torch.uint8, device=t.device)
+
+        def gather_root(c, s):
+            c.all_gather(raw.reshape(-1), flat, s)
+            with torch.cuda.stream(s):
+                raw.reshape(-1).copy_(flat[root * m:(root + 1) * m])
+
+        return self._run(tensors, t.device, gather_root, [t, flat])
 
     def barrier(self, opts) -> _Work:
         dev = torch.device("cuda", self._device if self._device is not None else torch.cuda.current_device())

@@ -139,3 +139,84 @@ def test_reference_pytorch_sample(n, transport):
         msg, res = got[r]
         assert msg == "ok", f"rank {r}: {msg}"
         assert all(res.values()), f"rank {r}: {res}"
+
+
+def _ddp_main(rank, n, port, q):
+    os.environ["HCCL_AMD_IPC_TIMEOUT_MS"] = "20000"
+    os.environ["HCCL_AMD_PG_TRANSPORT"] = "ipc"
+    os.makedirs("gpurun_out", exist_ok=True)
+    progress = open(f"gpurun_out/process_group_ddp_r{rank}.log", "w", buffering=1)
+    try:
+        import torch
+        import torch.distributed as dist
+        from torch.nn.parallel import DistributedDataParallel as DDP
+        import hccl_amd.process_group  # noqa: F401
+
+        torch.cuda.set_device(0)
+        dist.init_process_group(backend="hccl", rank=rank, world_size=n, init_method=f"tcp://127.0.0.1:{port}",
+                                timeout=datetime.timedelta(seconds=120))
+
+        def make(seed):
+            torch.manual_seed(seed)
+            return torch.nn.Sequential(torch.nn.Linear(512, 256), torch.nn.ReLU(), torch.nn.Linear(256, 8)).cuda()
+
+        checks = {}
+        model = make(1000 + rank)  # different on every rank: DDP's start-up broadcast must make them rank 0's
+        ddp = DDP(model, device_ids=[0], bucket_cap_mb=1)  # several gradient buckets
+        ref = make(1000)
+        checks["broadcast_bits"] = all(torch.equal(a, b) for a, b in zip(ddp.module.parameters(), ref.parameters()))
+        opt = torch.optim.SGD(ddp.parameters(), lr=0.1)
+        ref_opt = torch.optim.SGD(ref.parameters(), lr=0.1)
+        for step in range(3):
+            xs = [torch.randn(64, 512, generator=torch.Generator().manual_seed(50 * step + r)).cuda() for r in range(n)]
+            opt.zero_grad()
+            ddp(xs[rank]).square().mean().backward()
+            # reference: the mean of every rank's local gradient, on an undistributed copy of the model
+            ref_opt.zero_grad()
+            for r in range(n):
+                (ref(xs[r]).square().mean() / n).backward()
+            checks[f"grads_close_{step}"] = all(
+                torch.allclose(a.grad, b.grad, rtol=1e-4, atol=1e-6) for a, b in zip(ddp.parameters(), ref.parameters()))
+            opt.step()
+            ref_opt.step()
+        # every rank holds the same parameters, bit for bit, after the steps
+        flat = torch.cat([p.detach().reshape(-1) for p in ddp.parameters()])
+        everyone = torch.empty(n * flat.numel(), device="cuda")
+        dist.all_gather_into_tensor(everyone, flat)
+        checks["params_identical"] = all(torch.equal(everyone[r * flat.numel():(r + 1) * flat.numel()], flat)
+                                         for r in range(n))
+        dist.barrier()
+        dist.destroy_process_group()
+        progress.write(f"checks {checks}\n")
+        q.put((rank, "ok", checks))
+    except Exception:  # noqa: BLE001
+        progress.write(traceback.format_exc())
+        q.put((rank, traceback.format_exc(), None))
+        time.sleep(10)
+
+
+def test_ddp_training_steps_over_the_backend():
+    """DistributedDataParallel on the "hccl" backend (2 processes sharing the GPU, IPC communicator): its start-up
+    broadcast makes every replica rank 0's bit for bit, three SGD steps average the gradients through HcclAllReduce on
+    the backend's CUDA-aware futures (several buckets), and the replicas stay identical."""
+    n = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_main, args=(r, n, port, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    try:
+        got = {}
+        for _ in procs:
+            rank, msg, res = q.get(timeout=240)
+            got[rank] = (msg, res)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(n):
+        msg, res = got[r]
+        assert msg == "ok", f"rank {r}: {msg}"
+        assert all(res.values()), f"rank {r}: {res}"
