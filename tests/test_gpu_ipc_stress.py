@@ -1,7 +1,7 @@
 """Randomised sequence of IPC collectives in rank mode (n processes sharing the GPU, peers mapped through IPC
 handles): every kind (AllReduce one-shot / two-shot / MeshChunk, ReduceScatter, Reduce, AllGather), counts from 1
 element to several staging rounds, block counts changing from call to call (default or forced 1..256), order
-families fixed (IPC_TWOSHOT) or the auto family (IPC). This drives the barrier epochs, the alternating slot areas of
+families fixed (IPC_TWOSHOT), the auto family (IPC) or RHD's order (IPC_RHD). This drives the barrier epochs, the alternating slot areas of
 the single-barrier kinds and the per-launch windows through mixes no hand-written case lists.
 
 Data are small integers in fp32, so every association order gives the exact sum and the expected output is a
@@ -40,7 +40,7 @@ def _plan(n):
         count = rng.choice(sizes)
         if kind in (RS, AG) and count > (3 << 20):
             count //= n  # keep n x count within a few tens of MiB
-        algo = rng.choice((7, 9, 9))
+        algo = rng.choice((7, 9, 9, 12))  # 12 = IPC_RHD (AllReduce; the other kinds take the auto family)
         blocks = rng.choice((0, 0, 0, 1, 16, 64, 256, rng.randint(1, 256)))
         plan.append((kind, count, algo, blocks, rng.randrange(n)))
     return plan
