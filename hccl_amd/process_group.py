@@ -36,7 +36,8 @@ form on a one-GPU box.
 Streams are the NCCL backend's: each group owns one stream per device (the HCCL entries reject the null stream,
 as the reference's do, and torch's default stream is the null stream). A collective waits there for the caller's
 current stream, runs, and marks its tensors as used on that stream for the caching allocator; ``wait()`` makes the
-then-current stream wait for it. The host never blocks except in ``barrier``.
+then-current stream wait for it. The host never blocks except in ``barrier``. Under HIP-graph capture the call goes
+on the capturing stream itself.
 """
 from __future__ import annotations
 
@@ -177,6 +178,15 @@ class ProcessGroupHCCL(dist.ProcessGroup):
     def _run(self, result: List[torch.Tensor], device: torch.device, fn, used: List[torch.Tensor]) -> _Work:
         comm = self.comm(device)
         with torch.cuda.device(device):
+            if torch.cuda.is_current_stream_capturing():
+                # HIP-graph capture: the call goes on the capturing stream itself. Transport groups captured on a
+                # stream forked from the capture crash graph instantiation on this ROCm, and the graph
+                # orders everything after it anyway.
+                cur = torch.cuda.current_stream()
+                fn(comm, cur)
+                fut = torch.futures.Future(devices=[torch.device("cuda", torch.cuda.current_device())])
+                fut.set_result(result)
+                return _Work(result, None, fut)
             if self._stream is None:
                 self._stream = torch.cuda.Stream()
             side = self._stream

@@ -101,6 +101,20 @@ def _rank_main(rank, n, port, transport, q):
             work = dist.all_reduce(z, async_op=True)
         work.wait()
         checks["async_wait"] = bool(torch.all(z == n).item())
+        # --- captured in a HIP graph (after the communicator's first call, its set-up) and replayed twice
+        if n > 1:
+            gx = torch.zeros(4099, device="cuda")
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                dist.all_reduce(gx)
+            replays = []
+            for rep in range(2):
+                gx.fill_(float(rank + 1 + rep))
+                graph.replay()
+                torch.cuda.synchronize()
+                replays.append(bool(torch.all(gx == sum(r + 1 + rep for r in range(n))).item()))
+            checks["graph_replay"] = all(replays)
         # --- unsupported op and dtype surface as errors, not wrong data
         try:
             dist.all_reduce(torch.ones(4, device="cuda"), op=dist.ReduceOp.AVG)
