@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -70,14 +71,23 @@ struct Shared {
     char slot[kMaxRanks][kSlot];
 };
 
+// Cross-process barrier over the shared page. A rank that died never arrives: the others give up after a bound
+// instead of spinning forever, and the parent reports the failure.
 void Barrier(Shared* s, int n)
 {
     const uint32_t gen = s->generation.load();
     if (s->arrived.fetch_add(1) + 1 == uint32_t(n)) {
         s->arrived.store(0);
         s->generation.fetch_add(1);
-    } else {
-        while (s->generation.load() == gen) std::this_thread::yield();
+        return;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    while (s->generation.load() == gen) {
+        std::this_thread::yield();
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(600)) {
+            std::fprintf(stderr, "hccl_test: a rank did not reach the barrier within 600 s\n");
+            _exit(3);
+        }
     }
 }
 
