@@ -485,6 +485,7 @@ def test_c5_rhd_fp16_random_bit_exact(worlds, nbytes):
     (8, O.FP16, O.SUM, 32 << 20),  # 64 MiB: all seven instances, four staging rounds
     (4, O.FP32, O.SUM, 1000003), (2, O.BFP16, O.SUM, 70001), (8, O.FP32, O.MAX, 300007), (4, O.FP32, O.MIN, 4099),
     (8, O.INT32, O.PROD, 9999), (8, O.FP32, O.SUM, (3 << 20) + 5),
+    (8, O.FP32, O.SUM, 7), (4, O.FP16, O.SUM, 1),  # fewer elements than ranks: everything in chunk 0
 ])
 def test_ipc_rhd_is_rhd_bit_exact(worlds, monkeypatch, n, dtype, op, count):
     """HCCL_AMD_ALGO_IPC_RHD: RHD's bits (the RHD schedule's IR replayed by the oracle) from one one-shot launch of the
@@ -500,6 +501,20 @@ def test_ipc_rhd_is_rhd_bit_exact(worlds, monkeypatch, n, dtype, op, count):
     want = oracle_replay(AR, R.ALGO_RHD, n, count, dtype, op, xs, 0, 0)
     for r in range(n):
         assert O.equal_bits(dtype, outs[r], want[r]), r
+
+
+@pytest.mark.parametrize("n,count", [(8, 300007), (4, (9 << 20) + 1)])
+def test_ipc_rhd_in_place(worlds, monkeypatch, n, count):
+    """IPC_RHD with sendBuf == recvBuf: every rank pushes a round's elements before it folds over them, so in-place
+    keeps RHD's bits (one and several staging rounds)."""
+    monkeypatch.setenv("HCCL_AMD_IPC_TIMEOUT_MS", "20000")
+    comms = worlds(n)
+    xs = [O.random_operands(O.FP32, count, seed=970 + r, edge=False) for r in range(n)]
+    used, outs = collective(comms, AR, H.Algo.IPC_RHD, O.FP32, O.SUM, xs, count, inplace=True)
+    assert used == H.Algo.IPC_RHD
+    want = oracle_replay(AR, R.ALGO_RHD, n, count, O.FP32, O.SUM, xs, 0, 0)
+    for r in range(n):
+        assert O.equal_bits(O.FP32, outs[r], want[r]), r
 
 
 def aiv_expected(op_type, dtype, op, xs, count, n, core_limit):
