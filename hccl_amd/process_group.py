@@ -280,7 +280,8 @@ class ProcessGroupHCCL(dist.ProcessGroup):
         one = torch.ones(1, dtype=torch.int32, device=dev)
         work = self._run([one], dev, lambda c, s: c.all_reduce(one, one, H.HcclReduceOp.SUM, s),
                          [one])
-        work._event.synchronize()  # a barrier returns to the host only when every rank has arrived
+        if work._event is not None:  # under capture there is nothing to wait for on the host
+            work._event.synchronize()  # a barrier returns to the host only when every rank has arrived
         return work
 
     def getBackendName(self) -> str:
