@@ -242,7 +242,7 @@ def fold_roofline(dev, stream, n: int = 8, reps: int = 10) -> dict:
             "kernel_avg_us": round(kavg * 1e6, 1), "kernel_median_us": round(float(np.median(per)) * 1e6, 1),
             "achieved_GBps": round(nbytes / kavg / 1e9, 1), "peak_GBps": HBM_PEAK_GBPS,
             "frac": round(nbytes / kavg / 1e9 / HBM_PEAK_GBPS, 4),
-            "traffic": load_pmc_traffic("r02_pmc_fold_n8.json"), "result_ok": ok}
+            "traffic": load_pmc_traffic("r02b_pmc_fold_n8.json"), "result_ok": ok}
 
 
 def bench_local(args) -> dict:
@@ -304,7 +304,7 @@ def bench_local(args) -> dict:
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": load_pmc_traffic("r02_pmc_local_reduce.json"),
+            "traffic": load_pmc_traffic("r02b_pmc_local_reduce.json"),
             "kernel": "k_reduce2<EFp<float>, SUM>",
             "algorithmic_bytes_per_launch": bytes_step,
             "kernel_avg_us": round(kavg * 1e6, 2),
