@@ -763,15 +763,19 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    e0, e1 = evs[0], evs[-1]
     t0 = time.perf_counter()
     e0.record(stream)
-    for _ in range(args.steps):
+    for k in range(args.steps):
         comm.all_reduce(send, recv, H.HcclReduceOp.SUM, stream)
-    e1.record(stream)
+        evs[k + 1].record(stream)
     torch.cuda.synchronize()
     dist.barrier()
     wall = time.perf_counter() - t0
+    # per-step durations (median and p10/p90), each step's max over ranks
+    steps_ms = torch.tensor([evs[k].elapsed_time(evs[k + 1]) for k in range(args.steps)], dtype=torch.float64)
+    dist.all_reduce(steps_ms, op=dist.ReduceOp.MAX)
     t = torch.tensor([e0.elapsed_time(e1) / 1e3, wall], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t[0])
@@ -819,6 +823,10 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
         },
         "busbw_GBps": round(busbw, 2),
         "algbw_GBps": round(algbw, 2),
+        "step_ms": {"median": round(float(np.median(steps_ms.numpy())), 3),
+                    "p10": round(float(np.percentile(steps_ms.numpy(), 10)), 3),
+                    "p90": round(float(np.percentile(steps_ms.numpy(), 90)), 3),
+                    "note": "per-step HIP-event durations on the launch stream, max over ranks per step"},
         "transport": _transport_info(),
         "result_ok": result_ok,
         "result_ok_algorithm": verified_algo,
