@@ -144,8 +144,10 @@ struct Comm {
 HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void* sendBuf, void* recvBuf,
                             uint64_t count, HcclDataType dt, HcclReduceOp op, uint32_t root, hipStream_t stream);
 // The same for an explicit plan (the AIV engine's variants, SelectAivPlan).
+// vCounts / vDispls (kIpcGeomV, ReduceScatterV): every rank's block, as the caller passed them (equal on all ranks).
 HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* sendBuf, void* recvBuf, uint64_t count,
-                      HcclDataType dt, HcclReduceOp op, uint32_t root, hipStream_t stream);
+                      HcclDataType dt, HcclReduceOp op, uint32_t root, hipStream_t stream,
+                      const uint64_t* vCounts = nullptr, const uint64_t* vDispls = nullptr);
 HcclResult IpcPlanRhd(uint32_t n, IpcPlan* pl);
 HcclResult IpcPlanForFamily(int32_t opType, int32_t family, uint32_t n, uint64_t es, uint64_t cclBytes, IpcPlan* pl);
 

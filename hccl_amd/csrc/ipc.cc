@@ -422,8 +422,12 @@ HcclResult RunIpcCollective(Comm& c, int32_t opType, int32_t family, const void*
 }
 
 HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* sendBuf, void* recvBuf,
-                      uint64_t count, HcclDataType dt, HcclReduceOp op, uint32_t root, hipStream_t stream)
+                      uint64_t count, HcclDataType dt, HcclReduceOp op, uint32_t root, hipStream_t stream,
+                      const uint64_t* vCounts, const uint64_t* vDispls)
 {
+    if (plan.geom == kIpcGeomV && (vCounts == nullptr || vDispls == nullptr || plan.loopElems != 0)) {
+        return HCCL_E_INTERNAL;
+    }
     uint64_t es = DataTypeSize(dt);
     if (es == 0 || c.nRanks > kIpcMaxRanks) return HCCL_E_NOT_SUPPORT;
     uint64_t loopElems = plan.loopElems;
@@ -458,7 +462,11 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
     // of the call's arguments alone). A loopback world runs every rank's blocks in one launch on one GPU, so it keeps
     // at most kIpcBlocks per rank to stay co-resident.
     const bool blockLayout = opType == HCCL_AMD_OP_REDUCE_SCATTER || opType == HCCL_AMD_OP_ALLGATHER;
-    const uint64_t callBytes = (blockLayout ? uint64_t(c.nRanks) : 1u) * count * es;  // RS input / AG output
+    uint64_t callBytes = (blockLayout ? uint64_t(c.nRanks) : 1u) * count * es;  // RS input / AG output
+    if (plan.geom == kIpcGeomV) {
+        callBytes = 0;
+        for (uint32_t q = 0; q < c.nRanks; ++q) callBytes += vCounts[q] * es;
+    }
     s.blocks = c.ipcBlocks != 0 ? c.ipcBlocks : DefaultIpcBlocks(callBytes);
     if (c.transport->SharedDevice()) s.blocks = std::min(s.blocks, kIpcBlocks);
     // Co-residency: every block waits at barriers for its peers' blocks, so all blocks on this device must be resident
@@ -516,10 +524,23 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
     for (uint64_t off = 0; off < count; off += loopElems) launches.push_back({off, std::min(loopElems, count - off)});
     auto geometry = [&](IpcArgs& g, uint64_t cnt) {
         g.balanced = false;
+        g.vgeom = false;
         g.group = 1;
         g.rem = 0;
         g.total = cnt;
         switch (plan.geom) {
+            case kIpcGeomV:
+                // ReduceScatterV: rank c's block is counts[c] elements at displs[c] of every input (one launch: the
+                // mesh order O1 does not depend on executor loops)
+                g.vgeom = true;
+                g.chunkStride = 0;
+                g.chunkLen = 0;
+                for (uint32_t q = 0; q < n; ++q) {
+                    g.vStart[q] = vDispls[q];
+                    g.vLen[q] = vCounts[q];
+                    g.chunkLen = std::max(g.chunkLen, vCounts[q]);
+                }
+                break;
             case kIpcGeomBlock:
                 // block c of the input (recvCount elements, stride recvCount) is chunk c (reduce_scatter_op.cc:158-159)
                 g.chunkStride = count;

@@ -43,6 +43,7 @@ enum IpcGeom : uint32_t {
                               // the AIV large-core two-shot (g = groupSize, aiv_all_reduce_mesh_1d_twoshot.h:21-58)
     kIpcGeomBlock = 3,        // ReduceScatter: chunk c = input block c (reduce_scatter_op.cc:158-159)
     kIpcGeomWhole = 4,        // one-shot kinds and AllGather: every chunk is the whole range
+    kIpcGeomV = 5,            // ReduceScatterV: chunk c = counts[c] elements at displs[c] (per-rank, any alignment)
 };
 
 // Everything that decides a one-sided call's bits: the kind, the fold order, the chunk layout and the executor loop
@@ -119,6 +120,9 @@ struct IpcArgs {
                        // [5]: blocks of the running launch that have finished (kIpcEpochWord, kIpcDoneWord)
     uint32_t callSeq;  // this call's sequence number on the communicator
     bool aligned;      // every in[] / out[] is 16-B aligned (chunks whose start is not are still element-wise)
+    bool vgeom;                          // kIpcGeomV: chunk c is vStart[c], vLen[c] (elements)
+    uint64_t vStart[kIpcMaxRanks];
+    uint64_t vLen[kIpcMaxRanks];
     uint32_t rhdParts;       // kIpcRhd: RHD instances R (parts of the launch's range)
     uint32_t alignElems;     // kIpcRhd: HCCL_MIN_SLICE_ALIGN (128 B) in elements
     uint64_t rhdPartStride;  // kIpcRhd: elements per part (the last part may be shorter)

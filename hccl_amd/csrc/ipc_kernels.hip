@@ -155,12 +155,14 @@ struct Range {
 
 __device__ __forceinline__ uint64_t ChunkStart(const IpcArgs& a, uint32_t c)
 {
+    if (a.vgeom) return a.vStart[c];
     const uint64_t s = uint64_t(c) * a.group;  // first slice of chunk c (balanced)
     return a.balanced ? s * a.chunkLen + min(s, a.rem) : uint64_t(c) * a.chunkStride;
 }
 
 __device__ __forceinline__ uint64_t ChunkElems(const IpcArgs& a, uint32_t c)
 {
+    if (a.vgeom) return a.vLen[c];
     if (a.balanced) {
         const uint64_t s = uint64_t(c) * a.group;
         return a.group * a.chunkLen + (a.rem > s ? min(a.group, a.rem - s) : 0);

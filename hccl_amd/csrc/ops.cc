@@ -190,8 +190,24 @@ HcclResult RunReduceScatterV(Comm& c, void* sendBuf, const uint64_t* counts, con
     // ReduceScatterVAutoSelector::SelectAicpuAlgo (reduce_scatter_v_auto_selector.cc:180-197): UINT64 and FP64 have
     // no algorithm
     if (dt == HCCL_DATA_TYPE_UINT64 || dt == HCCL_DATA_TYPE_FP64) return HCCL_E_NOT_SUPPORT;
-    // a bootstrap-only communicator has no send/recv path and the one-sided kernel has no per-rank block layout
-    if (c.nRanks > 1 && !c.transport->HasSendRecv()) return HCCL_E_NOT_SUPPORT;
+    // The one-sided kernel runs it over per-rank blocks (kIpcGeomV) in the same order O1 (own block first, then the
+    // other ranks ascending): on an IPC-only communicator, which has no send/recv path, and when the communicator's
+    // family is IPC / IPC_TWOSHOT. Without peer mappings an IPC-only communicator answers NOT_SUPPORT.
+    const bool ipcOnly = !c.transport->HasSendRecv();
+    if (c.nRanks > 1 &&
+        (ipcOnly || c.algoOverride == HCCL_AMD_ALGO_IPC || c.algoOverride == HCCL_AMD_ALGO_IPC_TWOSHOT)) {
+        IpcPlan plan{};
+        plan.kind = kIpcReduceScatter;
+        plan.order = kIpcO1;
+        plan.geom = kIpcGeomV;
+        const HcclResult r = RunIpcPlan(c, HCCL_AMD_OP_REDUCE_SCATTER, plan, sendBuf, recvBuf, counts[c.rank], dt, op,
+                                        0, stream, counts, displs);
+        if (r != HCCL_E_NOT_SUPPORT) {
+            c.lastAlgo = ipcOnly ? HCCL_AMD_ALGO_IPC : c.algoOverride;
+            return r;
+        }
+        if (ipcOnly) return HCCL_E_NOT_SUPPORT;
+    }
     const uint32_t es = DataTypeSize(dt);
     ScheduleParams p;
     p.opType = HCCL_AMD_OP_REDUCE_SCATTER_V;

@@ -16,7 +16,8 @@ The mapping is the one ProcessGroupHCCL makes:
   all_reduce_auto_selector.cc:517-550);
 * ``reduce`` -> HcclReduce (root = the group rank ``dst``);
 * ``reduce_scatter_tensor`` / ``reduce_scatter`` -> HcclReduceScatter (input = rankSize blocks of the output's size,
-  reduce_scatter_op.cc:158-159; the list form is packed into one buffer first);
+  reduce_scatter_op.cc:158-159; the list form is packed into one buffer first), or HcclReduceScatterV when the list's
+  blocks differ in size;
 * ``all_gather_into_tensor`` / ``all_gather`` -> HcclAllGather;
 * ``barrier`` -> a one-element HcclAllReduce, then the host waits for it;
 * ``broadcast`` -> HcclAllGather of the tensor's bytes, keeping the root's block (for DDP's start-up sync; the reduce
@@ -228,8 +229,19 @@ class ProcessGroupHCCL(dist.ProcessGroup):
     def reduce_scatter(self, outputs: List[torch.Tensor], inputs: List[List[torch.Tensor]], opts) -> _Work:
         if len(outputs) != 1 or len(inputs) != 1 or len(inputs[0]) != self.size():
             raise ValueError(f"backend {BACKEND_NAME!r}: reduce_scatter takes one output and world_size inputs")
-        packed = torch.cat([x.reshape(-1) for x in inputs[0]])
-        return self._reduce_scatter_base(outputs[0], packed, opts)
+        parts, output = inputs[0], outputs[0]
+        packed = torch.cat([x.reshape(-1) for x in parts])
+        counts = [x.numel() for x in parts]
+        if all(c == output.numel() for c in counts):
+            return self._reduce_scatter_base(output, packed, opts)
+        # uneven blocks: HcclReduceScatterV over the packed input (rank q's block at the running offset)
+        op = hccl_op(opts.reduceOp)
+        self._check(output, "reduce_scatter output")
+        if output.numel() != counts[self.rank()] or any(x.dtype != output.dtype for x in parts):
+            raise ValueError(f"backend {BACKEND_NAME!r}: reduce_scatter output must hold this rank's block")
+        displs = [sum(counts[:q]) for q in range(len(counts))]
+        return self._run([output], output.device,
+                         lambda c, s: c.reduce_scatter_v(packed, counts, displs, output, op, s), [packed, output])
 
     def _allgather_base(self, output: torch.Tensor, input: torch.Tensor, opts) -> _Work:
         self._check(output, "all_gather output")

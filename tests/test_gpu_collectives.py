@@ -637,13 +637,19 @@ def test_aiv_only_has_no_fallback(worlds):
 @pytest.mark.parametrize("n,layout", [(2, "ragged"), (4, "gapped"), (8, "ragged"), (8, "overlap"), (3, "empty")])
 @pytest.mark.parametrize("dtype,op", [(O.FP32, O.SUM), (O.FP16, O.SUM), (O.BFP16, O.MAX), (O.INT32, O.PROD),
                                       (O.INT64, O.MIN)], ids=lambda v: str(v))
-@pytest.mark.parametrize("streams", ["auto", "two"])
+@pytest.mark.parametrize("streams", ["auto", "two", "ipc"])
 def test_reduce_scatter_v(worlds, monkeypatch, n, layout, dtype, op, streams):
     """HcclReduceScatterV through the executor: rank r's output is the mesh template's O1 fold of every rank's block r
-    (ins_temp_reduce_scatter_v_mesh_1D.cc:107-146), bit-exact against the closed form and the oracle's IR replay."""
+    (ins_temp_reduce_scatter_v_mesh_1D.cc:107-146), bit-exact against the closed form and the oracle's IR replay.
+    "ipc": the same call on the one-sided kernel over per-rank blocks (kIpcGeomV), the path IPC-only communicators
+    take."""
     if streams == "two":
         monkeypatch.setenv("HCCL_AMD_SINGLE_STREAM_BYTES", "0")
+    if streams == "ipc":
+        monkeypatch.setenv("HCCL_AMD_IPC_TIMEOUT_MS", "20000")
     comms = worlds(n)
+    for c in comms:
+        c.set_algo(9 if streams == "ipc" else 0)
     if layout == "gapped":
         counts, displs = [70001] * n, [q * 80000 + 3 for q in range(n)]
     elif layout == "overlap":
@@ -663,9 +669,13 @@ def test_reduce_scatter_v(worlds, monkeypatch, n, layout, dtype, op, streams):
     try:
         run_ranks(n, lambda r: comms[r].reduce_scatter_v(sends[r], counts, displs, recvs[r], op, streams_[r]))
         torch.cuda.synchronize()
+        used = comms[0].last_algo
     finally:
         for c in comms:
             c.set_piece_bytes(0)
+            c.set_algo(0)
+    if streams == "ipc":
+        assert used == 9 and ipc_status(comms[0]) & 1 == 0
     want = R.reduce_scatter_v_o1(dtype, op, xs, counts, displs)
     for r in range(n):
         got = to_host(dtype, recvs[r])[:counts[r]]

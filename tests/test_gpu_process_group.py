@@ -84,6 +84,13 @@ def _rank_main(rank, n, port, transport, q):
         out2 = torch.empty(rc, device="cuda")
         dist.reduce_scatter(out2, list(inp.chunk(n)))
         checks["reduce_scatter_list"] = bool(torch.equal(out2, want))
+        # --- reduce_scatter with uneven blocks (HcclReduceScatterV): rank q's block has 1000 + 37 q elements
+        sizes = [1000 + 37 * q for q in range(n)]
+        blocks = [torch.arange(sz, dtype=torch.float32, device="cuda") % 7 + rank for sz in sizes]
+        mine = torch.empty(sizes[rank], device="cuda")
+        dist.reduce_scatter(mine, blocks)
+        checks["reduce_scatter_uneven"] = bool(torch.equal(
+            mine, n * (torch.arange(sizes[rank], dtype=torch.float32, device="cuda") % 7) + n * (n - 1) / 2))
         # --- all_gather_into_tensor and the list form (bf16: data movement, any dtype)
         a = torch.full((777,), float(rank), dtype=torch.bfloat16, device="cuda")
         full = torch.empty(777 * n, dtype=torch.bfloat16, device="cuda")
