@@ -17,12 +17,17 @@ AR1, RED1, ARMC = 3, 4, 5  # one-shot AllReduce, one-shot Reduce, MeshChunk AllR
 ARBAL = 6  # AIV large-core two-shot AllReduce: group * n balanced slices, rank c owning [c*group, (c+1)*group)
 
 
-def geometry(kind, n, count, es, group=1):
+RSV = 7  # ReduceScatterV: kIpcGeomV, chunk c = (displs[c], counts[c]), any alignment, order O1
+
+
+def geometry(kind, n, count, es, group=1, vblocks=None):
     """RunIpcCollective for one launch: (chunks [(start, len)] in input coordinates, piece, block elems, rounds).
     AllReduce: ceil(count/n) rounded to 128 B; ReduceScatter: the blocks; Reduce: the balanced two-shot split;
     one-shot kinds: every chunk is the whole range; MeshChunk AllReduce: ceil(count/n) without alignment."""
     v = 16 // es
-    if kind in (AR1, RED1):
+    if kind == RSV:
+        chunks = list(vblocks)
+    elif kind in (AR1, RED1):
         chunks = [(0, count) for _ in range(n)]
     elif kind == ARMC:
         cs = -(-count // n)
@@ -91,12 +96,14 @@ def fold_segments(kind, n, es, chunk_len, kp, lo, hi, o6):
     return out
 
 
-def check_general(kind, n, count, es, vec, root=0, o6=False):
+def check_general(kind, n, count, es, vec, root=0, o6=False, vblocks=None):
     """The generalised kernel: one-shot kinds push the whole piece (Reduce: to the root only) and fold it without a
     phase 2; O6 folds a window per sub-slice with scalar head and tail around the vector body."""
     v = 16 // es
-    chunks, piece, block, rounds = geometry(kind, n, count, es)
+    chunks, piece, block, rounds = geometry(kind, n, count, es, vblocks=vblocks)
     total = n * count if kind == RS else count
+    if kind == RSV:
+        total = max(st + ln for st, ln in chunks)
     for me in range(n):
         cover1 = np.zeros(total, np.int32)
         pushed = np.zeros((n, total), np.int32)  # pushed[c]: elements delivered to owner c by me
@@ -300,3 +307,24 @@ def test_old_element_loop_start_is_caught():
     bad = (vhi * v, hi)
     assert bad[0] < lo  # would write element 4 for the empty window [5, 5)
     assert touched(lo, hi, v)[1][0] >= lo
+
+
+@pytest.mark.parametrize("layout", ["ragged", "gapped", "overlap", "empty", "unaligned"])
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("es", [1, 2, 4, 8])
+def test_ipc_reduce_scatter_v_in_bounds_and_exact_cover(layout, n, es):
+    """kIpcGeomV (HcclReduceScatterV on the one-sided kernel): blocks of any size at any displacement, overlapping
+    or empty; every block pushed to its owner once and folded by it once, inside every buffer."""
+    if layout == "gapped":
+        blocks = [(q * 9001 + 3, 7001) for q in range(n)]
+    elif layout == "overlap":
+        blocks = [(q * 100, 30007) for q in range(n)]
+    elif layout == "empty":
+        blocks = [(q * 5000, 0 if q == 1 else 4099) for q in range(n)]
+    elif layout == "unaligned":
+        blocks = [(q * 4097 + q, 4097) for q in range(n)]
+    else:
+        counts = [(40961 * (q + 3)) % 15001 + 1 for q in range(n)]
+        blocks = [(sum(counts[:q]), counts[q]) for q in range(n)]
+    check_general(RSV, n, 0, es, vec=True, vblocks=blocks)
+    check_general(RSV, n, 0, es, vec=False, vblocks=blocks)
