@@ -520,8 +520,16 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
         uint64_t off, cnt;
     };
     std::vector<Launch> launches;
-    if (loopElems == 0) loopElems = count;
-    for (uint64_t off = 0; off < count; off += loopElems) launches.push_back({off, std::min(loopElems, count - off)});
+    if (plan.geom == kIpcGeomV) {
+        // one launch on every rank, whatever this rank's own block: the launch is collective (every block meets its
+        // peers at the barriers), and a rank whose block is empty still pushes its share of the others' blocks
+        launches.push_back({0, 0});
+    } else {
+        if (loopElems == 0) loopElems = count;
+        for (uint64_t off = 0; off < count; off += loopElems) {
+            launches.push_back({off, std::min(loopElems, count - off)});
+        }
+    }
     auto geometry = [&](IpcArgs& g, uint64_t cnt) {
         g.balanced = false;
         g.vgeom = false;

@@ -634,7 +634,8 @@ def test_aiv_only_has_no_fallback(worlds):
             c.set_algo(0)
 
 
-@pytest.mark.parametrize("n,layout", [(2, "ragged"), (4, "gapped"), (8, "ragged"), (8, "overlap"), (3, "empty")])
+@pytest.mark.parametrize("n,layout", [(2, "ragged"), (4, "gapped"), (8, "ragged"), (8, "overlap"), (3, "empty"),
+                                      (4, "empty0")])
 @pytest.mark.parametrize("dtype,op", [(O.FP32, O.SUM), (O.FP16, O.SUM), (O.BFP16, O.MAX), (O.INT32, O.PROD),
                                       (O.INT64, O.MIN)], ids=lambda v: str(v))
 @pytest.mark.parametrize("streams", ["auto", "two", "ipc"])
@@ -654,6 +655,8 @@ def test_reduce_scatter_v(worlds, monkeypatch, n, layout, dtype, op, streams):
         counts, displs = [70001] * n, [q * 80000 + 3 for q in range(n)]
     elif layout == "overlap":
         counts, displs = [300007] * n, [q * 1000 for q in range(n)]
+    elif layout == "empty0":  # rank 0's own block is empty: it must still take part (a loopback world launches
+        counts, displs = [0] + [50003] * (n - 1), [0] + [q * 50003 for q in range(n - 1)]  # from rank 0)
     else:
         counts = [(40961 * (q + 3)) % 150001 + (0 if layout != "empty" or q != 1 else -((40961 * 4) % 150001))
                   for q in range(n)]
