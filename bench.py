@@ -756,11 +756,34 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     # reference's own selection at this size (MeshChunk, order O6) and every other family run beside it in
     # other_configs.c3_schedules.
     headline = H.Algo[(args.algo or "ring").upper()]
-    comm.set_algo(headline)
     stream = torch.cuda.current_stream()
-    for _ in range(args.warmup):
-        comm.all_reduce(send, recv, H.HcclReduceOp.SUM, stream)
-    torch.cuda.synchronize()
+
+    def warm(c, algo):
+        c.set_algo(algo)
+        for _ in range(args.warmup):
+            c.all_reduce(send, recv, H.HcclReduceOp.SUM, stream)
+        torch.cuda.synchronize()
+
+    # A schedule that errors on its first run on this node must not cost the whole line: every rank agrees (over gloo)
+    # and the headline falls back to the reference's own selection on a fresh communicator, with the error recorded.
+    fallback = None
+    err = ""
+    try:
+        warm(comm, headline)
+        mine = 1
+    except H.HcclError as e:
+        mine, err = 0, str(e)
+    flag = torch.tensor([mine], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if not flag.item():
+        fallback = {"headline_failed": headline.name, "error": err or "on another rank", "measured": "AUTO"}
+        try:
+            comm.destroy()
+        except H.HcclError:
+            pass
+        comm = new_comm()
+        headline = H.Algo.AUTO
+        warm(comm, headline)
     dist.barrier()
     torch.cuda.synchronize()
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
@@ -830,6 +853,7 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
         "transport": _transport_info(),
         "result_ok": result_ok,
         "result_ok_algorithm": verified_algo,
+        "headline_fallback": fallback,
         "rccl_allreduce_reference": None,
         "other_configs": {},
         "roofline": {
