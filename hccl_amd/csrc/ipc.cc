@@ -20,6 +20,7 @@ namespace {
 struct Exported {
     hipIpcMemHandle_t stg;
     hipIpcMemHandle_t flags;
+    char busId[32];  // the rank's device: ranks that share one count against its resident blocks together
 };
 
 struct RawPtrs {
@@ -95,7 +96,8 @@ HcclResult IpcSetup(Comm& c)
         // two-shot on every rank alike, never a mix of paths that would leave peers waiting).
         Exported mine{};
         ok = ok && hipIpcGetMemHandle(&mine.stg, s.stg) == hipSuccess &&
-             hipIpcGetMemHandle(&mine.flags, s.flags) == hipSuccess;
+             hipIpcGetMemHandle(&mine.flags, s.flags) == hipSuccess &&
+             hipDeviceGetPCIBusId(mine.busId, sizeof mine.busId - 1, c.device) == hipSuccess;
         std::vector<Exported> all(n);
         HcclResult xr = c.transport->AllGatherHost(&mine, sizeof mine, all.data());
         if (xr != HCCL_SUCCESS) {
@@ -104,6 +106,14 @@ HcclResult IpcSetup(Comm& c)
             IpcRelease(c);
             s.unavailable = true;
             return xr;
+        }
+        // the most ranks any one device holds, from every rank's bus id: the same number on every rank, so the block
+        // counts (block b pairs with block b of each peer) stay equal whatever the placement
+        s.ranksOnDevice = 1;
+        for (uint32_t r = 0; r < n; ++r) {
+            uint32_t k = 0;
+            for (uint32_t q = 0; q < n; ++q) k += std::strncmp(all[r].busId, all[q].busId, sizeof mine.busId) == 0;
+            s.ranksOnDevice = std::max(s.ranksOnDevice, k);
         }
         for (uint32_t r = 0; r < n && ok; ++r) {
             if (r == me) {
@@ -470,10 +480,11 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
     s.blocks = c.ipcBlocks != 0 ? c.ipcBlocks : DefaultIpcBlocks(callBytes);
     if (c.transport->SharedDevice()) s.blocks = std::min(s.blocks, kIpcBlocks);
     // Co-residency: every block waits at barriers for its peers' blocks, so all blocks on this device must be resident
-    // at once (a loopback world puts every rank's blocks on it). The count depends only on the kernel and the device,
+    // at once (a loopback world puts every rank's blocks on it; in rank mode, the ranks whose processes share this
+    // device, counted at set-up by PCI bus id). The count depends only on the kernel, the device and the placement,
     // so ranks of a node agree on it.
     {
-        const uint32_t here = c.transport->SharedDevice() ? n : 1u;
+        const uint32_t here = c.transport->SharedDevice() ? n : std::max<uint32_t>(1, s.ranksOnDevice);
         const uint32_t resident = IpcResidentBlocks(dt, op, plan.order == kIpcRhd);
         if (resident != 0) s.blocks = std::max<uint32_t>(1, std::min(s.blocks, resident / here));
     }

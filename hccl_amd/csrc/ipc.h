@@ -157,6 +157,7 @@ struct IpcState {
     uint64_t stgResBytes = 0;
     uint64_t stgAltBytes = 0;      // each of the two alternate slot areas of the single-barrier kinds
     uint32_t blocks = 0;
+    uint32_t ranksOnDevice = 1;    // rank mode: the most ranks that share one device (by PCI bus id), same on all ranks
 };
 
 constexpr uint32_t kIpcBlocks = 128;     // workgroups per rank and launch in a loopback world (cap)
