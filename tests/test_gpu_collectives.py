@@ -438,6 +438,57 @@ def test_random_collectives_match_oracle(worlds, monkeypatch, case):
         assert O.equal_bits(dtype, outs[r], want[r]), (case, r)
 
 
+def _random_ipc_cases(k):
+    rng = np.random.default_rng(20261017)
+    dts = [O.INT8, O.INT16, O.INT32, O.INT64, O.UINT64, O.FP16, O.BFP16, O.FP32, O.FP64]
+    out = []
+    for i in range(k):
+        op_type = int(rng.choice([AR, AR, RS, RED, AG]))
+        n = int(rng.choice([2, 3, 4, 8]))
+        algo = int(rng.choice([7, 9] + ([12] if op_type == AR and n & (n - 1) == 0 else [])))
+        dtype = int(rng.choice(dts))
+        op = int(rng.choice(O.OPS)) if op_type != AG else O.SUM
+        if op == O.PROD and dtype in (O.INT16, O.BFP16):
+            op = O.MAX
+        count = int(rng.choice([1, 5, 100, 4099, 65537, 300001, (3 << 20) + 1]))
+        out.append((i, op_type, algo, n, dtype, op, count))
+    return out
+
+
+def _ipc_twin(op_type, algo, n, count, dtype, op):
+    """The RCCL-path family whose bits an IPC family gives: IPC_TWOSHOT = two-shot AllReduce (O2) / mesh
+    ReduceScatter (O1) / two-shot Reduce; IPC = the auto selector's family; IPC_RHD = RHD."""
+    if algo == 12:
+        return R.ALGO_RHD
+    if algo == 7:
+        return 1 if op_type in (RS, AG) else 2
+    es = np.dtype(O.NP_STORAGE[dtype]).itemsize
+    special = dtype in (O.INT64, O.UINT64, O.FP64) or op == O.PROD
+    return H.select_algo(op_type, n, count * es, special)
+
+
+@pytest.mark.parametrize("case", _random_ipc_cases(int(os.environ.get("HCCL_AMD_RANDOM_DRAWS_IPC", "300"))),
+                         ids=lambda c: f"ipc{c[0]}")
+def test_random_ipc_collectives_match_their_rccl_twin(worlds, monkeypatch, case):
+    """Seeded random draws over the one-sided kernel's families (IPC_TWOSHOT, IPC, IPC_RHD) x operation x ranks x
+    dtype x op x count, each bit-exact against the oracle replaying the RCCL-path schedule whose order it follows."""
+    _, op_type, algo, n, dtype, op, count = case
+    monkeypatch.setenv("HCCL_AMD_IPC_TIMEOUT_MS", "20000")
+    comms = worlds(n)
+    root = (count + 1) % n
+    in_count = count * n if op_type == RS else count
+    xs = [O.random_operands(dtype, in_count, seed=9100 + 17 * case[0] + r, edge=False) for r in range(n)]
+    used, outs = collective(comms, op_type, algo, dtype, op, xs, count, root=root)
+    assert used == algo, used
+    assert ipc_status(comms[0]) & 1 == 0
+    want = oracle_replay(op_type, _ipc_twin(op_type, algo, n, count, dtype, op), n, count, dtype, op, xs, root, 0)
+    for r in range(n):
+        if op_type == RED and r != root:
+            assert not outs[r].any(), "non-root recvBuf written"
+            continue
+        assert O.equal_bits(dtype, outs[r], want[r]), (case, r)
+
+
 @pytest.mark.parametrize("dtype", [O.INT8, O.INT16, O.INT32, O.INT64, O.UINT64, O.FP16, O.BFP16, O.FP64],
                          ids=lambda v: O.DTYPE_NAMES[v])
 @pytest.mark.parametrize("op", O.OPS, ids=lambda v: O.OP_NAMES[v])
