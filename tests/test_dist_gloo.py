@@ -7,7 +7,6 @@ closed-form association order on every rank. This checks that independently gene
 message for message across process boundaries, as they must over RCCL.
 """
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -16,12 +15,6 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-
-
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
 
 
 def _execute(prog, nops, bufs, dtype, op):
@@ -66,7 +59,9 @@ def _worker(rank, world, port, cases, q):
         from oracle import oracle as O
         from tests import sched_ref as R
 
-        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        import datetime
+        store = dist.TCPStore("127.0.0.1", port, is_master=False, timeout=datetime.timedelta(seconds=120))
+        dist.init_process_group("gloo", store=store, rank=rank, world_size=world)
         for op_type, algo, count, dtype, op in cases:
             prog, nops, used, scratch = H.build_schedule(op_type, algo, world, rank, count, dtype, root=world - 1,
                                                          piece_bytes=4096)
@@ -88,9 +83,13 @@ def _worker(rank, world, port, cases, q):
 
 
 def _launch(world, cases):
+    import datetime
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    # the store's server lives in this process on a port the OS picks: no free-port race with parallel test workers
+    master = dist.TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False,
+                           timeout=datetime.timedelta(seconds=120))
+    port = master.port
     procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q)) for r in range(world)]
     for p in procs:
         p.start()

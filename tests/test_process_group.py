@@ -7,7 +7,6 @@ run before any GPU call.
 """
 import datetime
 import multiprocessing as mp
-import socket
 
 import pytest
 import torch
@@ -34,14 +33,8 @@ def test_reduce_op_mapping():
             PG.hccl_op(op)
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def _ag_rank(rank, n, port, q):
-    store = dist.TCPStore("127.0.0.1", port, n, rank == 0, timeout=datetime.timedelta(seconds=60))
+    store = dist.TCPStore("127.0.0.1", port, is_master=False, timeout=datetime.timedelta(seconds=60))
     ag = PG.StoreAllGather(store, rank, n, "t")
     rounds = [ag(bytes([rank]) * (3 + i)) for i in range(3)]
     q.put((rank, rounds))
@@ -51,7 +44,10 @@ def test_store_all_gather_two_processes():
     n = 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    # the parent holds the store's server on a port the OS picks (no free-port race with parallel test workers)
+    master = dist.TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False,
+                           timeout=datetime.timedelta(seconds=60))
+    port = master.port
     procs = [ctx.Process(target=_ag_rank, args=(r, n, port, q)) for r in range(n)]
     for p in procs:
         p.start()
