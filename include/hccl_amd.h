@@ -242,8 +242,9 @@ typedef int32_t (*HcclAmdHostAllGatherFn)(void* ctx, const void* mine, uint64_t 
 
 /* Rank `rank` of an IPC-only communicator on the current HIP device, bootstrapped through `fn` instead of RCCL.
  * Its data path is the one-sided kernel over peer-mapped memory opened with hipIpcOpenMemHandle:
- * HCCL_AMD_ALGO_IPC_TWOSHOT (the default on such a communicator), otherwise HCCL_AMD_ALGO_IPC whatever family is
- * set; AllGather (no IPC form) returns HCCL_E_NOT_SUPPORT.
+ * HCCL_AMD_ALGO_IPC_TWOSHOT (the default on such a communicator), HCCL_AMD_ALGO_IPC_RHD when RHD or IPC_RHD is set
+ * (AllReduce, power-of-two ranks), otherwise HCCL_AMD_ALGO_IPC whatever family is set. Every operator has an IPC form,
+ * HcclReduceScatterV included (per-rank blocks, order O1).
  * Ranks may share a device (separate processes), which is how the rank-mode IPC path is tested on one GPU.
  * `fn` and `ctx` must stay valid for the communicator's lifetime. */
 extern HcclResult HcclAmdCommInitHostExchange(uint32_t nRanks, uint32_t rank, HcclAmdHostAllGatherFn fn, void* ctx,
