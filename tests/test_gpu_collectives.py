@@ -608,6 +608,43 @@ def test_aiv_engine_orders(worlds, monkeypatch, op_type, n, count, core_limit, d
         assert O.equal_bits(dtype, outs[r], want[r]), (r, variant)
 
 
+def _random_aiv_cases(k):
+    rng = np.random.default_rng(20261018)
+    dts = [O.INT8, O.INT16, O.INT32, O.INT64, O.FP16, O.BFP16, O.FP32]  # the AIV engine's dtypes (no UINT64/FP64)
+    out = []
+    while len(out) < k:
+        op_type = int(rng.choice([AR, RS]))
+        n = int(rng.choice([2, 3, 4, 5, 8]))
+        dtype = int(rng.choice(dts))
+        op = int(rng.choice([O.SUM, O.MAX, O.MIN]))  # PROD is not an AIV op (falls back)
+        count = int(rng.choice([1, 7, 1001, 30001, 70001, 131077, 300007, (1 << 20) + 3]))
+        core_limit = int(rng.choice([4, 6, 9, 16, 48, 56]))
+        es = np.dtype(O.NP_STORAGE[dtype]).itemsize
+        variant, _ = R.aiv_select(op_type, n, count, es, False, False, core_limit=core_limit)
+        if variant == R.AIV_NOT_MATCHED:
+            continue
+        out.append((len(out), op_type, n, dtype, op, count, core_limit))
+    return out
+
+
+@pytest.mark.parametrize("case", _random_aiv_cases(int(os.environ.get("HCCL_AMD_RANDOM_DRAWS_AIV", "150"))),
+                         ids=lambda c: f"aiv{c[0]}")
+def test_random_aiv_engine_orders(worlds, monkeypatch, case):
+    """Seeded random draws over the AIV engine (operation x ranks x dtype x op x count x vector-core limit), each
+    bit-exact against the closed form of the variant SelectAivAlgo picks."""
+    _, op_type, n, dtype, op, count, core_limit = case
+    monkeypatch.setenv("HCCL_AMD_AIV_CORE_LIMIT", str(core_limit))
+    monkeypatch.setenv("HCCL_AMD_IPC_TIMEOUT_MS", "20000")
+    comms = worlds(n)
+    in_count = count * n if op_type == RS else count
+    xs = [O.random_operands(dtype, in_count, seed=9700 + 11 * case[0] + r, edge=False) for r in range(n)]
+    variant, want = aiv_expected(op_type, dtype, op, xs, count, n, core_limit)
+    used, outs = collective(comms, op_type, H.Algo.AIV, dtype, op, xs, count)
+    assert used == H.Algo.AIV
+    for r in range(n):
+        assert O.equal_bits(dtype, outs[r], want[r]), (case, r, variant)
+
+
 @pytest.mark.parametrize("n,count", [(8, (1 << 20) + 7), (4, (3 << 19) + 5), (3, 700001)])
 def test_aiv_two_shot_slices_follow_its_loops(monkeypatch, n, count):
     """The AIV large-core two-shot slices every executor loop of min(UB_MAX_DATA_SIZE, ccl/4) into groupSize * n
