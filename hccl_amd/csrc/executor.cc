@@ -290,15 +290,18 @@ HcclResult CompileCollective(Comm& c, const ScheduleParams& p, void* const bufs[
 HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const bufs[3], HcclDataType dt,
                    HcclReduceOp op, hipStream_t user, bool singleStream, const std::vector<UnitPlan>* cached)
 {
+    hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
+    HIP_CHK(hipStreamIsCapturing(user, &capture));
+    const bool captured = capture != hipStreamCaptureStatusNone;
+    // A loopback world meets its peers through host rendezvous and events exchanged between threads on every group,
+    // which a graph cannot replay: refused under capture, before anything is enqueued (every rank alike).
+    if (captured && c.transport->SharedDevice()) return HCCL_E_NOT_SUPPORT;
     if (singleStream) return ExecuteSingleStream(c, ops, bufs, dt, op, user);
     const uint64_t es = DataTypeSize(dt);
     // Under stream capture the transport groups go on the capturing stream itself and only the folds on a forked
     // stream: an RCCL group captured on a stream joined to the capture (rather than its origin) brought down graph
     // instantiation (hipStreamEndCapture segfaulted; tools/rccl_capture_probe.py), while the same group on the origin
     // stream captures and replays. The plan and its waits are the same; only the link stream's identity changes.
-    hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
-    HIP_CHK(hipStreamIsCapturing(user, &capture));
-    const bool captured = capture != hipStreamCaptureStatusNone;
     hipStream_t streams[2] = {captured ? user : c.commStream, c.reduceStream};
     c.nextEvent = 0;
     hipEvent_t start;
