@@ -43,9 +43,6 @@ def check_live(progs):
     """progs[r] = list of groups. Raises AssertionError with the stuck state on a deadlock."""
     n = len(progs)
     pos = [0] * n
-    # posted[(a, b)]: messages a->b already completed (sends on a, recvs on b counted separately)
-    sent = {}
-    recvd = {}
     # tag each message with its per-pair sequence number, once, in posting order
     tagged = []
     for r in range(n):
@@ -179,3 +176,22 @@ def test_group_sizes_fit_rccl_p2p_limits():
     worst = max(len(g) for p in progs for g in p)
     assert worst <= 14, worst
     assert np.all([len(p) == len(progs[0]) for p in progs])
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
+@pytest.mark.parametrize("layout", ["ragged", "gapped", "empty"])
+def test_reduce_scatter_v_schedules_are_live(n, layout):
+    """HcclReduceScatterV's programs (HcclAmdBuildScheduleV): blocks of different sizes, gaps and empty blocks."""
+    if layout == "gapped":
+        counts, displs = [7001] * n, [q * 9001 + 3 for q in range(n)]
+    elif layout == "empty":
+        counts = [0 if q == 1 else 4099 for q in range(n)]
+        displs = [q * 5000 for q in range(n)]
+    else:
+        counts = [(40961 * (q + 3)) % 150001 + 1 for q in range(n)]
+        displs = [sum(counts[:q]) for q in range(n)]
+    progs = []
+    for r in range(n):
+        arr, nops, _ = H.build_schedule_v(n, r, counts, displs, O.FP32, piece_bytes=16 << 10)
+        progs.append(groups_of(arr, nops))
+    check_live(progs)
