@@ -339,3 +339,36 @@ def comm_init_all(devices) -> List[Comm]:
     arr = (ctypes.c_void_p * len(devices))()
     check("HcclCommInitAll", lib.HcclCommInitAll(len(devices), arr_dev, arr))
     return [Comm(arr[i]) for i in range(len(devices))]
+
+
+def last_bootstrap():
+    """(stage, id_digest) of this process' last HcclCommInitClusterInfo: stage 0 = failed before the unique-id exchange
+    completed, 1 = id exchanged over TCP, 2 = RCCL communicator created; id_digest = FNV-1a 64 of the exchanged id."""
+    d = ctypes.c_uint64(0)
+    st = ctypes.c_int32(0)
+    check("HcclAmdLastBootstrap", lib.HcclAmdLastBootstrap(ctypes.byref(d), ctypes.byref(st)))
+    return st.value, d.value
+
+
+def bootstrap_exchange_id(path: str, rank: int, ident: bytes = b"") -> bytes:
+    """The rank-table TCP exchange alone (host only): rank 0 serves `ident` (128 bytes), the others receive it."""
+    buf = ctypes.create_string_buffer(ident.ljust(128, b"\0")[:128], 128)
+    check("HcclAmdBootstrapExchangeId", lib.HcclAmdBootstrapExchangeId(path.encode(), rank, buf))
+    return buf.raw
+
+
+def pending_destroys() -> int:
+    """Communicators whose HcclCommDestroy waits for the graphs captured on them to be destroyed."""
+    return int(lib.HcclAmdCommPendingDestroys())
+
+
+HOST_PROFILE_CATEGORIES = ("execute", "group", "fold", "copy", "record", "wait", "plan")
+
+
+def host_profile(reset: bool = True) -> dict:
+    """Executor host time by category while HCCL_AMD_HOST_PROFILE=1: {category: (ns, calls)}."""
+    n = len(HOST_PROFILE_CATEGORIES)
+    ns = (ctypes.c_uint64 * n)()
+    calls = (ctypes.c_uint64 * n)()
+    check("HcclAmdHostProfile", lib.HcclAmdHostProfile(ns, calls, n, 1 if reset else 0))
+    return {k: (ns[i], calls[i]) for i, k in enumerate(HOST_PROFILE_CATEGORIES)}

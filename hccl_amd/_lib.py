@@ -198,6 +198,10 @@ SIGNATURES = {
     "HcclAmdRankTableInfo": (_res, [ctypes.c_char_p, _u32, ctypes.POINTER(_u32), ctypes.POINTER(ctypes.c_int32)]),
     "HcclCommInitClusterInfo": (_res, [ctypes.c_char_p, _u32, ctypes.POINTER(_vp)]),
     "HcclCommInitAll": (_res, [_u32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(_vp)]),
+    "HcclAmdLastBootstrap": (_res, [ctypes.POINTER(_u64), ctypes.POINTER(ctypes.c_int32)]),
+    "HcclAmdBootstrapExchangeId": (_res, [ctypes.c_char_p, _u32, _vp]),
+    "HcclAmdCommPendingDestroys": (_u32, []),
+    "HcclAmdHostProfile": (_res, [ctypes.POINTER(_u64), ctypes.POINTER(_u64), _u32, _i32]),
 }
 
 

@@ -18,6 +18,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -338,8 +339,7 @@ HcclResult ResolveRoot(const std::string& host, uint16_t port, sockaddr_storage*
 HcclResult ExchangeUniqueId(const std::string& host, uint16_t port, uint32_t n, uint32_t rank, char id[128])
 {
     if (n == 1) return HCCL_SUCCESS;
-    const uint64_t timeoutS = EnvU64("HCCL_CONNECT_TIMEOUT", 120, 120, 7200) + 20;
-    const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(timeoutS);
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(ConnectTimeoutMs());
     sockaddr_storage sa{};
     socklen_t salen = 0;
     HCCL_CHK(ResolveRoot(host, port, &sa, &salen));
@@ -422,36 +422,97 @@ extern "C" HcclResult HcclAmdRankTableInfo(const char* clusterInfo, uint32_t ran
     return HCCL_SUCCESS;
 }
 
-extern "C" HcclResult HcclCommInitClusterInfo(const char* clusterInfo, uint32_t rank, HcclComm* comm)
+namespace hccl_amd {
+
+namespace {
+
+// Where the rank-0 unique id is published for a table: the rank-0 server's host_ip, else HCCL_IF_IP, else 127.0.0.1
+// for a single server; the rank-0 device's host_port, else HCCL_IF_BASE_PORT.
+HcclResult RootAddress(const RankTable& rt, std::string* host, uint16_t* port)
 {
-    if (clusterInfo == nullptr || comm == nullptr) return HCCL_E_PTR;
-    RankTable rt;
-    HCCL_CHK(LoadRankTable(clusterInfo, &rt));
-    const uint32_t n = static_cast<uint32_t>(rt.ranks.size());
-    if (rank >= n) {
-        HCCL_AMD_ERR("rank %u is not in the rank table (%u ranks)", rank, n);
-        return HCCL_E_PARA;
-    }
     const RankEntry& root = rt.ranks[0];
-    std::string host = rt.serverHostIp[root.server];
-    if (host.empty()) {
+    *host = rt.serverHostIp[root.server];
+    if (host->empty()) {
         const char* ip = std::getenv("HCCL_IF_IP");
         if (ip != nullptr && *ip != '\0') {
-            host = ip;
+            *host = ip;
         } else if (rt.serverHostIp.size() == 1) {
-            host = "127.0.0.1";
+            *host = "127.0.0.1";
         } else {
             HCCL_AMD_ERR("rank table spans %zu servers: give the rank-0 server a host_ip or set HCCL_IF_IP",
                          rt.serverHostIp.size());
             return HCCL_E_PARA;
         }
     }
-    const uint16_t port = static_cast<uint16_t>(
+    *port = static_cast<uint16_t>(
         root.hostPort > 0 ? static_cast<uint64_t>(root.hostPort) : EnvU64("HCCL_IF_BASE_PORT", 60000, 1024, 65520));
+    return HCCL_SUCCESS;
+}
+
+HcclResult LoadForRank(const char* clusterInfo, uint32_t rank, RankTable* rt)
+{
+    HCCL_CHK(LoadRankTable(clusterInfo, rt));
+    if (rank >= rt->ranks.size()) {
+        HCCL_AMD_ERR("rank %u is not in the rank table (%zu ranks)", rank, rt->ranks.size());
+        return HCCL_E_PARA;
+    }
+    return HCCL_SUCCESS;
+}
+
+// The last HcclCommInitClusterInfo of the process (HcclAmdLastBootstrap).
+std::atomic<uint64_t> gLastIdDigest{0};
+std::atomic<int32_t> gLastStage{0};
+
+uint64_t Fnv1a64(const char* p, size_t n)
+{
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < n; ++i) {
+        h ^= static_cast<uint8_t>(p[i]);
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+
+}  // namespace
+
+}  // namespace hccl_amd
+
+extern "C" HcclResult HcclAmdBootstrapExchangeId(const char* clusterInfo, uint32_t rank, void* id128)
+{
+    if (clusterInfo == nullptr || id128 == nullptr) return HCCL_E_PTR;
+    RankTable rt;
+    HCCL_CHK(LoadForRank(clusterInfo, rank, &rt));
+    std::string host;
+    uint16_t port = 0;
+    HCCL_CHK(RootAddress(rt, &host, &port));
+    return ExchangeUniqueId(host, port, static_cast<uint32_t>(rt.ranks.size()), rank, static_cast<char*>(id128));
+}
+
+extern "C" HcclResult HcclAmdLastBootstrap(uint64_t* idDigest, int32_t* stage)
+{
+    if (idDigest == nullptr || stage == nullptr) return HCCL_E_PTR;
+    *stage = gLastStage.load();
+    *idDigest = gLastIdDigest.load();
+    return HCCL_SUCCESS;
+}
+
+extern "C" HcclResult HcclCommInitClusterInfo(const char* clusterInfo, uint32_t rank, HcclComm* comm)
+{
+    if (clusterInfo == nullptr || comm == nullptr) return HCCL_E_PTR;
+    gLastStage = 0;
+    gLastIdDigest = 0;
+    RankTable rt;
+    HCCL_CHK(LoadForRank(clusterInfo, rank, &rt));
+    const uint32_t n = static_cast<uint32_t>(rt.ranks.size());
+    std::string host;
+    uint16_t port = 0;
+    HCCL_CHK(RootAddress(rt, &host, &port));
     HIP_CHK(hipSetDevice(rt.ranks[rank].device));
     char id[128] = {};
     if (rank == 0) HCCL_CHK(RcclGetUniqueId(id));
     HCCL_CHK(ExchangeUniqueId(host, port, n, rank, id));
+    gLastIdDigest = Fnv1a64(id, sizeof id);
+    gLastStage = 1;
     auto c = std::make_unique<Comm>();
     c->rank = rank;
     c->nRanks = n;
@@ -459,6 +520,8 @@ extern "C" HcclResult HcclCommInitClusterInfo(const char* clusterInfo, uint32_t 
     HcclResult err = HCCL_SUCCESS;
     c->transport = MakeRcclTransport(id, n, rank, &err);
     if (c->transport == nullptr) return err == HCCL_SUCCESS ? HCCL_E_INTERNAL : err;
+    HCCL_CHK(c->StartWatchdog());
+    gLastStage = 2;
     *comm = c.release();
     return HCCL_SUCCESS;
 }
@@ -487,7 +550,8 @@ extern "C" HcclResult HcclCommInitAll(uint32_t ndev, int32_t* devices, HcclComm*
     HCCL_CHK(MakeRcclTransportsAll(ndev, devices, &transports));
     for (uint32_t r = 0; r < ndev; ++r) {
         made[r]->transport = std::move(transports[r]);
-        comms[r] = made[r].release();
+        HCCL_CHK(made[r]->StartWatchdog());
     }
+    for (uint32_t r = 0; r < ndev; ++r) comms[r] = made[r].release();
     return HCCL_SUCCESS;
 }

@@ -102,21 +102,51 @@ HcclResult Comm::Gate()
     return e;
 }
 
+HcclResult Comm::StartWatchdog()
+{
+    if (transport == nullptr || !transport->Abortable()) return HCCL_SUCCESS;
+    const char* e = std::getenv("HCCL_AMD_INJECT_STALL_GROUP");
+    if (e != nullptr && *e != '\0') {
+        stallAtGroup = std::strtoull(e, nullptr, 10);
+        if (stallAtGroup != 0) {
+            HIP_CHK(hipHostMalloc(reinterpret_cast<void**>(&stallHost), 64,
+                                  hipHostMallocCoherent | hipHostMallocMapped));
+            HIP_CHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&stallDev), stallHost, 0));
+            *stallHost = 0;
+        }
+    }
+    const uint64_t bound = RcclExecTimeoutMs();
+    if (bound != 0) watchdog = std::make_unique<Watchdog>(this, bound);
+    return HCCL_SUCCESS;
+}
+
+// Teardown order (each step time-stamped on stderr with HCCL_AMD_TEARDOWN_TRACE=1): drain the communicator's streams
+// while the watchdog still runs (a lost peer is aborted past the bound, so the drain ends), stop the watchdog, release
+// the IPC mappings (collective), then RCCL (ncclCommFinalize bounded by the execution timeout, else ncclCommAbort).
 Comm::~Comm()
 {
     magic = 0;
     if (commStream != nullptr || reduceStream != nullptr) {
         (void)hipSetDevice(device);
     }
+    TeardownTrace(rank, "sync link stream", true);
     if (commStream != nullptr) (void)hipStreamSynchronize(commStream);
+    TeardownTrace(rank, "sync reduce stream", true);
     if (reduceStream != nullptr) (void)hipStreamSynchronize(reduceStream);
+    TeardownTrace(rank, "stop watchdog", true);
+    watchdog.reset();
+    TeardownTrace(rank, "IPC quiesce + release", true);
     IpcQuiesce(*this);
     IpcRelease(*this);
+    TeardownTrace(rank, "transport teardown", true);
     transport.reset();
+    TeardownTrace(rank, "events, staging, streams", true);
     for (hipEvent_t e : events) (void)hipEventDestroy(e);
     if (scratch != nullptr) (void)hipFree(scratch);
     if (commStream != nullptr) (void)hipStreamDestroy(commStream);
     if (reduceStream != nullptr) (void)hipStreamDestroy(reduceStream);
+    if (stallHost != nullptr) (void)hipHostFree(stallHost);
+    TeardownTrace(rank, "done", false);
 }
 
 // ------------------------------------------------------------------------------------------------ RCCL transport
@@ -136,54 +166,149 @@ HcclResult FromNccl(ncclResult_t r, const char* what)
     }
 }
 
+// HCCL_AMD_RCCL_BLOCKING=1 creates blocking RCCL communicators (the pre-r03 behaviour; diagnostics). By default they
+// are non-blocking (ncclConfig_t::blocking = 0): a call that must wait for a peer (communicator set-up, the first
+// message to a peer, finalize) returns ncclInProgress and the wait is ours to bound, where a blocking call would hang
+// the host on a lost peer.
+bool RcclBlocking()
+{
+    const char* e = std::getenv("HCCL_AMD_RCCL_BLOCKING");
+    return e != nullptr && std::strcmp(e, "1") == 0;
+}
+
+// Polls a non-blocking communicator until the call that returned `r` has finished, at most boundMs (0 = no bound).
+// Returns ncclInProgress when the bound passed.
+ncclResult_t WaitSettled(ncclComm_t comm, ncclResult_t r, uint64_t boundMs)
+{
+    if (r != ncclInProgress) return r;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+        if (ncclCommGetAsyncError(comm, &r) != ncclSuccess) return ncclInternalError;
+        if (r != ncclInProgress) return r;
+        if (boundMs != 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(boundMs)) {
+            return ncclInProgress;
+        }
+        if (spin < 1000) {
+            std::this_thread::yield();
+        } else {
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+    }
+}
+
 class RcclTransport : public Transport {
 public:
-    ncclComm_t comm = nullptr;
+    explicit RcclTransport(ncclComm_t comm) : comm_(comm) {}
     ~RcclTransport() override
     {
-        if (comm != nullptr) (void)ncclCommDestroy(comm);
+        std::lock_guard<std::mutex> lk(mu_);
+        if (comm_ == nullptr) return;
+        // ncclCommFinalize flushes this rank's outstanding work; bounded like any other wait on a peer
+        ncclResult_t r = WaitSettled(comm_, ncclCommFinalize(comm_), RcclExecTimeoutMs());
+        if (r == ncclSuccess) {
+            (void)ncclCommDestroy(comm_);
+        } else {
+            HCCL_AMD_ERR("ncclCommFinalize: %s: aborting the communicator", ncclGetErrorString(r));
+            (void)ncclCommAbort(comm_);
+        }
+        comm_ = nullptr;
     }
     HcclResult Group(const std::vector<P2pOp>& ops, hipStream_t stream) override
     {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (comm_ == nullptr) return HCCL_E_SUSPENDING;  // aborted by the watchdog
         ncclResult_t r = ncclGroupStart();
         if (r != ncclSuccess) return FromNccl(r, "ncclGroupStart");
         for (const P2pOp& o : ops) {
-            r = o.isSend ? ncclSend(o.ptr, o.bytes, ncclUint8, static_cast<int>(o.peer), comm, stream)
-                         : ncclRecv(o.ptr, o.bytes, ncclUint8, static_cast<int>(o.peer), comm, stream);
-            if (r != ncclSuccess) {
+            r = o.isSend ? ncclSend(o.ptr, o.bytes, ncclUint8, static_cast<int>(o.peer), comm_, stream)
+                         : ncclRecv(o.ptr, o.bytes, ncclUint8, static_cast<int>(o.peer), comm_, stream);
+            if (r != ncclSuccess && r != ncclInProgress) {
                 (void)ncclGroupEnd();
                 return FromNccl(r, o.isSend ? "ncclSend" : "ncclRecv");
             }
         }
-        return FromNccl(ncclGroupEnd(), "ncclGroupEnd");
+        return Settle(ncclGroupEnd(), "ncclGroupEnd");
     }
     const char* Name() const override { return "rccl"; }
+    bool Abortable() const override { return true; }
+    void Abort() override
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        AbortLocked();
+    }
     HcclResult AsyncError() override
     {
+        // never waits behind a group being posted (HcclGetCommAsyncError is polled by watchdog threads)
+        std::unique_lock<std::mutex> lk(mu_, std::try_to_lock);
+        if (!lk.owns_lock() || comm_ == nullptr) return HCCL_SUCCESS;
         ncclResult_t a = ncclSuccess;
-        if (ncclCommGetAsyncError(comm, &a) != ncclSuccess) return HCCL_E_INTERNAL;
+        if (ncclCommGetAsyncError(comm_, &a) != ncclSuccess) return HCCL_E_INTERNAL;
         return (a == ncclSuccess || a == ncclInProgress) ? HCCL_SUCCESS : FromNccl(a, "RCCL asynchronous error");
     }
     HcclResult AllGatherHost(const void* mine, size_t bytes, void* all) override
     {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (comm_ == nullptr) return HCCL_E_SUSPENDING;
         int n = 0;
-        HcclResult r = FromNccl(ncclCommCount(comm, &n), "ncclCommCount");
+        HcclResult r = FromNccl(ncclCommCount(comm_, &n), "ncclCommCount");
         if (r != HCCL_SUCCESS) return r;
         void* d = nullptr;
         hipStream_t s = nullptr;
         HIP_CHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-        HIP_CHK(hipMalloc(&d, bytes * (size_t(n) + 1)));
-        char* dAll = static_cast<char*>(d) + bytes;
-        HIP_CHK(hipMemcpyAsync(d, mine, bytes, hipMemcpyHostToDevice, s));
-        r = FromNccl(ncclAllGather(d, dAll, bytes, ncclUint8, comm, s), "ncclAllGather");
-        if (r == HCCL_SUCCESS) {
-            HIP_CHK(hipMemcpyAsync(all, dAll, bytes * size_t(n), hipMemcpyDeviceToHost, s));
-            HIP_CHK(hipStreamSynchronize(s));
+        if (hipMalloc(&d, bytes * (size_t(n) + 1)) != hipSuccess) {
+            (void)hipStreamDestroy(s);
+            return HCCL_E_MEMORY;
         }
+        char* dAll = static_cast<char*>(d) + bytes;
+        r = hipMemcpyAsync(d, mine, bytes, hipMemcpyHostToDevice, s) == hipSuccess ? HCCL_SUCCESS : HCCL_E_RUNTIME;
+        if (r == HCCL_SUCCESS) r = Settle(ncclAllGather(d, dAll, bytes, ncclUint8, comm_, s), "ncclAllGather");
+        if (r == HCCL_SUCCESS) {
+            r = hipMemcpyAsync(all, dAll, bytes * size_t(n), hipMemcpyDeviceToHost, s) == hipSuccess ? HCCL_SUCCESS
+                                                                                                   : HCCL_E_RUNTIME;
+        }
+        if (r == HCCL_SUCCESS) {
+            // a host-side wait on peers: bounded by the execution timeout like the device-side ones
+            const uint64_t bound = RcclExecTimeoutMs();
+            const auto t0 = std::chrono::steady_clock::now();
+            hipError_t q;
+            while ((q = hipStreamQuery(s)) == hipErrorNotReady) {
+                if (bound != 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(bound)) {
+                    HCCL_AMD_ERR("host all-gather over RCCL ran past HCCL_EXEC_TIMEOUT: aborting the communicator");
+                    AbortLocked();
+                    (void)hipStreamSynchronize(s);  // the aborted all-gather returns
+                    q = hipSuccess;
+                    r = HCCL_E_TIMEOUT;
+                    break;
+                }
+                std::this_thread::sleep_for(std::chrono::microseconds(20));
+            }
+            if (q != hipSuccess) r = HCCL_E_RUNTIME;
+        }
+        (void)hipStreamSynchronize(s);
         (void)hipFree(d);
         (void)hipStreamDestroy(s);
         return r;
     }
+
+private:
+    HcclResult Settle(ncclResult_t r, const char* what)  // mu_ held
+    {
+        r = WaitSettled(comm_, r, RcclExecTimeoutMs());
+        if (r == ncclInProgress) {
+            HCCL_AMD_ERR("%s did not complete within HCCL_EXEC_TIMEOUT: aborting the communicator", what);
+            AbortLocked();
+            return HCCL_E_TIMEOUT;
+        }
+        return FromNccl(r, what);
+    }
+    void AbortLocked()
+    {
+        if (comm_ == nullptr) return;
+        (void)ncclCommAbort(comm_);  // RCCL's kernels of this communicator see the abort flag and return
+        comm_ = nullptr;
+    }
+    std::mutex mu_;
+    ncclComm_t comm_;
 };
 
 }  // namespace
@@ -200,30 +325,62 @@ HcclResult RcclGetUniqueId(void* id128)
 
 std::unique_ptr<Transport> MakeRcclTransport(void* uniqueId, uint32_t nRanks, uint32_t rank, HcclResult* err)
 {
-    auto t = std::make_unique<RcclTransport>();
     ncclUniqueId id;
     std::memcpy(&id, uniqueId, sizeof id);
-    *err = FromNccl(ncclCommInitRank(&t->comm, static_cast<int>(nRanks), id, static_cast<int>(rank)),
-                    "ncclCommInitRank");
-    if (*err != HCCL_SUCCESS) {
-        t->comm = nullptr;
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = RcclBlocking() ? 1 : 0;
+    ncclComm_t comm = nullptr;
+    ncclResult_t r = ncclCommInitRankConfig(&comm, static_cast<int>(nRanks), id, static_cast<int>(rank), &cfg);
+    if (comm != nullptr) r = WaitSettled(comm, r, ConnectTimeoutMs());
+    if (r == ncclInProgress) {
+        HCCL_AMD_ERR("ncclCommInitRankConfig: rank %u of %u: not every rank joined within the connect timeout", rank,
+                     nRanks);
+        (void)ncclCommAbort(comm);
+        *err = HCCL_E_TIMEOUT;
         return nullptr;
     }
-    return t;
+    *err = FromNccl(r, "ncclCommInitRankConfig");
+    if (*err != HCCL_SUCCESS) {
+        if (comm != nullptr) (void)ncclCommAbort(comm);
+        return nullptr;
+    }
+    return std::make_unique<RcclTransport>(comm);
 }
 
 HcclResult MakeRcclTransportsAll(uint32_t ndev, const int32_t* devices, std::vector<std::unique_ptr<Transport>>* out)
 {
+    // ncclCommInitAll's steps, with the communicators' config: one unique id, ncclCommInitRankConfig per device in a
+    // group.
+    ncclUniqueId id;
+    HCCL_CHK(FromNccl(ncclGetUniqueId(&id), "ncclGetUniqueId"));
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = RcclBlocking() ? 1 : 0;
     std::vector<ncclComm_t> comms(ndev, nullptr);
-    std::vector<int> devs(devices, devices + ndev);
-    HcclResult r = FromNccl(ncclCommInitAll(comms.data(), static_cast<int>(ndev), devs.data()), "ncclCommInitAll");
-    if (r != HCCL_SUCCESS) return r;
-    out->clear();
-    for (uint32_t i = 0; i < ndev; ++i) {
-        auto t = std::make_unique<RcclTransport>();
-        t->comm = comms[i];
-        out->push_back(std::move(t));
+    int dev0 = 0;
+    HIP_CHK(hipGetDevice(&dev0));
+    ncclResult_t r = ncclGroupStart();
+    for (uint32_t i = 0; i < ndev && r == ncclSuccess; ++i) {
+        if (hipSetDevice(devices[i]) != hipSuccess) {
+            r = ncclInvalidArgument;
+            break;
+        }
+        r = ncclCommInitRankConfig(&comms[i], static_cast<int>(ndev), id, static_cast<int>(i), &cfg);
+        if (r == ncclInProgress) r = ncclSuccess;
     }
+    ncclResult_t e = ncclGroupEnd();
+    (void)hipSetDevice(dev0);
+    if (r == ncclSuccess) r = e == ncclInProgress ? ncclSuccess : e;
+    for (uint32_t i = 0; i < ndev && r == ncclSuccess; ++i) {
+        if (comms[i] != nullptr) r = WaitSettled(comms[i], ncclInProgress, ConnectTimeoutMs());
+    }
+    if (r != ncclSuccess) {
+        for (ncclComm_t c : comms) {
+            if (c != nullptr) (void)ncclCommAbort(c);
+        }
+        return r == ncclInProgress ? HCCL_E_TIMEOUT : FromNccl(r, "ncclCommInitRankConfig (all devices)");
+    }
+    out->clear();
+    for (uint32_t i = 0; i < ndev; ++i) out->push_back(std::make_unique<RcclTransport>(comms[i]));
     return HCCL_SUCCESS;
 }
 

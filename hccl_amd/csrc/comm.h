@@ -7,10 +7,12 @@
 #pragma once
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "internal.h"
@@ -42,6 +44,11 @@ public:
     // An asynchronous failure of the transport (RCCL: ncclCommGetAsyncError), HCCL_SUCCESS if none. Non-blocking and
     // callable from any thread.
     virtual HcclResult AsyncError() { return HCCL_SUCCESS; }
+    // True when a lost peer can leave this transport's device work waiting forever (RCCL): such a communicator keeps a
+    // watchdog (Watchdog) that aborts it past HCCL_EXEC_TIMEOUT.
+    virtual bool Abortable() const { return false; }
+    // ncclCommAbort: in-flight device work returns, later groups fail. Callable from any thread.
+    virtual void Abort() {}
     // Loopback world: the pinned failure word all its ranks share (the world's single IPC launch writes it), owned by
     // the world so that it outlives every rank's communicator; *dev receives its device address. nullptr elsewhere.
     virtual uint32_t* SharedFailWord(uint32_t** dev)
@@ -86,6 +93,70 @@ struct CompiledSchedule {
     uint64_t lastUse = 0;
 };
 
+struct Comm;
+
+// HCCL_EXEC_TIMEOUT for the RCCL path in ms (0 = never; default 1836 s), and the bound of communicator set-up
+// (HCCL_CONNECT_TIMEOUT + 20 s); watchdog.cc.
+uint64_t RcclExecTimeoutMs();
+uint64_t ConnectTimeoutMs();
+
+// The execution bound of a communicator whose transport is Abortable (watchdog.cc has the contract). Begin records a
+// start event on the caller's stream before the collective's work, Commit a completion event after it; the watchdog
+// thread aborts the transport once a started collective has not completed within the bound.
+class Watchdog {
+public:
+    struct Ticket {
+        hipEvent_t start = nullptr;
+        hipEvent_t done = nullptr;
+        hipStream_t stream = nullptr;
+    };
+    Watchdog(Comm* c, uint64_t boundMs);
+    ~Watchdog();
+    Watchdog(const Watchdog&) = delete;
+    Watchdog& operator=(const Watchdog&) = delete;
+    HcclResult Begin(hipStream_t s, Ticket* t);
+    void Commit(Ticket* t);
+
+private:
+    struct Entry {
+        hipEvent_t start;
+        hipEvent_t done;
+        bool started;
+        std::chrono::steady_clock::time_point t0;
+    };
+    HcclResult Take(hipEvent_t* e);
+    void Run();
+    void Fire(HcclResult why);
+    Comm* c_;
+    uint64_t boundMs_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<Entry> pending_;
+    std::vector<hipEvent_t> free_;
+    bool stop_ = false;
+    bool fired_ = false;
+    std::thread th_;
+};
+
+// Brackets one collective's work with the watchdog's events (nothing when wd is null or the stream is capturing).
+class WatchScope {
+public:
+    WatchScope(Watchdog* wd, hipStream_t s) : wd_(wd)
+    {
+        if (wd_ != nullptr && wd_->Begin(s, &t_) != HCCL_SUCCESS) wd_ = nullptr;
+    }
+    ~WatchScope()
+    {
+        if (wd_ != nullptr) wd_->Commit(&t_);
+    }
+    WatchScope(const WatchScope&) = delete;
+    WatchScope& operator=(const WatchScope&) = delete;
+
+private:
+    Watchdog* wd_;
+    Watchdog::Ticket t_;
+};
+
 struct Comm {
     uint32_t magic = 0x48434C41;  // "HCLA"
     uint32_t rank = 0;
@@ -119,6 +190,20 @@ struct Comm {
     bool failed = false;
     std::atomic<int32_t> failCode{HCCL_SUCCESS};
     std::atomic<const volatile uint32_t*> failWord{nullptr};  // the pinned word the IPC launches set on a timeout
+    std::unique_ptr<Watchdog> watchdog;  // RCCL transports: the execution bound (watchdog.cc)
+
+    // Graphs captured on this communicator that are still alive (NoteCapture); HcclCommDestroy defers the teardown
+    // until they are gone (DeferDestroy).
+    std::atomic<int32_t> graphRefs{0};
+    unsigned long long lastCaptureId = 0;
+
+    // Fault injection for the timeout tests (HCCL_AMD_INJECT_STALL_GROUP=k): before the k-th transport group the link
+    // stream runs a kernel that waits on this pinned word, as an RCCL kernel waits for a lost peer's message. The
+    // watchdog's abort sets the word; the kernel also gives up by itself after a minute.
+    uint64_t stallAtGroup = 0;
+    uint64_t groupsPosted = 0;
+    uint32_t* stallHost = nullptr;
+    uint32_t* stallDev = nullptr;
 
     // Compiled collectives, least recently used evicted (a training loop repeats the same few bucket calls: they skip
     // BuildSchedule and PlanUnits after the first). HCCL_AMD_PLAN_CACHE=0 compiles every call.
@@ -128,6 +213,8 @@ struct Comm {
     uint64_t compileMisses = 0;
 
     HcclResult Init(int dev);
+    // After the transport is set: the watchdog for an Abortable transport and the fault-injection hook.
+    HcclResult StartWatchdog();
     HcclResult NextEvent(hipEvent_t* e);
     // Non-blocking, lock-free: the first asynchronous error seen on this communicator, HCCL_SUCCESS if none.
     HcclResult PollAsyncError();
@@ -166,6 +253,17 @@ void IpcQuiesce(Comm& c);
 void IpcRelease(Comm& c);
 
 Comm* AsComm(HcclComm c);
+
+// Called at every collective entry with the caller's stream: under capture, counts the capturing graph against the
+// communicator until the graph is destroyed (once per capture).
+HcclResult NoteCapture(Comm& c, hipStream_t s);
+// HcclCommDestroy while graphs hold the communicator: queue it for the reaper thread and return true.
+bool DeferDestroy(Comm* c);
+uint32_t PendingDestroys();
+// HCCL_AMD_TEARDOWN_TRACE=1: time-stamped steps of ~Comm on stderr.
+void TeardownTrace(uint32_t rank, const char* step, bool begin);
+// The injected stall kernel (fault_inject.hip).
+HcclResult LaunchStall(const uint32_t* word, uint64_t maxMs, hipStream_t stream);
 
 // HCCL_BUFFSIZE (MB, default 200) in bytes; staging per communicator is twice that. Must be equal on every rank: the
 // executor loops and the pipelining granule are derived from it.

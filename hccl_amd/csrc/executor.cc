@@ -11,12 +11,63 @@
 // This is the reference ST's memory-conflict rule (test/st/algorithm/.../mem_conflict_check) turned into the
 // synchronisation itself. The host never blocks (except loopback rendezvous); the user stream is joined at the end.
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <climits>
 #include <cstring>
 
 #include "comm.h"
 
 namespace hccl_amd {
+
+// ------------------------------------------------------------------------------------------------ host profile
+
+// HCCL_AMD_HOST_PROFILE=1: host time of Execute by category (HcclAmdHostProfile), for the breakdown of the RCCL path's
+// enqueue cost. Off by default: one cached flag test per site.
+namespace {
+
+struct HostProfile {
+    std::atomic<uint64_t> ns[HCCL_AMD_HP_COUNT];
+    std::atomic<uint64_t> calls[HCCL_AMD_HP_COUNT];
+};
+
+HostProfile& Hp()
+{
+    static HostProfile p{};
+    return p;
+}
+
+bool HpOn()
+{
+    static const bool on = [] {
+        const char* e = std::getenv("HCCL_AMD_HOST_PROFILE");
+        return e != nullptr && std::strcmp(e, "1") == 0;
+    }();
+    return on;
+}
+
+class HpScope {
+public:
+    explicit HpScope(int cat) : cat_(HpOn() ? cat : -1)
+    {
+        if (cat_ >= 0) t0_ = std::chrono::steady_clock::now();
+    }
+    ~HpScope()
+    {
+        if (cat_ < 0) return;
+        const auto ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0_);
+        Hp().ns[cat_].fetch_add(static_cast<uint64_t>(ns.count()), std::memory_order_relaxed);
+        Hp().calls[cat_].fetch_add(1, std::memory_order_relaxed);
+    }
+    HpScope(const HpScope&) = delete;
+    HpScope& operator=(const HpScope&) = delete;
+
+private:
+    int cat_;
+    std::chrono::steady_clock::time_point t0_;
+};
+
+}  // namespace
 
 namespace {
 
@@ -92,12 +143,22 @@ HcclResult LaunchFolds(const std::vector<HcclAmdIrOp>& ops, size_t i, size_t m, 
     return LaunchReduceNBatch(segs, static_cast<uint32_t>(m), static_cast<uint32_t>(ops[i].nsrc), dt, op, stream);
 }
 
+// HCCL_AMD_INJECT_STALL_GROUP=k (timeout tests): before the communicator's k-th transport group, outside capture, the
+// group's stream waits on the injected stall kernel, as if the peer never posted its half of the group.
+HcclResult MaybeInjectStall(Comm& c, hipStream_t s)
+{
+    if (c.stallAtGroup == 0 || ++c.groupsPosted != c.stallAtGroup) return HCCL_SUCCESS;
+    HCCL_AMD_ERR("rank %u: injected stall before transport group %llu (HCCL_AMD_INJECT_STALL_GROUP)", c.rank,
+                 (unsigned long long)c.groupsPosted);
+    return LaunchStall(c.stallDev, 60000, s);
+}
+
 }  // namespace
 
 // Small collectives have one pipeline piece, so the two-stream split cannot overlap anything: every unit goes on
 // the caller's stream in program order and no event is recorded or waited on (the latency floor of C5).
 static HcclResult ExecuteSingleStream(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const bufs[3],
-                                      HcclDataType dt, HcclReduceOp op, hipStream_t user)
+                                      HcclDataType dt, HcclReduceOp op, hipStream_t user, bool captured)
 {
     const uint64_t es = DataTypeSize(dt);
     auto addr = [&](int32_t buf, uint64_t off) -> uintptr_t {
@@ -118,14 +179,18 @@ static HcclResult ExecuteSingleStream(Comm& c, const std::vector<HcclAmdIrOp>& o
                 p2p.push_back({send, static_cast<uint32_t>(q.peer), reinterpret_cast<void*>(a), q.count * es});
                 ++i;
             }
+            if (!captured) HCCL_CHK(MaybeInjectStall(c, user));
+            HpScope hp(HCCL_AMD_HP_GROUP);
             HCCL_CHK(c.transport->Group(p2p, user));
             continue;
         }
         void* dst = reinterpret_cast<void*>(addr(o.dstBuf, o.dstOff));
         if (o.kind == HCCL_AMD_IR_COPY) {
+            HpScope hp(HCCL_AMD_HP_COPY);
             const void* src = reinterpret_cast<const void*>(addr(o.srcBuf[0], o.srcOff[0]));
             if (src != dst) HIP_CHK(hipMemcpyAsync(dst, src, o.count * es, hipMemcpyDeviceToDevice, user));
         } else if (o.kind == HCCL_AMD_IR_REDUCE) {
+            HpScope hp(HCCL_AMD_HP_FOLD);
             const size_t m = BatchRun(ops, i, es, bufs);
             HCCL_CHK(LaunchFolds(ops, i, m, es, bufs, dt, op, user));
             i += m;
@@ -296,7 +361,11 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
     // A loopback world meets its peers through host rendezvous and events exchanged between threads on every group,
     // which a graph cannot replay: refused under capture, before anything is enqueued (every rank alike).
     if (captured && c.transport->SharedDevice()) return HCCL_E_NOT_SUPPORT;
-    if (singleStream) return ExecuteSingleStream(c, ops, bufs, dt, op, user);
+    // The execution bound (watchdog.cc): this call's work on `user`, bracketed by the watchdog's events. A captured
+    // call runs later, from a graph, outside any entry: not tracked.
+    HpScope hpTotal(HCCL_AMD_HP_EXECUTE);
+    WatchScope watch(captured ? nullptr : c.watchdog.get(), user);
+    if (singleStream) return ExecuteSingleStream(c, ops, bufs, dt, op, user, captured);
     const uint64_t es = DataTypeSize(dt);
     // Under stream capture the transport groups go on the capturing stream itself and only the folds on a forked
     // stream: an RCCL group captured on a stream joined to the capture (rather than its origin) brought down graph
@@ -315,7 +384,10 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
     };
 
     std::vector<UnitPlan> fresh;
-    if (cached == nullptr) fresh = PlanUnits(ops, bufs, es);
+    if (cached == nullptr) {
+        HpScope hp(HCCL_AMD_HP_PLAN);
+        fresh = PlanUnits(ops, bufs, es);
+    }
     const std::vector<UnitPlan>& plan = cached != nullptr ? *cached : fresh;
     std::vector<hipEvent_t> evs(plan.size(), nullptr);
     bool used[2] = {false, false};
@@ -323,7 +395,10 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
     for (size_t ui = 0; ui < plan.size(); ++ui) {
         const UnitPlan& u = plan[ui];
         const int x = u.stream;
-        if (u.waitUnit >= 0) HIP_CHK(hipStreamWaitEvent(streams[x], evs[size_t(u.waitUnit)], 0));
+        if (u.waitUnit >= 0) {
+            HpScope hp(HCCL_AMD_HP_WAIT);
+            HIP_CHK(hipStreamWaitEvent(streams[x], evs[size_t(u.waitUnit)], 0));
+        }
         if (u.isComm) {
             p2p.clear();
             for (size_t k = u.first; k < u.first + u.count; ++k) {
@@ -332,10 +407,13 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
                 const uintptr_t a = send ? addr(o.srcBuf[0], o.srcOff[0]) : addr(o.dstBuf, o.dstOff);
                 p2p.push_back({send, static_cast<uint32_t>(o.peer), reinterpret_cast<void*>(a), o.count * es});
             }
+            if (!captured) HCCL_CHK(MaybeInjectStall(c, streams[x]));
+            HpScope hp(HCCL_AMD_HP_GROUP);
             HCCL_CHK(c.transport->Group(p2p, streams[x]));
         } else {
             const HcclAmdIrOp& o = ops[u.first];
             void* dst = reinterpret_cast<void*>(addr(o.dstBuf, o.dstOff));
+            HpScope hp(o.kind == HCCL_AMD_IR_COPY ? HCCL_AMD_HP_COPY : HCCL_AMD_HP_FOLD);
             if (o.kind == HCCL_AMD_IR_COPY) {
                 const void* src = reinterpret_cast<const void*>(addr(o.srcBuf[0], o.srcOff[0]));
                 if (src != dst) {
@@ -347,8 +425,11 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
                 return HCCL_E_INTERNAL;
             }
         }
-        HCCL_CHK(c.NextEvent(&evs[ui]));
-        HIP_CHK(hipEventRecord(evs[ui], streams[x]));
+        {
+            HpScope hp(HCCL_AMD_HP_RECORD);
+            HCCL_CHK(c.NextEvent(&evs[ui]));
+            HIP_CHK(hipEventRecord(evs[ui], streams[x]));
+        }
         used[x] = true;
     }
 
@@ -364,3 +445,19 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
 }
 
 }  // namespace hccl_amd
+
+extern "C" HcclResult HcclAmdHostProfile(uint64_t* ns, uint64_t* calls, uint32_t n, int32_t reset)
+{
+    using hccl_amd::Hp;
+    for (uint32_t i = 0; i < n && i < HCCL_AMD_HP_COUNT; ++i) {
+        if (ns != nullptr) ns[i] = Hp().ns[i].load();
+        if (calls != nullptr) calls[i] = Hp().calls[i].load();
+    }
+    if (reset != 0) {
+        for (uint32_t i = 0; i < HCCL_AMD_HP_COUNT; ++i) {
+            Hp().ns[i] = 0;
+            Hp().calls[i] = 0;
+        }
+    }
+    return HCCL_SUCCESS;
+}

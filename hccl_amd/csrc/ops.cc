@@ -82,6 +82,7 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     std::lock_guard<std::mutex> lk(c.mu);
     HCCL_CHK(c.Gate());  // a failed communicator takes no more work (op_common.cc:89-97)
     HIP_CHK(hipSetDevice(c.device));
+    HCCL_CHK(NoteCapture(c, stream));
     const uint32_t es = DataTypeSize(dt);
     if (c.nRanks == 1) {
         // SingleRankProc (op_common.cc:3042-3098): copy in -> out unless they are the same buffer.
@@ -187,6 +188,7 @@ HcclResult RunReduceScatterV(Comm& c, void* sendBuf, const uint64_t* counts, con
     std::lock_guard<std::mutex> lk(c.mu);
     HCCL_CHK(c.Gate());
     HIP_CHK(hipSetDevice(c.device));
+    HCCL_CHK(NoteCapture(c, stream));
     // ReduceScatterVAutoSelector::SelectAicpuAlgo (reduce_scatter_v_auto_selector.cc:180-197): UINT64 and FP64 have
     // no algorithm
     if (dt == HCCL_DATA_TYPE_UINT64 || dt == HCCL_DATA_TYPE_FP64) return HCCL_E_NOT_SUPPORT;
@@ -362,6 +364,7 @@ HcclResult HcclCommInitRootInfo(uint32_t nRanks, const HcclRootInfo* rootInfo, u
     HcclResult err = HCCL_SUCCESS;
     c->transport = MakeRcclTransport(const_cast<char*>(rootInfo->internal + 8), nRanks, rank, &err);
     if (c->transport == nullptr) return err == HCCL_SUCCESS ? HCCL_E_INTERNAL : err;
+    HCCL_CHK(c->StartWatchdog());
     *comm = c.release();
     return HCCL_SUCCESS;
 }
@@ -370,6 +373,10 @@ HcclResult HcclCommDestroy(HcclComm comm)
 {
     Comm* c = AsComm(comm);
     if (c == nullptr) return HCCL_E_PTR;
+    c->magic = 0;  // no further use through this handle, whether torn down now or later
+    // A graph captured on this communicator still holds its staging and RCCL plans, and ncclCommDestroy would wait
+    // for that graph to be destroyed: the teardown then runs when the last such graph goes (watchdog.cc).
+    if (DeferDestroy(c)) return HCCL_SUCCESS;
     delete c;
     return HCCL_SUCCESS;
 }
@@ -518,6 +525,7 @@ HcclResult HcclAmdCommExecute(HcclComm comm, const HcclAmdIrOp* ops, uint64_t nu
     }
     HCCL_CHK(c->Gate());
     HIP_CHK(hipSetDevice(c->device));
+    HCCL_CHK(NoteCapture(*c, static_cast<hipStream_t>(stream)));
     const std::vector<HcclAmdIrOp> prog(ops, ops + numOps);
     void* bufs[3] = {sendBuf, recvBuf, c->scratch};
     return Execute(*c, prog, bufs, dataType, op, static_cast<hipStream_t>(stream), singleStream != 0);

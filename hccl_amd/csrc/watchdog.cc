@@ -1,0 +1,345 @@
+// watchdog.cc — the execution bound of the RCCL path, graph references of a communicator, deferred destroy.
+//
+// The reference bounds every handshake wait of its write/read-reduce steps by HCCL_EXEC_TIMEOUT
+// (HcommChannelNotifyWaitOnThread(..., execTimeout), alg_data_trans_wrapper.cc:258-268, 284-286; the bound from
+// ExecTimeoutManager, exec_timeout_manager.cc:30-44, default CUSTOM_TIMEOUT = 1836 s, alg_param.h:79), and a failed
+// communicator takes no more work (Selector, op_common.cc:89-97). On this path the waits are inside RCCL's send/recv
+// kernels, which poll until the peer's matching message arrives. A communicator therefore keeps a watchdog thread:
+//   * every collective it runs outside stream capture is bracketed by two events on the caller's stream;
+//   * once the first has completed (the collective's work has started on the GPU), the second must complete within
+//     the bound; the thread also polls ncclCommGetAsyncError;
+//   * past the bound, or on an asynchronous RCCL error, it records the error (HcclGetCommAsyncError reports it at
+//     once), calls ncclCommAbort (RCCL's kernels poll the abort flag and return), and the communicator is failed:
+//     the next collective entry returns the error (HCCL_E_TIMEOUT), every later one HCCL_E_SUSPENDING (Comm::Gate).
+// This is the contract the one-sided IPC kernel already has with its in-kernel bound (ipc.cc IpcTimeoutTicks).
+//
+// Graph references. A HIP graph captured on a communicator's collective holds the communicator's staging, streams
+// and RCCL plans. RCCL's ncclCommDestroy waits until every graph holding one of its plans is destroyed, so destroying
+// a communicator while such a graph is alive did not return. Each capture now
+// retains a HIP user object on the capturing graph that counts the graph against the communicator, and
+// HcclCommDestroy of a communicator with live graphs returns at once: the teardown runs on a reaper thread when the
+// last such graph is destroyed (and never, if the process exits first).
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <thread>
+
+#include "comm.h"
+
+namespace hccl_amd {
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+// Non-negative integer from the environment, or dflt when unset / malformed.
+bool EnvMs(const char* name, uint64_t lo, uint64_t hi, uint64_t* out)
+{
+    const char* e = std::getenv(name);
+    if (e == nullptr || *e == '\0') return false;
+    char* end = nullptr;
+    const unsigned long long v = std::strtoull(e, &end, 10);
+    if (end == e || *end != '\0' || v < lo || v > hi) return false;
+    *out = v;
+    return true;
+}
+
+bool EnvFlag(const char* name, bool dflt)
+{
+    const char* e = std::getenv(name);
+    if (e == nullptr || *e == '\0') return dflt;
+    return std::strcmp(e, "0") != 0;
+}
+
+}  // namespace
+
+uint64_t RcclExecTimeoutMs()
+{
+    // HCCL_EXEC_TIMEOUT in the reference's AI_CPU-mode rule (docs/zh/user_guide/hccl_env/HCCL_EXEC_TIMEOUT.md:
+    // seconds, [0, 2147483647], default 1836, 0 = never), parsed with ParseExecTimeout's format check
+    // (alg_env_config.cc:43-110). HCCL_AMD_EXEC_TIMEOUT_MS (0 .. 2^40) overrides it for tests.
+    uint64_t ms = 0;
+    if (EnvMs("HCCL_AMD_EXEC_TIMEOUT_MS", 0, 1ull << 40, &ms)) return ms;
+    double sec = 0;
+    if (ParseExecTimeoutSeconds(std::getenv("HCCL_EXEC_TIMEOUT"), &sec) && sec <= 2147483647.0) {
+        return sec == 0 ? 0 : std::max<uint64_t>(1, static_cast<uint64_t>(sec * 1000.0 + 0.5));
+    }
+    return 1836ull * 1000;
+}
+
+uint64_t ConnectTimeoutMs()
+{
+    // HCCL_CONNECT_TIMEOUT (docs/zh/user_guide/hccl_env/HCCL_CONNECT_TIMEOUT.md: seconds, [120, 7200], default 120)
+    // plus 20 s of slack for the slowest rank's start; HCCL_AMD_CONNECT_TIMEOUT_MS overrides it for tests.
+    uint64_t ms = 0;
+    if (EnvMs("HCCL_AMD_CONNECT_TIMEOUT_MS", 1, 1ull << 40, &ms)) return ms;
+    uint64_t s = 120;
+    (void)EnvMs("HCCL_CONNECT_TIMEOUT", 120, 7200, &s);  // out of range or malformed: the default
+    return (s + 20) * 1000;
+}
+
+// ------------------------------------------------------------------------------------------------ teardown trace
+
+bool TeardownTraceEnabled()
+{
+    static const bool on = EnvFlag("HCCL_AMD_TEARDOWN_TRACE", false);
+    return on;
+}
+
+void TeardownTrace(uint32_t rank, const char* step, bool begin)
+{
+    if (!TeardownTraceEnabled()) return;
+    static const Clock::time_point t0 = Clock::now();
+    const double ms = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+    std::fprintf(stderr, "[hccl_amd] teardown rank %u: %-26s %-5s +%.3f ms\n", rank, step, begin ? "begin" : "end",
+                 ms);
+    std::fflush(stderr);
+}
+
+// ------------------------------------------------------------------------------------------------ watchdog
+
+Watchdog::Watchdog(Comm* c, uint64_t boundMs) : c_(c), boundMs_(boundMs)
+{
+    th_ = std::thread([this] { Run(); });
+}
+
+Watchdog::~Watchdog()
+{
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        stop_ = true;
+    }
+    cv_.notify_all();
+    if (th_.joinable()) th_.join();
+    for (Entry& e : pending_) {
+        (void)hipEventDestroy(e.start);
+        (void)hipEventDestroy(e.done);
+    }
+    for (hipEvent_t e : free_) (void)hipEventDestroy(e);
+}
+
+HcclResult Watchdog::Take(hipEvent_t* e)
+{
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!free_.empty()) {
+            *e = free_.back();
+            free_.pop_back();
+            return HCCL_SUCCESS;
+        }
+    }
+    HIP_CHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    return HCCL_SUCCESS;
+}
+
+HcclResult Watchdog::Begin(hipStream_t s, Ticket* t)
+{
+    HCCL_CHK(Take(&t->start));
+    HCCL_CHK(Take(&t->done));
+    HIP_CHK(hipEventRecord(t->start, s));
+    t->stream = s;
+    return HCCL_SUCCESS;
+}
+
+void Watchdog::Commit(Ticket* t)
+{
+    if (t->stream == nullptr) return;
+    if (hipEventRecord(t->done, t->stream) != hipSuccess) {
+        HCCL_AMD_ERR("rank %u: watchdog could not record a completion event", c_->rank);
+        std::lock_guard<std::mutex> lk(mu_);
+        free_.push_back(t->start);
+        free_.push_back(t->done);
+        t->stream = nullptr;
+        return;
+    }
+    std::lock_guard<std::mutex> lk(mu_);
+    pending_.push_back({t->start, t->done, false, {}});
+    t->stream = nullptr;
+}
+
+void Watchdog::Run()
+{
+    (void)hipSetDevice(c_->device);
+    std::unique_lock<std::mutex> lk(mu_);
+    while (!stop_) {
+        // a 10 ms poll: no wake-up is paid per collective, and the bound is seconds
+        cv_.wait_for(lk, std::chrono::milliseconds(10), [&] { return stop_; });
+        if (stop_) break;
+        const Clock::time_point now = Clock::now();
+        bool overdue = false;
+        for (size_t i = 0; i < pending_.size();) {
+            Entry& e = pending_[i];
+            if (!e.started) {
+                const hipError_t q = hipEventQuery(e.start);
+                if (q == hipErrorNotReady) {
+                    ++i;
+                    continue;
+                }
+                e.started = true;
+                e.t0 = now;
+            }
+            const hipError_t q = hipEventQuery(e.done);
+            if (q != hipErrorNotReady) {
+                free_.push_back(e.start);
+                free_.push_back(e.done);
+                pending_.erase(pending_.begin() + static_cast<std::ptrdiff_t>(i));
+                continue;
+            }
+            if (!fired_ && boundMs_ != 0 &&
+                std::chrono::duration_cast<std::chrono::milliseconds>(now - e.t0).count() >
+                    static_cast<int64_t>(boundMs_)) {
+                overdue = true;
+            }
+            ++i;
+        }
+        if (fired_) continue;  // keep recycling events as the aborted work drains
+        HcclResult why = HCCL_SUCCESS;
+        if (overdue) {
+            why = HCCL_E_TIMEOUT;
+        } else if (!pending_.empty()) {
+            why = c_->transport != nullptr ? c_->transport->AsyncError() : HCCL_SUCCESS;
+        }
+        if (why == HCCL_SUCCESS) continue;
+        fired_ = true;
+        lk.unlock();
+        Fire(why);
+        lk.lock();
+    }
+}
+
+void Watchdog::Fire(HcclResult why)
+{
+    int32_t expected = HCCL_SUCCESS;
+    c_->failCode.compare_exchange_strong(expected, why, std::memory_order_acq_rel);
+    if (why == HCCL_E_TIMEOUT) {
+        HCCL_AMD_ERR("rank %u: a collective ran past HCCL_EXEC_TIMEOUT (%llu ms): aborting the RCCL communicator; "
+                     "the next collective returns HCCL_E_TIMEOUT, later ones HCCL_E_SUSPENDING",
+                     c_->rank, (unsigned long long)boundMs_);
+    } else {
+        HCCL_AMD_ERR("rank %u: RCCL reported an asynchronous error (%s): aborting the communicator", c_->rank,
+                     HcclAmdGetErrorString(why));
+    }
+    // The injected stall (HCCL_AMD_INJECT_STALL_GROUP) stands for an RCCL kernel waiting on a lost peer: it returns
+    // on the abort as RCCL's kernels do on their abort flag. It is released first, so that the RCCL kernels queued
+    // behind it have run before RCCL reclaims the communicator.
+    if (c_->stallHost != nullptr) __atomic_store_n(c_->stallHost, 1u, __ATOMIC_RELEASE);
+    if (c_->transport != nullptr) c_->transport->Abort();
+}
+
+// ------------------------------------------------------------------------------------------------ graph references
+
+namespace {
+
+// Communicators whose HcclCommDestroy came while graphs captured on them were alive: torn down by the reaper thread
+// once their last graph is destroyed. Allocated once and never freed (a graph may outlive main()).
+struct Reaper {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<Comm*> pending;
+    bool started = false;
+};
+
+Reaper& TheReaper()
+{
+    static Reaper* r = new Reaper();
+    return *r;
+}
+
+struct GraphRef {
+    Comm* comm;
+};
+
+// The user object's destructor: runs on a HIP-internal thread when the graph (and every executable instantiated from
+// it) is destroyed. No HIP call may be made here; it only counts down and wakes the reaper.
+void ReleaseGraphRef(void* p)
+{
+    GraphRef* ref = static_cast<GraphRef*>(p);
+    Reaper& r = TheReaper();
+    {
+        std::lock_guard<std::mutex> lk(r.mu);
+        ref->comm->graphRefs.fetch_sub(1, std::memory_order_acq_rel);
+    }
+    r.cv.notify_all();
+    delete ref;
+}
+
+void ReaperLoop()
+{
+    Reaper& r = TheReaper();
+    std::unique_lock<std::mutex> lk(r.mu);
+    for (;;) {
+        r.cv.wait(lk, [&] {
+            for (Comm* c : r.pending) {
+                if (c->graphRefs.load(std::memory_order_acquire) == 0) return true;
+            }
+            return false;
+        });
+        for (size_t i = 0; i < r.pending.size();) {
+            Comm* c = r.pending[i];
+            if (c->graphRefs.load(std::memory_order_acquire) != 0) {
+                ++i;
+                continue;
+            }
+            r.pending.erase(r.pending.begin() + static_cast<std::ptrdiff_t>(i));
+            lk.unlock();
+            TeardownTrace(c->rank, "deferred destroy (reaper)", true);
+            delete c;
+            lk.lock();
+        }
+    }
+}
+
+}  // namespace
+
+HcclResult NoteCapture(Comm& c, hipStream_t s)
+{
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    hipGraph_t g = nullptr;
+    HIP_CHK(hipStreamGetCaptureInfo_v2(s, &st, &id, &g, nullptr, nullptr));
+    if (st != hipStreamCaptureStatusActive || g == nullptr || id == c.lastCaptureId) return HCCL_SUCCESS;
+    GraphRef* ref = new GraphRef{&c};
+    hipUserObject_t obj = nullptr;
+    if (hipUserObjectCreate(&obj, ref, ReleaseGraphRef, 1, hipUserObjectNoDestructorSync) != hipSuccess) {
+        delete ref;
+        HCCL_AMD_ERR("rank %u: hipUserObjectCreate failed", c.rank);
+        return HCCL_E_RUNTIME;
+    }
+    c.graphRefs.fetch_add(1, std::memory_order_acq_rel);
+    if (hipGraphRetainUserObject(g, obj, 1, hipGraphUserObjectMove) != hipSuccess) {
+        (void)hipUserObjectRelease(obj, 1);  // runs ReleaseGraphRef: the count goes back
+        HCCL_AMD_ERR("rank %u: hipGraphRetainUserObject failed", c.rank);
+        return HCCL_E_RUNTIME;
+    }
+    c.lastCaptureId = id;
+    return HCCL_SUCCESS;
+}
+
+bool DeferDestroy(Comm* c)
+{
+    if (!EnvFlag("HCCL_AMD_DEFER_DESTROY", true)) return false;  // diagnostics: tear down at once, as before r03
+    Reaper& r = TheReaper();
+    std::lock_guard<std::mutex> lk(r.mu);
+    if (c->graphRefs.load(std::memory_order_acquire) == 0) return false;
+    TeardownTrace(c->rank, "destroy deferred (graphs)", true);
+    r.pending.push_back(c);
+    if (!r.started) {
+        r.started = true;
+        std::thread(ReaperLoop).detach();
+    }
+    r.cv.notify_all();
+    return true;
+}
+
+uint32_t PendingDestroys()
+{
+    Reaper& r = TheReaper();
+    std::lock_guard<std::mutex> lk(r.mu);
+    return static_cast<uint32_t>(r.pending.size());
+}
+
+}  // namespace hccl_amd
+
+extern "C" uint32_t HcclAmdCommPendingDestroys(void) { return hccl_amd::PendingDestroys(); }

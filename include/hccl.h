@@ -66,12 +66,19 @@ extern HcclResult HcclCommInitClusterInfo(const char* clusterInfo, uint32_t rank
 /* One communicator per listed device in this process (single-node batch creation); comms[i] is rank i on
  * devices[i]. Drive each rank from its own host thread. */
 extern HcclResult HcclCommInitAll(uint32_t ndev, int32_t* devices, HcclComm* comms);
+/* Destroys the communicator. Its outstanding work is flushed first (ncclCommFinalize, bounded by HCCL_EXEC_TIMEOUT;
+ * past it the communicator is aborted). If a HIP graph captured on a collective of this communicator is still alive,
+ * the call returns HCCL_SUCCESS at once and the teardown runs when the last such graph is destroyed: the graph holds
+ * the communicator's staging and RCCL plans (RCCL's own destroy would wait for the graph). The handle is invalid on
+ * return either way. */
 extern HcclResult HcclCommDestroy(HcclComm comm);
 extern HcclResult HcclGetRankSize(HcclComm comm, uint32_t* rankSize);
 extern HcclResult HcclGetRankId(HcclComm comm, uint32_t* rank);
 /* Asynchronous error of the communicator (CANN hccl_comm.h; polled by framework watchdogs such as torch_npu's
- * ProcessGroupHCCL). Non-blocking. *asyncError = HCCL_E_TIMEOUT after a one-sided barrier wait exceeded its bound
- * (HCCL_EXEC_TIMEOUT), the transport's error after an RCCL asynchronous failure, else HCCL_SUCCESS. Once the first
+ * ProcessGroupHCCL). Non-blocking. *asyncError = HCCL_E_TIMEOUT after a one-sided barrier wait exceeded its bound,
+ * or after a collective on the RCCL path ran past HCCL_EXEC_TIMEOUT once started (default 1836 s, 0 = never; the
+ * communicator's watchdog then aborts RCCL), the transport's error after an RCCL asynchronous failure, else
+ * HCCL_SUCCESS. Once the first
  * collective entry has observed such an error (and returned it), every later collective on the communicator returns
  * HCCL_E_SUSPENDING: the reference's status gate, src/ops/op_common/op_common.cc:89-97. */
 extern HcclResult HcclGetCommAsyncError(HcclComm comm, HcclResult* asyncError);

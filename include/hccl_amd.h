@@ -236,6 +236,32 @@ extern uint64_t HcclAmdIpcTimeoutMs(void);
  * device_id of `rank`. HCCL_E_PARA for a malformed table or a rank outside it. */
 extern HcclResult HcclAmdRankTableInfo(const char* clusterInfo, uint32_t rank, uint32_t* nRanks, int32_t* deviceId);
 
+/* The last HcclCommInitClusterInfo of this process: *stage = 0 (none, or it failed before the unique-id exchange
+ * completed), 1 (the transport's unique id was exchanged over TCP; *idDigest = FNV-1a 64 of the 128-byte id, the same
+ * on every rank of a good exchange), 2 (the RCCL communicator was then created). Diagnostics for bootstrap tests. */
+extern HcclResult HcclAmdLastBootstrap(uint64_t* idDigest, int32_t* stage);
+
+/* The rank-table TCP exchange alone (host only, no device): rank 0 serves the 128 bytes at id128 to every other
+ * rank of the table, which receive them into id128. Same addresses and bounds as HcclCommInitClusterInfo. */
+extern HcclResult HcclAmdBootstrapExchangeId(const char* clusterInfo, uint32_t rank, void* id128);
+
+/* Host time of the executor by category, accumulated while HCCL_AMD_HOST_PROFILE=1 (read at library load): ns[i]
+ * and calls[i] for i < n of the categories below; reset != 0 zeroes them afterwards. Diagnostics of the enqueue cost. */
+enum {
+    HCCL_AMD_HP_EXECUTE = 0, /* a whole Execute call */
+    HCCL_AMD_HP_GROUP = 1,   /* transport groups (ncclGroupStart .. ncclGroupEnd) */
+    HCCL_AMD_HP_FOLD = 2,    /* fold launches */
+    HCCL_AMD_HP_COPY = 3,    /* copy launches */
+    HCCL_AMD_HP_RECORD = 4,  /* unit event records */
+    HCCL_AMD_HP_WAIT = 5,    /* cross-stream waits */
+    HCCL_AMD_HP_PLAN = 6,    /* planning outside the compiled-collective cache */
+    HCCL_AMD_HP_COUNT = 7
+};
+extern HcclResult HcclAmdHostProfile(uint64_t* ns, uint64_t* calls, uint32_t n, int32_t reset);
+
+/* Communicators whose HcclCommDestroy is waiting for the graphs captured on them to be destroyed. */
+extern uint32_t HcclAmdCommPendingDestroys(void);
+
 /* Blocking host all-gather supplied by the caller's bootstrap (a TCP store, MPI, torch.distributed gloo ...):
  * gathers `bytes` bytes from every rank into all[nRanks * bytes] in rank order; returns 0 on success. */
 typedef int32_t (*HcclAmdHostAllGatherFn)(void* ctx, const void* mine, uint64_t bytes, void* all);

@@ -1,7 +1,7 @@
 """Communicator creation from a rank table (HcclCommInitClusterInfo) and for all local devices (HcclCommInitAll) on
 the one-GPU box. A 1-rank table gives a working communicator; a 2-rank table run by two processes on the same GPU
-exercises the TCP unique-id exchange end to end — both ranks get past it and then RCCL refuses two ranks on one device
-(HCCL_E_PARA), which is the expected outcome here (a broken exchange would end in HCCL_E_TIMEOUT / TCP errors)."""
+exercises the TCP unique-id exchange end to end: both ranks must hold the same unique id after it
+(HcclAmdLastBootstrap digests), and the only failure allowed is RCCL's refusal of two ranks on one device after it."""
 import json
 import multiprocessing as mp
 import socket
@@ -48,20 +48,26 @@ def test_cluster_info_single_rank(tmp_path):
 def _cluster_rank(path, rank, q):
     import os
     os.environ["HCCL_CONNECT_TIMEOUT"] = "120"
+    os.environ["HCCL_AMD_CONNECT_TIMEOUT_MS"] = "60000"
     try:
         import hccl_amd as H2
         from hccl_amd._lib import HcclError as E
         try:
             c = H2.comm_init_cluster_info(path, rank)
             c.destroy()
-            q.put((rank, "HCCL_SUCCESS"))
+            res = "HCCL_SUCCESS"
         except E as e:
-            q.put((rank, str(e)))
+            res = str(e)
+        stage, digest = H2.last_bootstrap()
+        q.put((rank, res, stage, digest))
     except Exception as e:  # noqa: BLE001
-        q.put((rank, f"{type(e).__name__}: {e}"))
+        q.put((rank, f"{type(e).__name__}: {e}", -1, 0))
 
 
 def test_cluster_info_two_ranks_exchange_unique_id(tmp_path):
+    """Both ranks must get through the TCP exchange (stage >= 1) holding the same unique id (equal digests). Past it,
+    RCCL may refuse two ranks on one device (HCCL_E_PARA): that is the only failure allowed, and only after the
+    exchange. A broken exchange leaves stage 0 or different digests and fails here."""
     path = str(tmp_path / "rt2.json")
     _write_table(path, 2, _free_port())
     ctx = mp.get_context("spawn")
@@ -70,14 +76,18 @@ def test_cluster_info_two_ranks_exchange_unique_id(tmp_path):
     for p in procs:
         p.start()
     try:
-        got = dict(q.get(timeout=300) for _ in procs)
+        got = {r: (res, stage, digest) for r, res, stage, digest in (q.get(timeout=300) for _ in procs)}
     finally:
         for p in procs:
             p.join(timeout=60)
             if p.is_alive():
                 p.kill()
     for r in range(2):
-        assert "HCCL_SUCCESS" in got[r] or "HCCL_E_PARA" in got[r], got
+        res, stage, digest = got[r]
+        assert stage >= 1, f"rank {r} did not complete the unique-id exchange: {got}"
+        assert digest != 0
+        assert res == "HCCL_SUCCESS" or ("HCCL_E_PARA" in res and stage == 1), got
+    assert got[0][2] == got[1][2], f"the ranks hold different unique ids: {got}"
 
 
 def test_comm_init_all_one_device():

@@ -1,0 +1,116 @@
+#!/bin/bash
+# One parameterised GPU call (replaces r02's one-off gpu_call_r02*.sh recipes). Run on the GPU box from the repo root:
+#   tools/gpu_call.sh STEP [STEP ...]        e.g. /usr/local/graft/bin/gpurun -- 'tools/gpu_call.sh rccl_failure host_cost'
+# Each step runs under its own time limit and writes gpurun_out/<step>*. An ordinary failure (exit 1) moves on to the
+# next step; a time limit (124/137), an abort (134) or a segfault (139) ends the call there: nothing more touches the
+# GPU after it. Steps:
+#   suite          pytest -m gpu (the round-end suite), smoke, default bench
+#   rccl_failure   tests of the RCCL path's failure handling, bootstrap and capture
+#   destroy_probe  which teardown step waits on a live graph (non-blocking RCCL, finalize bounded at 5 s)
+#   destroy_probe_blocking  the same with blocking RCCL and immediate teardown (r02's conditions; ends on its limit)
+#   host_cost      host enqueue cost of the RCCL path by category (default, watchdog off, blocking RCCL)
+#   ipc_pmc        rocprofv3 kernel trace + FETCH_SIZE + WRITE_SIZE of the one-sided kernel, rank mode, n = 2
+#   span_pmc       the same over a self-loop MeshChunk program (RCCL copies + folds)
+#   bench          bench.py default line
+#   counters       the TCC counters this rocprofv3 offers
+set -o pipefail
+cd "$(dirname "$0")/.." || exit 1
+REPO=$(pwd)
+OUT=$REPO/gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+run() {  # run NAME LIMIT CMD...: stop the call on a time limit, abort or crash
+  local name=$1 limit=$2
+  shift 2
+  echo "== $name (limit ${limit}s)"
+  timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "   rc=$rc"
+  tail -5 "$OUT/$name.log"
+  case $rc in 124|137|134|139) echo "stopping: $name ended with $rc"; exit $rc ;; esac
+  return $rc
+}
+
+step_suite() {
+  export HCCL_AMD_RANDOM_DRAWS=${HCCL_AMD_RANDOM_DRAWS:-1000}
+  run suite 780 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
+  run smoke 180 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+  step_bench
+}
+
+step_rccl_failure() {
+  run rccl_failure 600 python3 -u -m pytest tests/test_gpu_rccl_failure.py tests/test_gpu_bootstrap.py \
+    tests/test_gpu_rccl.py -v -s --timeout 200 --timeout-method thread -p no:cacheprovider
+}
+
+step_destroy_probe() {
+  HCCL_AMD_DEFER_DESTROY=0 HCCL_EXEC_TIMEOUT=5 run destroy_probe_immediate 60 python3 -u tools/destroy_probe.py
+  run destroy_probe_deferred 60 python3 -u tools/destroy_probe.py
+}
+
+step_destroy_probe_blocking() {
+  HCCL_AMD_DEFER_DESTROY=0 HCCL_AMD_RCCL_BLOCKING=1 run destroy_probe_blocking 40 python3 -u tools/destroy_probe.py
+}
+
+step_host_cost() {
+  : > "$OUT/host_cost.jsonl"
+  HCCL_AMD_HOST_PROFILE=1 run host_cost_default 120 python3 -u tools/host_cost_probe.py
+  cat "$OUT/host_cost_default.log" | grep '^{' >> "$OUT/host_cost.jsonl"
+  HCCL_AMD_HOST_PROFILE=1 HCCL_EXEC_TIMEOUT=0 run host_cost_no_watchdog 120 python3 -u tools/host_cost_probe.py
+  cat "$OUT/host_cost_no_watchdog.log" | grep '^{' >> "$OUT/host_cost.jsonl"
+  HCCL_AMD_HOST_PROFILE=1 HCCL_AMD_RCCL_BLOCKING=1 run host_cost_blocking 120 python3 -u tools/host_cost_probe.py
+  cat "$OUT/host_cost_blocking.log" | grep '^{' >> "$OUT/host_cost.jsonl"
+}
+
+ipc_pmc_one() {  # DTYPE MODE(trace|fetch|write) PORT
+  local dt=$1 mode=$2 port=$3
+  local args=(--world 2 --mib 512 --dtype "$dt" --algo IPC_TWOSHOT --iters 10 --port "$port")
+  local prof
+  case $mode in
+    trace) prof=(--kernel-trace --stats) ;;
+    fetch) prof=(--pmc FETCH_SIZE) ;;
+    write) prof=(--pmc WRITE_SIZE) ;;
+  esac
+  timeout -k 10 150 python3 -u tools/ipc_pmc_rank.py --rank 1 "${args[@]}" > "$OUT/ipc_pmc_${dt}_${mode}_r1.log" 2>&1 &
+  local pid1=$!
+  run "ipc_pmc_${dt}_${mode}" 150 rocprofv3 "${prof[@]}" --output-format csv -d "$OUT/ipc_pmc_${dt}_${mode}" -o run \
+    -- python3 -u tools/ipc_pmc_rank.py --rank 0 "${args[@]}"
+  local rc=$?
+  wait $pid1
+  return $rc
+}
+
+step_ipc_pmc() {
+  local port=29631
+  for dt in fp32 fp16; do
+    for mode in trace fetch write; do
+      port=$((port + 1))
+      ipc_pmc_one "$dt" "$mode" "$port"
+    done
+  done
+}
+
+step_span_pmc() {
+  local args=(--algo mesh_chunk --units 64 --iters 5)
+  run span_mesh_chunk_trace 150 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/span_trace" -o run \
+    -- python3 -u tools/rccl_selfloop_trace.py "${args[@]}"
+  run span_mesh_chunk_fetch 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/span_fetch" -o run \
+    -- python3 -u tools/rccl_selfloop_trace.py "${args[@]}"
+  run span_mesh_chunk_write 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/span_write" -o run \
+    -- python3 -u tools/rccl_selfloop_trace.py "${args[@]}"
+}
+
+step_bench() {
+  run bench 300 python3 bench.py
+  grep '^{' "$OUT/bench.log" > "$OUT/bench.json" || true
+}
+
+step_counters() {
+  run counters 60 rocprofv3 -L
+  grep -E "TCC_EA0?_(RD|WR)REQ|FETCH_SIZE|WRITE_SIZE" "$OUT/counters.log" | head -60 > "$OUT/counters_tcc.txt" || true
+}
+
+for s in "$@"; do
+  "step_$s" || echo "step $s: failed (rc=$?), continuing"
+done

@@ -62,9 +62,17 @@ def main():
     dt = (time.perf_counter() - t0) / a.iters
     comm.destroy()
     groups = len({arr[i].group for i in range(nops) if arr[i].kind in (H.IrKind.SEND, H.IrKind.RECV)})
+    # HBM bytes the program must move on this one GPU: a self send/recv pair of B bytes is an RCCL copy (read B,
+    # write B); a fold of k inputs reads k and writes 1 operand; a copy reads and writes its bytes
+    copy_b = sum(2 * arr[i].count * es for i in range(nops) if arr[i].kind == H.IrKind.SEND)
+    fold_b = sum((arr[i].nsrc + 1) * arr[i].count * es for i in range(nops) if arr[i].kind == H.IrKind.REDUCE)
+    dcopy_b = sum(2 * arr[i].count * es for i in range(nops) if arr[i].kind == H.IrKind.COPY)
     print(json.dumps({"algo": algo.name, "ranks": a.ranks, "rank": a.rank, "dtype": a.dtype.upper(),
                       "bytes_per_rank": count * x.element_size(), "records": nops, "groups": groups,
-                      "single_stream": a.single, "piece_bytes": piece, "us_per_program": round(dt * 1e6, 1)}),
+                      "single_stream": a.single, "piece_bytes": piece, "us_per_program": round(dt * 1e6, 1),
+                      "iters": a.iters, "algorithmic_bytes_per_program": {"rccl_copies": copy_b, "folds": fold_b,
+                                                                          "copies": dcopy_b,
+                                                                          "total": copy_b + fold_b + dcopy_b}}),
           flush=True)
 
 
