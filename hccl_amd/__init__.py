@@ -227,6 +227,12 @@ class Comm:
         check("HcclAmdCommCompileStats", lib.HcclAmdCommCompileStats(self.handle, ctypes.byref(h), ctypes.byref(m)))
         return h.value, m.value
 
+    def graph_stats(self) -> tuple:
+        """(launches, captures) of the communicator's executor graphs (HcclAmdCommGraphStats)."""
+        la, ca = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        check("HcclAmdCommGraphStats", lib.HcclAmdCommGraphStats(self.handle, ctypes.byref(la), ctypes.byref(ca)))
+        return la.value, ca.value
+
     def reduce_scatter_v(self, send: torch.Tensor, counts: Sequence[int], displs: Sequence[int], recv: torch.Tensor,
                          op: int = HcclReduceOp.SUM, stream=None) -> None:
         """HcclReduceScatterV: rank q's block of `send` is counts[q] elements at displs[q]."""

@@ -191,6 +191,7 @@ SIGNATURES = {
     "HcclAmdCommSetIpcBlocks": (_res, [_vp, _u32]),
     "HcclAmdCommLastAlgo": (_i32, [_vp]),
     "HcclAmdCommCompileStats": (_res, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
+    "HcclAmdCommGraphStats": (_res, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     "HcclAmdCommExecute": (_res, [_vp, ctypes.POINTER(HcclAmdIrOp), _u64, _vp, _vp, _i32, _i32, _i32, _vp]),
     "HcclAmdCommIpcStatus": (_res, [_vp, ctypes.POINTER(_u32)]),
     "HcclAmdIpcTimeoutMs": (_u64, []),

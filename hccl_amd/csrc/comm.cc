@@ -133,6 +133,9 @@ Comm::~Comm()
     if (commStream != nullptr) (void)hipStreamSynchronize(commStream);
     TeardownTrace(rank, "sync reduce stream", true);
     if (reduceStream != nullptr) (void)hipStreamSynchronize(reduceStream);
+    TeardownTrace(rank, "sync last call + graphs", true);
+    if (tail != nullptr) (void)hipEventSynchronize(tail);
+    ReleaseGraphs(*this);
     TeardownTrace(rank, "stop watchdog", true);
     watchdog.reset();
     TeardownTrace(rank, "IPC quiesce + release", true);
@@ -146,6 +149,7 @@ Comm::~Comm()
     if (commStream != nullptr) (void)hipStreamDestroy(commStream);
     if (reduceStream != nullptr) (void)hipStreamDestroy(reduceStream);
     if (stallHost != nullptr) (void)hipHostFree(stallHost);
+    if (tail != nullptr) (void)hipEventDestroy(tail);
     TeardownTrace(rank, "done", false);
 }
 

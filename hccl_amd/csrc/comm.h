@@ -77,6 +77,7 @@ struct UnitPlan {
     size_t first = 0;  // IR records [first, first + count)
     size_t count = 0;
     int64_t waitUnit = -1;
+    bool waitedOn = false;  // a later unit waits for this one: Execute records an event after it (no one else's)
 };
 
 // One rank's compiled collective: the schedule for a set of ScheduleParams and the executor's plan for it. The plan
@@ -90,6 +91,18 @@ struct CompiledSchedule {
     int64_t relation[3] = {0, 0, 0};  // pairs (0,1), (0,2), (1,2): kDisjoint or the base difference
     bool hasPlan = false;
     std::vector<UnitPlan> plan;
+    uint64_t lastUse = 0;
+    mutable uint64_t eagerRuns = 0;  // RunCompiled: runs issued eagerly (a graph is captured only after one)
+};
+
+// One rank's executor program captured into a HIP graph for exact buffers, stream, dtype and op (RunCompiled).
+struct GraphEntry {
+    ScheduleParams params;
+    void* bufs[3] = {nullptr, nullptr, nullptr};
+    hipStream_t stream = nullptr;
+    HcclDataType dt = HCCL_DATA_TYPE_RESERVED;
+    HcclReduceOp op = HCCL_REDUCE_RESERVED;
+    hipGraphExec_t exec = nullptr;  // nullptr: capture failed for this key, run eagerly
     uint64_t lastUse = 0;
 };
 
@@ -212,6 +225,18 @@ struct Comm {
     uint64_t compileHits = 0;
     uint64_t compileMisses = 0;
 
+    // Executor graphs (RunCompiled): the two-stream programs of the RCCL path, captured once on a private stream and
+    // replayed with one hipGraphLaunch per call. graphLaunches / graphCaptures count them (HcclAmdCommGraphStats).
+    std::vector<GraphEntry> graphs;
+    hipStream_t captureStream = nullptr;
+    uint64_t graphLaunches = 0;
+    uint64_t graphCaptures = 0;
+
+    // The end of the last collective on its user stream: a call on another stream waits for it first, since every
+    // call of a communicator shares its staging (OrderAfterTail / MarkTail).
+    hipEvent_t tail = nullptr;
+    hipStream_t tailStream = nullptr;
+
     HcclResult Init(int dev);
     // After the transport is set: the watchdog for an Abortable transport and the fault-injection hook.
     HcclResult StartWatchdog();
@@ -279,10 +304,39 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
 
 std::vector<UnitPlan> PlanUnits(const std::vector<HcclAmdIrOp>& ops, void* const bufs[3], uint64_t es);
 
+// Runs a compiled two-stream collective: from the communicator's graph cache when the transport allows capture (RCCL)
+// and HCCL_AMD_GRAPH_CACHE is not 0 (the first run of a compiled collective is eager, later ones with the same
+// buffers, stream, dtype and op replay one captured graph), else through Execute.
+HcclResult RunCompiled(Comm& c, const CompiledSchedule& cs, void* const bufs[3], HcclDataType dt, HcclReduceOp op,
+                       hipStream_t user);
+void ReleaseGraphs(Comm& c);
+
+// Entry/exit of every collective: under the caller's capture, NoteCapture; otherwise wait for the previous call's end
+// when it ran on another stream, and record this call's end.
+class EntryScope {
+public:
+    EntryScope(Comm& c, hipStream_t s);
+    ~EntryScope();
+    HcclResult status() const { return status_; }
+    bool captured() const { return captured_; }
+    EntryScope(const EntryScope&) = delete;
+    EntryScope& operator=(const EntryScope&) = delete;
+
+private:
+    Comm& c_;
+    hipStream_t s_;
+    bool captured_ = false;
+    HcclResult status_ = HCCL_SUCCESS;
+};
+
 // The compiled form of p for the buffers bufs (cached on c; call with c.mu held): BuildSchedule's result and, when
 // withPlan, the plan for the buffers' overlap relation. The pointer stays valid until the next call on c.
 HcclResult CompileCollective(Comm& c, const ScheduleParams& p, void* const bufs[3], bool withPlan,
                              const CompiledSchedule** out);
+// The same for an IR program handed in whole (HcclAmdCommExecute), keyed by its records; always with its plan.
+constexpr int32_t kProgramOpType = -1;
+HcclResult CompileProgram(Comm& c, const HcclAmdIrOp* ops, uint64_t numOps, uint32_t elemSize, void* const bufs[3],
+                          const CompiledSchedule** out);
 
 // Collectives whose per-rank payload is at most this many bytes run single-stream (HCCL_AMD_SINGLE_STREAM_BYTES,
 // default 1 MiB).

@@ -258,6 +258,7 @@ std::vector<UnitPlan> PlanUnits(const std::vector<HcclAmdIrOp>& ops, void* const
             }
         }
         onStream[x].push_back(plan.size());
+        if (u.waitUnit >= 0) plan[size_t(u.waitUnit)].waitedOn = true;
         plan.push_back(u);
         ranges.push_back(std::move(rg));
     }
@@ -300,8 +301,13 @@ bool PlanCacheEnabled()
 
 }  // namespace
 
-HcclResult CompileCollective(Comm& c, const ScheduleParams& p, void* const bufs[3], bool withPlan,
-                             const CompiledSchedule** out)
+namespace {
+
+// The compiled-collective cache of c: the entry for p (a hit moves it to the front of the LRU order), else a new one
+// from make(), evicting the least recently used at kCompiledMax entries.
+template <class Make>
+HcclResult FindOrCompile(Comm& c, const ScheduleParams& p, void* const bufs[3], bool withPlan, Make make,
+                         const CompiledSchedule** out)
 {
     const bool cache = PlanCacheEnabled();
     if (!cache) c.compiled.clear();
@@ -316,7 +322,7 @@ HcclResult CompileCollective(Comm& c, const ScheduleParams& p, void* const bufs[
         ++c.compileMisses;
         auto e = std::make_unique<CompiledSchedule>();
         e->params = p;
-        HCCL_CHK(static_cast<HcclResult>(BuildSchedule(p, &e->sched)));
+        HCCL_CHK(make(&e->sched));
         for (const HcclAmdIrOp& o : e->sched.ops) {
             const uint64_t bytes = o.count * p.elemSize;
             if (o.dstBuf >= 0 && o.dstBuf < 3) {
@@ -349,6 +355,47 @@ HcclResult CompileCollective(Comm& c, const ScheduleParams& p, void* const bufs[
         }
     }
     *out = hit;
+    return HCCL_SUCCESS;
+}
+
+}  // namespace
+
+HcclResult CompileCollective(Comm& c, const ScheduleParams& p, void* const bufs[3], bool withPlan,
+                             const CompiledSchedule** out)
+{
+    return FindOrCompile(
+        c, p, bufs, withPlan, [&](Schedule* s) { return static_cast<HcclResult>(BuildSchedule(p, s)); }, out);
+}
+
+HcclResult CompileProgram(Comm& c, const HcclAmdIrOp* ops, uint64_t numOps, uint32_t elemSize, void* const bufs[3],
+                          const CompiledSchedule** out)
+{
+    // A program has no schedule parameters: it is keyed by its bytes (FNV-1a 64) and length, and a hit is confirmed
+    // record by record.
+    uint64_t h = 1469598103934665603ull;
+    const unsigned char* b = reinterpret_cast<const unsigned char*>(ops);
+    for (size_t i = 0; i < numOps * sizeof(HcclAmdIrOp); ++i) {
+        h ^= b[i];
+        h *= 1099511628211ull;
+    }
+    ScheduleParams p;
+    p.opType = kProgramOpType;
+    p.count = h;
+    p.nRanks = static_cast<uint32_t>(numOps);
+    p.elemSize = elemSize;
+    p.scratchCapBytes = c.scratchBytes;
+    HCCL_CHK(FindOrCompile(
+        c, p, bufs, true,
+        [&](Schedule* s) {
+            s->ops.assign(ops, ops + numOps);
+            return HCCL_SUCCESS;
+        },
+        out));
+    if ((*out)->sched.ops.size() != numOps ||
+        std::memcmp((*out)->sched.ops.data(), ops, numOps * sizeof(HcclAmdIrOp)) != 0) {
+        c.compiled.clear();  // a hash collision: compile afresh
+        return CompileProgram(c, ops, numOps, elemSize, bufs, out);
+    }
     return HCCL_SUCCESS;
 }
 
@@ -425,7 +472,7 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
                 return HCCL_E_INTERNAL;
             }
         }
-        {
+        if (u.waitedOn) {
             HpScope hp(HCCL_AMD_HP_RECORD);
             HCCL_CHK(c.NextEvent(&evs[ui]));
             HIP_CHK(hipEventRecord(evs[ui], streams[x]));
@@ -459,5 +506,149 @@ extern "C" HcclResult HcclAmdHostProfile(uint64_t* ns, uint64_t* calls, uint32_t
             Hp().calls[i] = 0;
         }
     }
+    return HCCL_SUCCESS;
+}
+
+namespace hccl_amd {
+
+// ------------------------------------------------------------------------------------------------ entry ordering
+
+EntryScope::EntryScope(Comm& c, hipStream_t s) : c_(c), s_(s)
+{
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess) {
+        status_ = HCCL_E_RUNTIME;
+        return;
+    }
+    captured_ = st != hipStreamCaptureStatusNone;
+    if (captured_) {
+        status_ = NoteCapture(c, s);
+        return;
+    }
+    // Every call of a communicator shares its staging. Calls on one stream are ordered by it, and eager two-stream
+    // calls by the communicator's own streams; a call that follows one on another stream waits for its end.
+    if (c.tailStream != nullptr && c.tailStream != s && hipStreamWaitEvent(s, c.tail, 0) != hipSuccess) {
+        status_ = HCCL_E_RUNTIME;
+    }
+}
+
+EntryScope::~EntryScope()
+{
+    if (captured_ || status_ != HCCL_SUCCESS) return;
+    if (c_.tail == nullptr && hipEventCreateWithFlags(&c_.tail, hipEventDisableTiming) != hipSuccess) {
+        c_.tail = nullptr;
+        return;
+    }
+    if (hipEventRecord(c_.tail, s_) == hipSuccess) c_.tailStream = s_;
+}
+
+// ------------------------------------------------------------------------------------------------ executor graphs
+
+namespace {
+
+// HCCL_AMD_GRAPH_CACHE: the number of executor graphs a communicator keeps (default 16; 0 = every call eager). Read
+// per call: tests switch it.
+size_t GraphCacheSize()
+{
+    const char* e = std::getenv("HCCL_AMD_GRAPH_CACHE");
+    if (e == nullptr || *e == '\0') return 16;
+    return static_cast<size_t>(std::strtoull(e, nullptr, 10));
+}
+
+// Captures the program on the communicator's private stream (thread-local capture mode: other threads' HIP calls do
+// not disturb it, and it disturbs no capture of theirs). Under capture Execute posts the transport groups on the
+// capturing stream and forks only the folds (executor.cc Execute), the RCCL capture pattern that instantiates.
+HcclResult CaptureProgram(Comm& c, const CompiledSchedule& cs, void* const bufs[3], HcclDataType dt, HcclReduceOp op,
+                          hipGraphExec_t* exec)
+{
+    *exec = nullptr;
+    if (c.captureStream == nullptr) HIP_CHK(hipStreamCreateWithFlags(&c.captureStream, hipStreamNonBlocking));
+    HIP_CHK(hipStreamBeginCapture(c.captureStream, hipStreamCaptureModeThreadLocal));
+    const HcclResult r = Execute(c, cs.sched.ops, bufs, dt, op, c.captureStream, false, &cs.plan);
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(c.captureStream, &g);
+    if (r != HCCL_SUCCESS || e != hipSuccess || g == nullptr) {
+        if (g != nullptr) (void)hipGraphDestroy(g);
+        HCCL_AMD_ERR("rank %u: executor graph capture failed (%s / %s); the collective runs eagerly", c.rank,
+                     HcclAmdGetErrorString(r), hipGetErrorString(e));
+        return r != HCCL_SUCCESS ? r : HCCL_E_RUNTIME;
+    }
+    const hipError_t ie = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);  // the executable keeps what it needs (RCCL's plans are held by it)
+    if (ie != hipSuccess) {
+        *exec = nullptr;
+        HCCL_AMD_ERR("rank %u: hipGraphInstantiate: %s; the collective runs eagerly", c.rank, hipGetErrorString(ie));
+        return HCCL_E_RUNTIME;
+    }
+    return HCCL_SUCCESS;
+}
+
+}  // namespace
+
+HcclResult RunCompiled(Comm& c, const CompiledSchedule& cs, void* const bufs[3], HcclDataType dt, HcclReduceOp op,
+                       hipStream_t user)
+{
+    const size_t cap = GraphCacheSize();
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    HIP_CHK(hipStreamIsCapturing(user, &st));
+    if (cap == 0 || st != hipStreamCaptureStatusNone || !c.transport->Abortable()) {
+        return Execute(c, cs.sched.ops, bufs, dt, op, user, false, &cs.plan);
+    }
+    GraphEntry* hit = nullptr;
+    for (GraphEntry& g : c.graphs) {
+        if (g.stream == user && g.dt == dt && g.op == op && std::memcmp(g.bufs, bufs, sizeof g.bufs) == 0 &&
+            SameParams(g.params, cs.params)) {
+            hit = &g;
+            break;
+        }
+    }
+    if (hit == nullptr) {
+        // The first run of a compiled collective is eager: it makes RCCL connect to the program's peers, which a
+        // capture must not have to do.
+        if (cs.eagerRuns++ == 0) return Execute(c, cs.sched.ops, bufs, dt, op, user, false, &cs.plan);
+        if (c.graphs.size() >= cap) {
+            auto lru = std::min_element(c.graphs.begin(), c.graphs.end(),
+                                        [](const GraphEntry& x, const GraphEntry& y) { return x.lastUse < y.lastUse; });
+            if (lru->exec != nullptr) (void)hipGraphExecDestroy(lru->exec);
+            c.graphs.erase(lru);
+        }
+        GraphEntry e;
+        e.params = cs.params;
+        std::memcpy(e.bufs, bufs, sizeof e.bufs);
+        e.stream = user;
+        e.dt = dt;
+        e.op = op;
+        (void)CaptureProgram(c, cs, bufs, dt, op, &e.exec);
+        if (e.exec != nullptr) ++c.graphCaptures;
+        c.graphs.push_back(e);
+        hit = &c.graphs.back();
+    }
+    hit->lastUse = ++c.compileTick;
+    if (hit->exec == nullptr) return Execute(c, cs.sched.ops, bufs, dt, op, user, false, &cs.plan);
+    WatchScope watch(c.watchdog.get(), user);
+    HIP_CHK(hipGraphLaunch(hit->exec, user));
+    ++c.graphLaunches;
+    return HCCL_SUCCESS;
+}
+
+void ReleaseGraphs(Comm& c)
+{
+    for (GraphEntry& g : c.graphs) {
+        if (g.exec != nullptr) (void)hipGraphExecDestroy(g.exec);
+    }
+    c.graphs.clear();
+    if (c.captureStream != nullptr) (void)hipStreamDestroy(c.captureStream);
+    c.captureStream = nullptr;
+}
+
+}  // namespace hccl_amd
+
+extern "C" HcclResult HcclAmdCommGraphStats(HcclComm comm, uint64_t* launches, uint64_t* captures)
+{
+    hccl_amd::Comm* c = hccl_amd::AsComm(comm);
+    if (c == nullptr || launches == nullptr || captures == nullptr) return HCCL_E_PTR;
+    std::lock_guard<std::mutex> lk(c->mu);
+    *launches = c->graphLaunches;
+    *captures = c->graphCaptures;
     return HCCL_SUCCESS;
 }

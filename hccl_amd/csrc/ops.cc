@@ -82,7 +82,8 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     std::lock_guard<std::mutex> lk(c.mu);
     HCCL_CHK(c.Gate());  // a failed communicator takes no more work (op_common.cc:89-97)
     HIP_CHK(hipSetDevice(c.device));
-    HCCL_CHK(NoteCapture(c, stream));
+    const EntryScope entry(c, stream);
+    HCCL_CHK(entry.status());
     const uint32_t es = DataTypeSize(dt);
     if (c.nRanks == 1) {
         // SingleRankProc (op_common.cc:3042-3098): copy in -> out unless they are the same buffer.
@@ -177,7 +178,8 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     c.lastAlgo = s.algo;
     HCCL_AMD_LOG("rank %u op %d algo %d count %llu ops %zu", c.rank, opType, s.algo, (unsigned long long)count,
                  s.ops.size());
-    return Execute(c, s.ops, bufs, dt, op, stream, single, single ? nullptr : &cs->plan);
+    if (single) return Execute(c, s.ops, bufs, dt, op, stream, true);
+    return RunCompiled(c, *cs, bufs, dt, op, stream);
 }
 
 // ReduceScatterV (reduce_scatter_v_op.cc:24-83, ReduceScatterVOutPlaceCommon :285-330): the mesh template's order
@@ -188,7 +190,8 @@ HcclResult RunReduceScatterV(Comm& c, void* sendBuf, const uint64_t* counts, con
     std::lock_guard<std::mutex> lk(c.mu);
     HCCL_CHK(c.Gate());
     HIP_CHK(hipSetDevice(c.device));
-    HCCL_CHK(NoteCapture(c, stream));
+    const EntryScope entry(c, stream);
+    HCCL_CHK(entry.status());
     // ReduceScatterVAutoSelector::SelectAicpuAlgo (reduce_scatter_v_auto_selector.cc:180-197): UINT64 and FP64 have
     // no algorithm
     if (dt == HCCL_DATA_TYPE_UINT64 || dt == HCCL_DATA_TYPE_FP64) return HCCL_E_NOT_SUPPORT;
@@ -231,7 +234,8 @@ HcclResult RunReduceScatterV(Comm& c, void* sendBuf, const uint64_t* counts, con
     const Schedule& s = cs->sched;
     if (s.scratchElems * es > c.scratchBytes) return HCCL_E_INTERNAL;
     c.lastAlgo = s.algo;
-    return Execute(c, s.ops, bufs, dt, op, stream, single, single ? nullptr : &cs->plan);
+    if (single) return Execute(c, s.ops, bufs, dt, op, stream, true);
+    return RunCompiled(c, *cs, bufs, dt, op, stream);
 }
 
 }  // namespace
@@ -525,10 +529,16 @@ HcclResult HcclAmdCommExecute(HcclComm comm, const HcclAmdIrOp* ops, uint64_t nu
     }
     HCCL_CHK(c->Gate());
     HIP_CHK(hipSetDevice(c->device));
-    HCCL_CHK(NoteCapture(*c, static_cast<hipStream_t>(stream)));
-    const std::vector<HcclAmdIrOp> prog(ops, ops + numOps);
+    const EntryScope entry(*c, static_cast<hipStream_t>(stream));
+    HCCL_CHK(entry.status());
     void* bufs[3] = {sendBuf, recvBuf, c->scratch};
-    return Execute(*c, prog, bufs, dataType, op, static_cast<hipStream_t>(stream), singleStream != 0);
+    if (singleStream != 0) {
+        const std::vector<HcclAmdIrOp> prog(ops, ops + numOps);
+        return Execute(*c, prog, bufs, dataType, op, static_cast<hipStream_t>(stream), true);
+    }
+    const CompiledSchedule* cs = nullptr;
+    HCCL_CHK(CompileProgram(*c, ops, numOps, static_cast<uint32_t>(es), bufs, &cs));
+    return RunCompiled(*c, *cs, bufs, dataType, op, static_cast<hipStream_t>(stream));
 }
 
 HcclResult HcclAmdCommCompileStats(HcclComm comm, uint64_t* hits, uint64_t* misses)

@@ -159,9 +159,18 @@ void Watchdog::Commit(Ticket* t)
     t->stream = nullptr;
 }
 
+// A helper thread's HIP calls (event queries, teardown) must not invalidate a stream capture another thread runs in
+// the global capture mode (torch's default): this thread is put in the relaxed mode.
+void RelaxCaptureMode()
+{
+    hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
+    (void)hipThreadExchangeStreamCaptureMode(&m);
+}
+
 void Watchdog::Run()
 {
     (void)hipSetDevice(c_->device);
+    RelaxCaptureMode();
     std::unique_lock<std::mutex> lk(mu_);
     while (!stop_) {
         // a 10 ms poll: no wake-up is paid per collective, and the bound is seconds
@@ -267,6 +276,7 @@ void ReleaseGraphRef(void* p)
 
 void ReaperLoop()
 {
+    RelaxCaptureMode();
     Reaper& r = TheReaper();
     std::unique_lock<std::mutex> lk(r.mu);
     for (;;) {

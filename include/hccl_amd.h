@@ -221,6 +221,12 @@ extern HcclResult HcclAmdCommExecute(HcclComm comm, const HcclAmdIrOp* ops, uint
  * *hits and *misses count the RCCL-path calls that reused or built one. */
 extern HcclResult HcclAmdCommCompileStats(HcclComm comm, uint64_t* hits, uint64_t* misses);
 
+/* Executor graphs of comm (RCCL path, two-stream programs): *launches = calls served by one hipGraphLaunch of a
+ * captured program, *captures = programs captured. A compiled collective runs eagerly the first time; later calls with
+ * the same buffers, stream, dtype and op replay its graph. HCCL_AMD_GRAPH_CACHE = graphs kept per communicator
+ * (default 16, least recently used evicted; 0 = every call eager). */
+extern HcclResult HcclAmdCommGraphStats(HcclComm comm, uint64_t* launches, uint64_t* captures);
+
 /* Status of the IPC path of comm (synchronous read). Bit 0: a cross-rank barrier wait exceeded HCCL_AMD_IPC_TIMEOUT_MS
  * (default 60000) — the results of that and every later IPC AllReduce on comm are invalid (sticky: the communicator is
  * failed, as after an asynchronous error). Bits 8-15: bit length of the longest barrier wait of the last IPC

@@ -388,3 +388,70 @@ def test_rccl_path_graph_capture_replays():
     assert status == "ok", results
     assert not [r for r in results if r[-1] not in ("ok", "unpaired")], results
     assert sum(r[-1] == "ok" for r in results) >= 8, results
+
+
+def _graph_cache_worker(q):
+    """Each program run five times on the same buffers with a fresh input every time (two-stream mode): the first run
+    is eager, the second captures the executor graph, the later ones replay it; the last two alternate the caller's
+    stream (a graph per stream, ordered after the previous call's end). Every output bit-exact against the oracle."""
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        import torch
+        import hccl_amd as H
+        from oracle import oracle as O
+        from tests._util import to_device, to_host
+        torch.cuda.set_device(0)
+        comm = H.comm_init_root_info(1, H.get_root_info(), 0)
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        results = []
+        dtype, op = O.FP32, O.SUM
+        for k, (op_type, algo, n, rank, count) in enumerate(CAPTURE_CASES):
+            prog = self_looped(op_type, algo, n, rank, count, dtype)
+            if prog is None:
+                results.append((k, "unpaired"))
+                continue
+            arr, nops, scratch = prog
+            in_len = count * n if op_type == 1 else count
+            out_len = count * n if op_type == 3 else count
+            st = O.NP_STORAGE[dtype]
+            xd = to_device(dtype, np.zeros(in_len, st))
+            od = to_device(dtype, np.zeros(out_len, st))
+            before = comm.graph_stats()[0]
+            for rep in range(5):
+                s = streams[rep % 2] if rep >= 3 else streams[0]
+                x = O.random_operands(dtype, in_len, seed=7000 + 10 * k + rep, edge=False)
+                bufs = [[x.copy(), np.zeros(out_len, st), np.zeros(max(scratch, 1), st)]]
+                assert O.replay(1, dtype, op, [(arr, nops)], bufs) == 0
+                torch.cuda.synchronize()
+                xd.copy_(to_device(dtype, x))
+                od.zero_()
+                torch.cuda.synchronize()
+                comm.execute(arr, nops, xd, od, op, False, s, dtype=dtype)
+                torch.cuda.synchronize()
+                same = O.equal_bits(dtype, to_host(dtype, od), bufs[0][1])
+                results.append((k, rep, "ok" if same else "mismatch"))
+            results.append((k, "graph_launches", comm.graph_stats()[0] - before))
+        comm.destroy()
+        q.put(("ok", results))
+    except Exception as e:  # noqa: BLE001
+        q.put(("err", f"{type(e).__name__}: {e}\n{traceback.format_exc()}"))
+
+
+def test_executor_graph_cache_replays_bit_exact():
+    """The RCCL path's executor graphs (HcclAmdCommGraphStats): programs replayed from the communicator's graph cache
+    on new inputs and on a second stream stay bit-exact, and the cache is used (>= 3 launches of 5 calls)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_graph_cache_worker, args=(q,))
+    p.start()
+    try:
+        status, results = q.get(timeout=300)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert status == "ok", results
+    assert not [r for r in results if r[-1] == "mismatch"], results
+    launches = [r[2] for r in results if len(r) == 3 and r[1] == "graph_launches"]
+    assert launches and all(x >= 3 for x in launches), results

@@ -57,9 +57,12 @@ step_host_cost() {
   : > "$OUT/host_cost.jsonl"
   HCCL_AMD_HOST_PROFILE=1 run host_cost_default 120 python3 -u tools/host_cost_probe.py
   cat "$OUT/host_cost_default.log" | grep '^{' >> "$OUT/host_cost.jsonl"
-  HCCL_AMD_HOST_PROFILE=1 HCCL_EXEC_TIMEOUT=0 run host_cost_no_watchdog 120 python3 -u tools/host_cost_probe.py
+  HCCL_AMD_HOST_PROFILE=1 HCCL_AMD_GRAPH_CACHE=0 run host_cost_eager 120 python3 -u tools/host_cost_probe.py
+  cat "$OUT/host_cost_eager.log" | grep '^{' >> "$OUT/host_cost.jsonl"
+  HCCL_AMD_HOST_PROFILE=1 HCCL_AMD_GRAPH_CACHE=0 HCCL_EXEC_TIMEOUT=0 run host_cost_no_watchdog 120 \
+    python3 -u tools/host_cost_probe.py
   cat "$OUT/host_cost_no_watchdog.log" | grep '^{' >> "$OUT/host_cost.jsonl"
-  HCCL_AMD_HOST_PROFILE=1 HCCL_AMD_RCCL_BLOCKING=1 run host_cost_blocking 120 python3 -u tools/host_cost_probe.py
+  HCCL_AMD_HOST_PROFILE=1 HCCL_AMD_GRAPH_CACHE=0 HCCL_AMD_RCCL_BLOCKING=1 run host_cost_blocking 120 python3 -u tools/host_cost_probe.py
   cat "$OUT/host_cost_blocking.log" | grep '^{' >> "$OUT/host_cost.jsonl"
 }
 

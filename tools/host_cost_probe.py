@@ -1,7 +1,9 @@
 """Host cost of the RCCL path, one GPU, one-rank RCCL communicator (self loop).
 
 Programs (rank 0's program of an 8-rank schedule, peers mapped onto the self loop; tests/test_gpu_rccl.py self_looped):
-  ring7m   the 8-rank ring AllReduce at 7 MiB fp32 (two-stream executor; tools/rccl_soak.py's program)
+  ring7m   the 8-rank ring AllReduce at 7 MiB fp32 (two-stream executor; tools/rccl_soak.py's program); with the
+           executor graph cache on (default) the timed calls replay one captured graph, with HCCL_AMD_GRAPH_CACHE=0
+           every call is eager
   oneshot  C5's 1 KiB fp16 AllReduce, one-shot (single-stream: one transport group + one 8-input fold)
   group1k  the one-shot's transport group alone (7 sends + 7 receives of 128 B): RCCL's own enqueue cost
 For each: eager wall time per program (enqueue + GPU, K back-to-back programs then one sync), host enqueue time per
@@ -57,7 +59,8 @@ def measure(comm, name, arr, nops, x, y, single, s, dtype):
     t_graph = time.perf_counter() - t0
     del g
     groups = len({arr[i].group for i in range(nops) if arr[i].kind in (H.IrKind.SEND, H.IrKind.RECV)})
-    out = {"program": name, "records": nops, "groups": groups, "single_stream": single, "iters": ITERS,
+    out = {"program": name, "graph_cache": os.environ.get("HCCL_AMD_GRAPH_CACHE", "16"),
+           "graph_stats_launches_captures": comm.graph_stats(), "records": nops, "groups": groups, "single_stream": single, "iters": ITERS,
            "eager_us": round(t_all / ITERS * 1e6, 2), "enqueue_us": round(t_enq / ITERS * 1e6, 2),
            "graph_us": round(t_graph / ITERS * 1e6, 2),
            "host_us_by_category": {k: round(ns / ITERS / 1e3, 2) for k, (ns, _) in prof.items() if ns},
