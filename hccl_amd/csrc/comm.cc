@@ -116,7 +116,10 @@ HcclResult Comm::StartWatchdog()
         }
     }
     const uint64_t bound = RcclExecTimeoutMs();
-    if (bound != 0) watchdog = std::make_unique<Watchdog>(this, bound);
+    if (bound != 0) {
+        watchdog = std::make_unique<Watchdog>(this, bound);
+        HCCL_CHK(watchdog->Init());
+    }
     return HCCL_SUCCESS;
 }
 

@@ -113,39 +113,45 @@ struct Comm;
 uint64_t RcclExecTimeoutMs();
 uint64_t ConnectTimeoutMs();
 
-// The execution bound of a communicator whose transport is Abortable (watchdog.cc has the contract). Begin records a
-// start event on the caller's stream before the collective's work, Commit a completion event after it; the watchdog
-// thread aborts the transport once a started collective has not completed within the bound.
+// The execution bound of a communicator whose transport is Abortable (watchdog.cc has the contract). Begin enqueues
+// a start stamp on the caller's stream before the collective's work, Commit a completion stamp after it: device writes
+// of the call's sequence number into a pinned host ring, which the watchdog thread reads with plain loads (it makes
+// no HIP call, so it can never disturb another thread's stream capture). Past the bound between the two, it aborts.
 class Watchdog {
 public:
     struct Ticket {
-        hipEvent_t start = nullptr;
-        hipEvent_t done = nullptr;
+        uint64_t seq = 0;
         hipStream_t stream = nullptr;
     };
+    static constexpr uint64_t kSlots = 4096;  // collectives in flight per communicator that the watchdog follows
     Watchdog(Comm* c, uint64_t boundMs);
     ~Watchdog();
     Watchdog(const Watchdog&) = delete;
     Watchdog& operator=(const Watchdog&) = delete;
+    HcclResult Init();
     HcclResult Begin(hipStream_t s, Ticket* t);
     void Commit(Ticket* t);
 
 private:
+    struct Slot {
+        uint64_t start;
+        uint64_t done;
+    };
     struct Entry {
-        hipEvent_t start;
-        hipEvent_t done;
+        uint64_t seq;
         bool started;
         std::chrono::steady_clock::time_point t0;
     };
-    HcclResult Take(hipEvent_t* e);
     void Run();
     void Fire(HcclResult why);
     Comm* c_;
     uint64_t boundMs_;
+    volatile Slot* host_ = nullptr;  // pinned, coherent: written by the device, read by the watchdog
+    Slot* dev_ = nullptr;
+    uint64_t nextSeq_ = 0;  // under Comm::mu (Begin is called inside a collective entry)
     std::mutex mu_;
     std::condition_variable cv_;
     std::deque<Entry> pending_;
-    std::vector<hipEvent_t> free_;
     bool stop_ = false;
     bool fired_ = false;
     std::thread th_;

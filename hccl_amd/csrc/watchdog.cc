@@ -5,8 +5,11 @@
 // ExecTimeoutManager, exec_timeout_manager.cc:30-44, default CUSTOM_TIMEOUT = 1836 s, alg_param.h:79), and a failed
 // communicator takes no more work (Selector, op_common.cc:89-97). On this path the waits are inside RCCL's send/recv
 // kernels, which poll until the peer's matching message arrives. A communicator therefore keeps a watchdog thread:
-//   * every collective it runs outside stream capture is bracketed by two events on the caller's stream;
-//   * once the first has completed (the collective's work has started on the GPU), the second must complete within
+//   * every collective it runs outside stream capture is bracketed by two device-written stamps on the caller's
+//     stream (hipStreamWriteValue64 into a pinned host ring), which the thread reads with plain loads: it makes no HIP
+//     call, so it cannot invalidate a stream capture running on another thread (an earlier version polled events with
+//     hipEventQuery, and HIP failed a concurrent torch.cuda.graph capture on it even in the relaxed capture mode);
+//   * once the first stamp has landed (the collective's work has started on the GPU), the second must land within
 //     the bound; the thread also polls ncclCommGetAsyncError;
 //   * past the bound, or on an asynchronous RCCL error, it records the error (HcclGetCommAsyncError reports it at
 //     once), calls ncclCommAbort (RCCL's kernels poll the abort flag and return), and the communicator is failed:
@@ -100,9 +103,17 @@ void TeardownTrace(uint32_t rank, const char* step, bool begin)
 
 // ------------------------------------------------------------------------------------------------ watchdog
 
-Watchdog::Watchdog(Comm* c, uint64_t boundMs) : c_(c), boundMs_(boundMs)
+Watchdog::Watchdog(Comm* c, uint64_t boundMs) : c_(c), boundMs_(boundMs) {}
+
+HcclResult Watchdog::Init()
 {
+    void* h = nullptr;
+    HIP_CHK(hipHostMalloc(&h, kSlots * sizeof(Slot), hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(h, 0, kSlots * sizeof(Slot));
+    host_ = static_cast<volatile Slot*>(h);
+    HIP_CHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev_), h, 0));
     th_ = std::thread([this] { Run(); });
+    return HCCL_SUCCESS;
 }
 
 Watchdog::~Watchdog()
@@ -113,32 +124,22 @@ Watchdog::~Watchdog()
     }
     cv_.notify_all();
     if (th_.joinable()) th_.join();
-    for (Entry& e : pending_) {
-        (void)hipEventDestroy(e.start);
-        (void)hipEventDestroy(e.done);
-    }
-    for (hipEvent_t e : free_) (void)hipEventDestroy(e);
-}
-
-HcclResult Watchdog::Take(hipEvent_t* e)
-{
-    {
-        std::lock_guard<std::mutex> lk(mu_);
-        if (!free_.empty()) {
-            *e = free_.back();
-            free_.pop_back();
-            return HCCL_SUCCESS;
-        }
-    }
-    HIP_CHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    return HCCL_SUCCESS;
+    if (host_ != nullptr) (void)hipHostFree(const_cast<Slot*>(host_));
 }
 
 HcclResult Watchdog::Begin(hipStream_t s, Ticket* t)
 {
-    HCCL_CHK(Take(&t->start));
-    HCCL_CHK(Take(&t->done));
-    HIP_CHK(hipEventRecord(t->start, s));
+    const uint64_t seq = ++nextSeq_;
+    volatile Slot& slot = host_[seq % kSlots];
+    {
+        // a slot still in flight kSlots calls later: this call goes unwatched rather than overwrite it
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!pending_.empty() && seq - pending_.front().seq >= kSlots) return HCCL_E_AGAIN;
+    }
+    slot.start = 0;
+    slot.done = 0;
+    HIP_CHK(hipStreamWriteValue64(s, &dev_[seq % kSlots].start, seq, 0));
+    t->seq = seq;
     t->stream = s;
     return HCCL_SUCCESS;
 }
@@ -146,16 +147,13 @@ HcclResult Watchdog::Begin(hipStream_t s, Ticket* t)
 void Watchdog::Commit(Ticket* t)
 {
     if (t->stream == nullptr) return;
-    if (hipEventRecord(t->done, t->stream) != hipSuccess) {
-        HCCL_AMD_ERR("rank %u: watchdog could not record a completion event", c_->rank);
-        std::lock_guard<std::mutex> lk(mu_);
-        free_.push_back(t->start);
-        free_.push_back(t->done);
+    if (hipStreamWriteValue64(t->stream, &dev_[t->seq % kSlots].done, t->seq, 0) != hipSuccess) {
+        HCCL_AMD_ERR("rank %u: watchdog could not enqueue a completion stamp", c_->rank);
         t->stream = nullptr;
         return;
     }
     std::lock_guard<std::mutex> lk(mu_);
-    pending_.push_back({t->start, t->done, false, {}});
+    pending_.push_back({t->seq, false, {}});
     t->stream = nullptr;
 }
 
@@ -169,8 +167,6 @@ void RelaxCaptureMode()
 
 void Watchdog::Run()
 {
-    (void)hipSetDevice(c_->device);
-    RelaxCaptureMode();
     std::unique_lock<std::mutex> lk(mu_);
     while (!stop_) {
         // a 10 ms poll: no wake-up is paid per collective, and the bound is seconds
@@ -180,30 +176,23 @@ void Watchdog::Run()
         bool overdue = false;
         for (size_t i = 0; i < pending_.size();) {
             Entry& e = pending_[i];
-            if (!e.started) {
-                const hipError_t q = hipEventQuery(e.start);
-                if (q == hipErrorNotReady) {
-                    ++i;
-                    continue;
-                }
-                e.started = true;
-                e.t0 = now;
-            }
-            const hipError_t q = hipEventQuery(e.done);
-            if (q != hipErrorNotReady) {
-                free_.push_back(e.start);
-                free_.push_back(e.done);
+            volatile Slot& slot = host_[e.seq % kSlots];
+            if (slot.done == e.seq) {
                 pending_.erase(pending_.begin() + static_cast<std::ptrdiff_t>(i));
                 continue;
             }
-            if (!fired_ && boundMs_ != 0 &&
+            if (!e.started && slot.start == e.seq) {
+                e.started = true;
+                e.t0 = now;
+            }
+            if (e.started && !fired_ && boundMs_ != 0 &&
                 std::chrono::duration_cast<std::chrono::milliseconds>(now - e.t0).count() >
                     static_cast<int64_t>(boundMs_)) {
                 overdue = true;
             }
             ++i;
         }
-        if (fired_) continue;  // keep recycling events as the aborted work drains
+        if (fired_) continue;  // keep draining the entries as the aborted work ends
         HcclResult why = HCCL_SUCCESS;
         if (overdue) {
             why = HCCL_E_TIMEOUT;

@@ -6,8 +6,8 @@
 # GPU after it. Steps:
 #   suite          pytest -m gpu (the round-end suite), smoke, default bench
 #   rccl_failure   tests of the RCCL path's failure handling, bootstrap and capture
-#   destroy_probe  which teardown step waits on a live graph (non-blocking RCCL, finalize bounded at 5 s)
-#   destroy_probe_blocking  the same with blocking RCCL and immediate teardown (r02's conditions; ends on its limit)
+#   destroy_probe  destroy with a live graph: returns at once, the reaper tears down when the graph goes
+#   destroy_probe_immediate  the pre-r03 immediate teardown with a live graph (ends on its limit: run it last)
 #   host_cost      host enqueue cost of the RCCL path by category (default, watchdog off, blocking RCCL)
 #   ipc_pmc        rocprofv3 kernel trace + FETCH_SIZE + WRITE_SIZE of the one-sided kernel, rank mode, n = 2
 #   span_pmc       the same over a self-loop MeshChunk program (RCCL copies + folds)
@@ -45,13 +45,15 @@ step_rccl_failure() {
 }
 
 step_destroy_probe() {
-  HCCL_AMD_DEFER_DESTROY=0 HCCL_EXEC_TIMEOUT=5 run destroy_probe_immediate 60 python3 -u tools/destroy_probe.py
   run destroy_probe_deferred 60 python3 -u tools/destroy_probe.py
 }
 
-step_destroy_probe_blocking() {
-  HCCL_AMD_DEFER_DESTROY=0 HCCL_AMD_RCCL_BLOCKING=1 run destroy_probe_blocking 40 python3 -u tools/destroy_probe.py
+# r03 evidence (profiles/r03_destroy_probe_immediate.txt): with the immediate teardown ncclCommFinalize stays in
+# progress while the graph lives and ncclCommAbort then blocks too; the step ends on its limit (last in a call).
+step_destroy_probe_immediate() {
+  HCCL_AMD_DEFER_DESTROY=0 HCCL_EXEC_TIMEOUT=5 run destroy_probe_immediate 40 python3 -u tools/destroy_probe.py
 }
+
 
 step_host_cost() {
   : > "$OUT/host_cost.jsonl"
