@@ -43,9 +43,9 @@ on the capturing stream itself.
 from __future__ import annotations
 
 import datetime
-import itertools
 import os
 import threading
+import time
 from typing import Callable, List, Optional
 
 import torch
@@ -95,28 +95,49 @@ class StoreAllGather:
 class _Work(dist._Work):
     """Completion of one enqueued collective: an event recorded on the stream it was enqueued on, and a CUDA-aware
     future completed on that stream (its consumers' streams wait for it, as with the NCCL backend's futures; DDP's
-    gradient hooks chain on it)."""
+    gradient hooks chain on it).
+
+    Failures surface here as well as at the next collective: ``wait`` and ``is_success`` poll the communicator's
+    asynchronous error (HcclGetCommAsyncError: an IPC barrier timeout, an RCCL-path execution timeout or an RCCL
+    asynchronous error), and ``wait(timeout)`` blocks the host until the collective completes or the timeout passes,
+    as ProcessGroupNCCL's work does."""
 
     def __init__(self, result: List[torch.Tensor], event: Optional[torch.cuda.Event],
-                 future: Optional[torch.futures.Future] = None):
+                 future: Optional[torch.futures.Future] = None, comm: Optional["H.Comm"] = None):
         super().__init__()
         self._result = result
         self._event = event
+        self._comm = comm
         if future is None:
             future = torch.futures.Future()
             future.set_result(result)
         self._future = future
 
+    def _raise_async_error(self) -> None:
+        if self._comm is not None and self._comm.handle:
+            code = self._comm.async_error()
+            if code != 0:
+                raise H.HcclError("HcclGetCommAsyncError", code)
+
     def wait(self, timeout: Optional[datetime.timedelta] = None) -> bool:
-        if self._event is not None:
-            torch.cuda.current_stream().wait_event(self._event)
+        self._raise_async_error()
+        if self._event is None:
+            return True
+        if timeout is not None and timeout.total_seconds() > 0:
+            deadline = time.monotonic() + timeout.total_seconds()
+            while not self._event.query():
+                self._raise_async_error()
+                if time.monotonic() > deadline:
+                    raise RuntimeError(f"backend {BACKEND_NAME!r}: collective did not complete within {timeout}")
+                time.sleep(0.001)
+        torch.cuda.current_stream().wait_event(self._event)
         return True
 
     def is_completed(self) -> bool:
         return self._event is None or self._event.query()
 
     def is_success(self) -> bool:
-        return True
+        return self._comm is None or not self._comm.handle or self._comm.async_error() == 0
 
     def result(self) -> List[torch.Tensor]:
         return self._result
@@ -126,12 +147,15 @@ class _Work(dist._Work):
 
 
 class ProcessGroupHCCL(dist.ProcessGroup):
-    """One communicator per process group, created lazily on the first collective's device."""
+    """One communicator per process group, created lazily on the first collective's device.
 
-    _serial = itertools.count(1)  # every rank creates its groups in the same order, so the numbers agree
+    Its bootstrap keys live under `prefix` in the store it is given. torch hands every group's backend a store of its
+    own (a PrefixStore on the group's name, the same on every member), so the keys need no per-process numbering: a
+    counter would differ between ranks once they take part in different subgroups (torch builds no backend on a rank
+    outside a subgroup)."""
 
     def __init__(self, store, rank: int, size: int, timeout: datetime.timedelta,
-                 comm_factory: Optional[Callable[[int], "H.Comm"]] = None):
+                 comm_factory: Optional[Callable[[int], "H.Comm"]] = None, prefix: str = "hccl_amd"):
         super().__init__(rank, size)
         self._store = store
         self._timeout = timeout
@@ -140,7 +164,7 @@ class ProcessGroupHCCL(dist.ProcessGroup):
         self._stream: Optional[torch.cuda.Stream] = None
         self._lock = threading.Lock()
         self._factory = comm_factory or self._make_comm
-        self._prefix = f"hccl_amd/pg{next(ProcessGroupHCCL._serial)}"
+        self._prefix = prefix
 
     # ------------------------------------------------------------------------------------------------ communicator
     def _make_comm(self, device: int) -> "H.Comm":
@@ -187,7 +211,7 @@ class ProcessGroupHCCL(dist.ProcessGroup):
                 fn(comm, cur)
                 fut = torch.futures.Future(devices=[torch.device("cuda", torch.cuda.current_device())])
                 fut.set_result(result)
-                return _Work(result, None, fut)
+                return _Work(result, None, fut, comm)
             if self._stream is None:
                 self._stream = torch.cuda.Stream()
             side = self._stream
@@ -200,7 +224,7 @@ class ProcessGroupHCCL(dist.ProcessGroup):
             fut = torch.futures.Future(devices=[torch.device("cuda", torch.cuda.current_device())])
             with torch.cuda.stream(side):
                 fut.set_result(result)  # marks the result ready on the group's stream
-        return _Work(result, ev, fut)
+        return _Work(result, ev, fut, comm)
 
     # ------------------------------------------------------------------------------------------------ collectives
     def allreduce(self, tensors: List[torch.Tensor], opts) -> _Work:
@@ -276,7 +300,7 @@ class ProcessGroupHCCL(dist.ProcessGroup):
         t = tensors[opts.rootTensor]
         self._check(t, "broadcast tensor")
         root = opts.rootRank
-        raw = t.view(torch.uint8)
+        raw = t.reshape(-1).view(torch.uint8)  # contiguous: a view (a 0-dim tensor has no byte view of its own)
         m = raw.numel()
         flat = torch.empty(m * self.size(), dtype=torch.uint8, device=t.device)
 

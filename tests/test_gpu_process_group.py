@@ -100,6 +100,15 @@ def _rank_main(rank, n, port, transport, q):
         parts = [torch.empty(777, dtype=torch.bfloat16, device="cuda") for _ in range(n)]
         dist.all_gather(parts, a)
         checks["all_gather_list"] = all(bool(torch.all(p == q).item()) for q, p in enumerate(parts))
+        # --- broadcast of a 0-dim tensor (a seed or a loss; ADVICE r02: the byte view needs a reshape first)
+        seed = torch.tensor(1000.0 + rank, device="cuda")
+        dist.broadcast(seed, src=n - 1)
+        checks["broadcast_0dim"] = float(seed.item()) == 1000.0 + (n - 1)
+        # --- work.wait(timeout) blocks until the collective is done and reports success
+        wz = torch.full((4096,), 2.0, device="cuda")
+        work = dist.all_reduce(wz, async_op=True)
+        work.wait(timeout=datetime.timedelta(seconds=60))
+        checks["wait_timeout_and_success"] = work.is_success() and bool(torch.all(wz == 2.0 * n).item())
         # --- async work on a side stream, then wait() orders the current stream after it
         s = torch.cuda.Stream()
         z = torch.full((1 << 20,), 1.0, device="cuda")

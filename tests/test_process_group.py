@@ -70,7 +70,65 @@ def test_group_creation_and_host_checks():
     with pytest.raises(ValueError, match="SUM, PRODUCT, MAX and MIN"):
         opts.reduceOp = dist.ReduceOp.AVG
         pg.allreduce([torch.zeros(4)], opts)
-    # two groups made in the same order on every rank get the same, distinct store prefixes
+    # the keys live under a fixed prefix of the store torch gives each group (a PrefixStore on the group name)
     pg2 = PG._create(store, 0, 1, datetime.timedelta(seconds=30))
-    assert pg._prefix != pg2._prefix
+    assert pg._prefix == pg2._prefix == "hccl_amd"
     pg.shutdown()  # no communicator yet: nothing to destroy
+
+
+def _subgroup_rank(rank, n, port, q):
+    """Overlapping subgroups ([0, 1] then [1, 2]) over the "hccl" backend: each subgroup's bootstrap key must be the
+    same on its members, although rank 0 and rank 2 each build only one of the two backends (a per-process
+    counter had rank 1 and rank 2 disagree on the second group's key, and its first collective hung)."""
+    import os
+    os.environ["HCCL_AMD_PG_TRANSPORT"] = ""
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n,
+                                timeout=datetime.timedelta(seconds=60))
+        blobs = {}
+
+        def fake_root_info():
+            return f"root-of-{rank}".encode()
+
+        def fake_init(size, blob, r):
+            blobs[len(blobs)] = (size, bytes(blob), r)
+            return object()
+
+        H.get_root_info, H.comm_init_root_info = fake_root_info, fake_init
+        got = {}
+        for members in ([0, 1], [1, 2]):
+            g = dist.new_group(members, backend="hccl")
+            if rank in members:
+                # a ProcessGroup subclass is the group itself (torch's _new_process_group_helper)
+                be = g if isinstance(g, PG.ProcessGroupHCCL) else g._get_backend(torch.device("cuda"))
+                be._factory(0)  # the bootstrap: the group's rank 0 publishes, every member reads
+                got[tuple(members)] = blobs[len(blobs) - 1]
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, got))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, f"{type(e).__name__}: {e}"))
+
+
+def test_overlapping_subgroups_agree_on_the_bootstrap_key():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_subgroup_rank, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    try:
+        got = dict(q.get(timeout=120) for _ in procs)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r in range(3):
+        assert isinstance(got[r], dict), got
+    # group [0, 1]: group rank 0 is global rank 0; group [1, 2]: group rank 0 is global rank 1
+    assert got[0][(0, 1)] == (2, b"root-of-0", 0) and got[1][(0, 1)] == (2, b"root-of-0", 1)
+    assert got[1][(1, 2)] == (2, b"root-of-1", 0) and got[2][(1, 2)] == (2, b"root-of-1", 1)

@@ -6,6 +6,7 @@
 # GPU after it. Steps:
 #   suite          pytest -m gpu (the round-end suite), smoke, default bench
 #   rccl_failure   tests of the RCCL path's failure handling, bootstrap and capture
+#   pg             the torch.distributed backend's GPU tests
 #   destroy_probe  destroy with a live graph: returns at once, the reaper tears down when the graph goes
 #   destroy_probe_immediate  the pre-r03 immediate teardown with a live graph (ends on its limit: run it last)
 #   host_cost      host enqueue cost of the RCCL path by category (default, watchdog off, blocking RCCL)
@@ -42,6 +43,11 @@ step_suite() {
 step_rccl_failure() {
   run rccl_failure 600 python3 -u -m pytest tests/test_gpu_rccl_failure.py tests/test_gpu_bootstrap.py \
     tests/test_gpu_rccl.py -v -s --timeout 200 --timeout-method thread -p no:cacheprovider
+}
+
+step_pg() {
+  run pg 400 python3 -u -m pytest tests/test_gpu_process_group.py -v --timeout 300 --timeout-method thread \
+    -p no:cacheprovider
 }
 
 step_destroy_probe() {
