@@ -236,6 +236,7 @@ struct Reaper {
     std::mutex mu;
     std::condition_variable cv;
     std::vector<Comm*> pending;
+    uint32_t active = 0;  // teardowns in progress on the reaper thread
     bool started = false;
 };
 
@@ -282,10 +283,13 @@ void ReaperLoop()
                 continue;
             }
             r.pending.erase(r.pending.begin() + static_cast<std::ptrdiff_t>(i));
+            ++r.active;
             lk.unlock();
             TeardownTrace(c->rank, "deferred destroy (reaper)", true);
             delete c;
             lk.lock();
+            --r.active;
+            r.cv.notify_all();
         }
     }
 }
@@ -316,6 +320,15 @@ HcclResult NoteCapture(Comm& c, hipStream_t s)
     return HCCL_SUCCESS;
 }
 
+// At process exit, a teardown the reaper has begun is let finish (bounded): exiting under it races RCCL's own
+// teardown. Communicators still held by live graphs are left as they are.
+void WaitForReaperAtExit()
+{
+    Reaper& r = TheReaper();
+    std::unique_lock<std::mutex> lk(r.mu);
+    r.cv.wait_for(lk, std::chrono::seconds(10), [&] { return r.active == 0; });
+}
+
 bool DeferDestroy(Comm* c)
 {
     if (!EnvFlag("HCCL_AMD_DEFER_DESTROY", true)) return false;  // diagnostics: tear down at once, as before r03
@@ -327,6 +340,7 @@ bool DeferDestroy(Comm* c)
     if (!r.started) {
         r.started = true;
         std::thread(ReaperLoop).detach();
+        std::atexit(WaitForReaperAtExit);
     }
     r.cv.notify_all();
     return true;
@@ -336,7 +350,7 @@ uint32_t PendingDestroys()
 {
     Reaper& r = TheReaper();
     std::lock_guard<std::mutex> lk(r.mu);
-    return static_cast<uint32_t>(r.pending.size());
+    return static_cast<uint32_t>(r.pending.size()) + r.active;
 }
 
 }  // namespace hccl_amd

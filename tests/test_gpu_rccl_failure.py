@@ -25,7 +25,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _child(target, env, wait):
+def _child(target, env, wait, clean_exit=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=target, args=(q, env))
@@ -47,6 +47,8 @@ def _child(target, env, wait):
     assert got is not None, f"child did not report within {wait} s (exit code {p.exitcode})"
     status, res = got
     assert status == "ok", res
+    if clean_exit:
+        assert p.exitcode == 0, f"child exited with {p.exitcode} after reporting {res}"
     return res
 
 
@@ -191,7 +193,7 @@ def _graph_destroy_worker(q, env):
 
 
 def test_destroy_with_a_live_graph_returns():
-    res = _child(_graph_destroy_worker, {"HCCL_AMD_TEARDOWN_TRACE": "1"}, wait=120)
+    res = _child(_graph_destroy_worker, {"HCCL_AMD_TEARDOWN_TRACE": "1"}, wait=120, clean_exit=True)
     print(res)
     assert res["replay_ok"], res
     assert res["destroy_s"] < 5.0, res
