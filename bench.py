@@ -18,6 +18,7 @@ Every run prints exactly one JSON line on rank 0 (extra diagnostics go to stderr
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import platform
@@ -119,6 +120,35 @@ def c1_sim_replay() -> dict:
     med = float(np.median(times))
     return {"workload": "C1: 2-rank AllReduce SUM 1 MiB fp32, schedule replay on host (one-shot, order O1)",
             "us": round(med * 1e6, 1), "GiBps_per_rank_input": round((1 << 20) / med / GIB, 3), "cores": 1}
+
+
+def cpu_baseline_allreduce(world: int, algo: int, nbytes: int = 16 << 20, budget_s: float = 10.0) -> dict:
+    """The reference's CPU path at N > 1: every rank's program of this N-rank AllReduce (fp32 SUM, `nbytes` per rank,
+    the headline's schedule) replayed on the host by the oracle's sim world (AicpuReduceTemplate folds, one FIFO per
+    rank pair; one core), timed within a bounded budget. value = whole-job reduced input GiB/s, the unit of the line's
+    `value`."""
+    from oracle import oracle as O  # checker / baseline only
+
+    count = nbytes // 4
+    progs, scratch = [], 0
+    for r in range(world):
+        arr, nops, _, se = H.build_schedule(H.OpType.ALLREDUCE, algo, world, r, count, H.HcclDataType.FP32)
+        progs.append((arr, nops))
+        scratch = max(scratch, se)
+    rng = np.random.default_rng(0x5EED0004)
+    xs = [rng.random(count, dtype=np.float32) for _ in range(world)]
+    times = []
+    t_end = time.perf_counter() + budget_s
+    while len(times) < 2 or (time.perf_counter() < t_end and len(times) < 10):
+        bufs = [[x.copy(), np.zeros(count, np.float32), np.zeros(max(scratch, 1), np.float32)] for x in xs]
+        t0 = time.perf_counter()
+        assert O.replay(world, O.FP32, O.SUM, progs, bufs) == 0
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return {"value": round(world * nbytes / med / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{world}-rank AllReduce fp32 SUM, {nbytes >> 20} MiB per rank, {H.Algo(algo).name} schedule: "
+                      f"every rank's program replayed on the host by the oracle's sim world, {len(times)} passes, "
+                      f"median; host {cpu_model()}"}
 
 
 def end_to_end_host(steps: int = 5, chunk: int = 64 << 20) -> dict:
@@ -312,6 +342,13 @@ def bench_local(args) -> dict:
             "kernel_p10_us": round(float(np.percentile(per, 10)) * 1e6, 2),
             "kernel_p90_us": round(float(np.percentile(per, 90)) * 1e6, 2),
         },
+        # the same quantities at every N: buffer bytes per GPU per second (algbw), the bytes the
+        # bounding resource moves per second (busbw: HBM here, xGMI at N > 1) and its fraction of that roofline
+        "per_gpu": {"workload": "C2", "bytes_per_gpu_per_step": C2_COUNT * 4,
+                    "algbw_GBps": round(C2_COUNT * 4 / (total / args.steps) / 1e9, 2),
+                    "busbw_GBps": round(bytes_step / (total / args.steps) / 1e9, 2), "bound": "hbm",
+                    "roofline_peak_GBps": HBM_PEAK_GBPS,
+                    "frac": round(bytes_step / (total / args.steps) / 1e9 / HBM_PEAK_GBPS, 4)},
     }
     # the same stream shapes on PyTorch's own kernels, same buffers and stream: the vendor-library baseline for this
     # op (torch.add, 2 reads + 1 write) and the 1 read + 1 write copy, as measured context for `frac`
@@ -719,6 +756,29 @@ def bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
         return _bench_allreduce(args, rank, world, local_rank)
 
 
+def _failed_line(args, world: int, rank: int, code: int, after_s: float, fallback) -> dict:
+    """The line of an N > 1 run whose headline loop failed (a rank's communicator timed out or errored)."""
+    import torch.distributed as dist
+
+    try:
+        name = H.HcclResult(code).name
+    except ValueError:
+        name = str(code)
+    dist.destroy_process_group()
+    if rank != 0:
+        return None
+    return {"metric": "device-resident reduce GiB/s (fp32 sum) vs HBM peak; ring all-reduce bus GB/s", "value": 0.0,
+            "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": None,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (uniform [-1,1) fp32, device-generated)",
+            "config": {"workload": "C3: HcclAllReduce fp32 SUM, 4 GiB per rank", "bytes_per_rank": C3_BYTES,
+                       "parallelism": f"allreduce x{world}"},
+            "error": {"code": name, "after_s": round(after_s, 1), "exec_timeout_s": os.environ.get("HCCL_EXEC_TIMEOUT"),
+                      "note": "the headline loop failed on some rank (HcclGetCommAsyncError / entry code, max over "
+                              "ranks): an execution timeout aborts the communicator instead of hanging"},
+            "headline_fallback": fallback, "transport": _transport_info()}
+
+
 def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     import torch.distributed as dist
 
@@ -732,7 +792,8 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     with _stdout_to_stderr():  # gloo announces its connections on stdout, which carries only the JSON line
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # a rank lost on the host ends the others' gloo waits after 10 minutes, not gloo's default 30
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=600))
 
     def _all_gather(b):
         out = [None] * world
@@ -790,10 +851,22 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     e0, e1 = evs[0], evs[-1]
     t0 = time.perf_counter()
     e0.record(stream)
-    for k in range(args.steps):
-        comm.all_reduce(send, recv, H.HcclReduceOp.SUM, stream)
-        evs[k + 1].record(stream)
+    # The timed loop is bounded: a rank whose peer is lost has its communicator aborted by the library's watchdog
+    # past HCCL_EXEC_TIMEOUT (main() sets 120 s unless given), the synchronize then returns, and the line reports the
+    # error instead of the run hanging until the driver kills it.
+    loop_err = 0
+    try:
+        for k in range(args.steps):
+            comm.all_reduce(send, recv, H.HcclReduceOp.SUM, stream)
+            evs[k + 1].record(stream)
+    except H.HcclError as e:
+        loop_err = e.code
     torch.cuda.synchronize()
+    loop_err = loop_err or comm.async_error()
+    bad = torch.tensor([loop_err], dtype=torch.int32)
+    dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+    if bad.item():
+        return _failed_line(args, world, rank, int(bad.item()), time.perf_counter() - t0, fallback)
     dist.barrier()
     wall = time.perf_counter() - t0
     # per-step durations (median and p10/p90), each step's max over ranks
@@ -821,6 +894,7 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     result_ok = bool(ok.item())
     del check
+    graph_launches, graph_captures = comm.graph_stats()
     comm.destroy()
     g = torch.Generator(device=dev).manual_seed(0x5EED0003 + rank)
     send.copy_(torch.rand(count, device=dev, generator=g).mul_(2).sub_(1))
@@ -851,6 +925,12 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
                     "p90": round(float(np.percentile(steps_ms.numpy(), 90)), 3),
                     "note": "per-step HIP-event durations on the launch stream, max over ranks per step"},
         "transport": _transport_info(),
+        "executor_graphs": {"launches": graph_launches, "captures": graph_captures,
+                            "note": "rank 0's calls served by one hipGraphLaunch of the captured executor program "
+                                    "(HCCL_AMD_GRAPH_CACHE); the first call of a shape runs eagerly"},
+        "per_gpu": {"workload": "C3", "bytes_per_gpu_per_step": C3_BYTES, "algbw_GBps": round(algbw, 2),
+                    "busbw_GBps": round(busbw, 2), "bound": "xgmi", "roofline_peak_GBps": round(xgmi_peak, 1),
+                    "frac": None if harness else round(busbw / xgmi_peak, 4)},
         "result_ok": result_ok,
         "result_ok_algorithm": verified_algo,
         "headline_fallback": fallback,
@@ -896,6 +976,16 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     if not args.no_rccl_ref:
         wd.stage("rccl_allreduce_reference")
         res["rccl_allreduce_reference"] = rccl_allreduce_reference(send, recv, world, args)
+    if not args.no_cpu_baseline and rank == 0:
+        # the reference's CPU path on this box's host cores, beside the line (BASELINE.json north_star): the C2 leg
+        # and this N's AllReduce program replayed on the host at a stated size
+        wd.stage("cpu_baseline")
+        try:
+            cb = cpu_baseline_allreduce(world, int(headline))
+            cb["c2"] = cpu_baseline_c2(args.cpu_budget)
+            res["cpu_baseline"] = cb
+        except Exception as e:  # noqa: BLE001
+            res["cpu_baseline"] = {"error": f"{type(e).__name__}: {e}"}
     wd.cancel()
     dist.destroy_process_group()
     return res if rank == 0 else None
@@ -950,6 +1040,9 @@ def main():
     # a lost peer ends an IPC launch after this long (status bit 0, sticky per communicator) instead of 60 s, so a
     # failing secondary row cannot stretch the driver's run
     os.environ.setdefault("HCCL_AMD_IPC_TIMEOUT_MS", "10000")
+    # the RCCL path's execution bound (the library's watchdog aborts a communicator whose collective has not finished
+    # this long after it started): a lost rank ends the N > 1 run with a line
+    os.environ.setdefault("HCCL_EXEC_TIMEOUT", "120")
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)

@@ -13,6 +13,7 @@
 #   ipc_pmc        rocprofv3 kernel trace + FETCH_SIZE + WRITE_SIZE of the one-sided kernel, rank mode, n = 2
 #   span_pmc       the same over a self-loop MeshChunk program (RCCL copies + folds)
 #   bench          bench.py default line
+#   harness        bench.py's N > 1 code path with two ranks sharing the GPU (IPC-only; a crash check, not a result)
 #   counters       the TCC counters this rocprofv3 offers
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
@@ -115,6 +116,10 @@ step_span_pmc() {
 step_bench() {
   run bench 300 python3 bench.py
   grep '^{' "$OUT/bench.log" > "$OUT/bench.json" || true
+}
+
+step_harness() {
+  run harness_n2 420 bash tools/gpu_harness_n2.sh
 }
 
 step_counters() {
