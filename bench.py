@@ -272,7 +272,60 @@ def fold_roofline(dev, stream, n: int = 8, reps: int = 10) -> dict:
             "kernel_avg_us": round(kavg * 1e6, 1), "kernel_median_us": round(float(np.median(per)) * 1e6, 1),
             "achieved_GBps": round(nbytes / kavg / 1e9, 1), "peak_GBps": HBM_PEAK_GBPS,
             "frac": round(nbytes / kavg / 1e9 / HBM_PEAK_GBPS, 4),
-            "traffic": load_pmc_traffic("r02b_pmc_fold_n8.json"), "result_ok": ok}
+            "traffic": load_pmc_traffic("r03b_pmc_fold_n8.json") or load_pmc_traffic("r02b_pmc_fold_n8.json"),
+            "result_ok": ok}
+
+
+def ipc_two_shot_roofline(dev, n: int = 2, mib: int = 512, reps: int = 10) -> dict:
+    """The one-sided kernel (k_ipc_collective, the AIV engine's analogue) on one GPU: an n-rank
+    loopback world (every rank's blocks in one launch on rank 0's stream, each rank driven from its own host thread),
+    two-shot AllReduce fp32 SUM of `mib` MiB per rank. Per rank and launch the kernel reads and writes
+    2(3n-2)/n bytes per input byte (phase 0 stores (n-1)/n of the input into the owners' slots, phase 1 folds the own
+    chunk and n-1 slots and writes n results, phase 2 copies n-1 results), all of it this GPU's HBM here. Checked
+    against torch's add in the two-shot order O2 (acc = x0; acc = x1 + acc)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    comms = H.loopback_world(n)
+    count = (mib << 20) // 4
+    g = torch.Generator(device=dev).manual_seed(0x5EED0009)
+    xs = [torch.rand(count, device=dev, generator=g).mul_(2).sub_(1) for _ in range(n)]
+    ys = [torch.empty_like(x) for x in xs]
+    streams = [torch.cuda.Stream() for _ in range(n)]
+    torch.cuda.synchronize()
+    pool = ThreadPoolExecutor(n)
+    try:
+        for c in comms:
+            c.set_algo(H.Algo.IPC_TWOSHOT)
+
+        def call():
+            list(pool.map(lambda r: comms[r].all_reduce(xs[r], ys[r], H.HcclReduceOp.SUM, streams[r]), range(n)))
+
+        call()  # set-up (staging, peer pointers) on the first call
+        torch.cuda.synchronize()
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+        evs[0].record(streams[0])
+        for k in range(reps):
+            call()
+            evs[k + 1].record(streams[0])  # the world's launch runs on rank 0's stream
+        torch.cuda.synchronize()
+        per = [evs[k].elapsed_time(evs[k + 1]) / 1e3 for k in range(reps)]
+        want = torch.add(xs[1], xs[0]) if n == 2 else None
+        ok = want is not None and all(bool(torch.equal(y, want)) for y in ys)
+        ran = H.Algo(comms[0].last_algo).name
+        timeouts = comms[0].ipc_status() & 1
+    finally:
+        pool.shutdown()
+        for c in comms:
+            c.destroy()
+    nbytes = n * 2 * (3 * n - 2) * count * 4 // n
+    kavg = float(np.mean(per))
+    return {"kernel": "k_ipc_collective<EFp<float>, SUM> (two-shot AllReduce, loopback world)", "ranks": n,
+            "bytes_per_rank": count * 4, "ran": ran, "algorithmic_bytes_per_launch": nbytes,
+            "kernel_avg_us": round(kavg * 1e6, 1), "kernel_median_us": round(float(np.median(per)) * 1e6, 1),
+            "achieved_GBps": round(nbytes / kavg / 1e9, 1), "peak_GBps": HBM_PEAK_GBPS,
+            "frac": round(nbytes / kavg / 1e9 / HBM_PEAK_GBPS, 4),
+            "traffic": load_pmc_traffic("r03b_pmc_ipc_two_shot.json"), "barrier_timeouts": timeouts,
+            "result_ok": ok}
 
 
 def bench_local(args) -> dict:
@@ -334,7 +387,7 @@ def bench_local(args) -> dict:
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": load_pmc_traffic("r02b_pmc_local_reduce.json"),
+            "traffic": load_pmc_traffic("r03b_pmc_local_reduce.json") or load_pmc_traffic("r02b_pmc_local_reduce.json"),
             "kernel": "k_reduce2<EFp<float>, SUM>",
             "algorithmic_bytes_per_launch": bytes_step,
             "kernel_avg_us": round(kavg * 1e6, 2),
@@ -381,6 +434,10 @@ def bench_local(args) -> dict:
         res["other_kernels"] = {"fold_n8": fold_roofline(dev, stream)}
     except Exception as e:  # noqa: BLE001
         res["other_kernels"] = {"fold_n8": {"error": f"{type(e).__name__}: {e}"}}
+    try:
+        res["other_kernels"]["ipc_two_shot"] = ipc_two_shot_roofline(dev)
+    except Exception as e:  # noqa: BLE001
+        res["other_kernels"]["ipc_two_shot"] = {"error": f"{type(e).__name__}: {e}"}
     if not args.no_e2e:
         try:
             res["end_to_end_host_buffers"] = end_to_end_host()

@@ -13,6 +13,7 @@
 #   ipc_pmc        rocprofv3 kernel trace + FETCH_SIZE + WRITE_SIZE of the one-sided kernel, rank mode, n = 2
 #   span_pmc       the same over a self-loop MeshChunk program (RCCL copies + folds)
 #   bench          bench.py default line
+#   profile        tools/profile_round.sh: rocprofv3 trace + FETCH/WRITE of the N=1 bench line, per-kernel summaries
 #   harness        bench.py's N > 1 code path with two ranks sharing the GPU (IPC-only; a crash check, not a result)
 #   counters       the TCC counters this rocprofv3 offers
 set -o pipefail
@@ -116,6 +117,10 @@ step_span_pmc() {
 step_bench() {
   run bench 300 python3 bench.py
   grep '^{' "$OUT/bench.log" > "$OUT/bench.json" || true
+}
+
+step_profile() {
+  run profile_round 1000 bash tools/profile_round.sh "${PROFILE_TAG:-r03b}"
 }
 
 step_harness() {

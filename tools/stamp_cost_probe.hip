@@ -23,10 +23,12 @@
         }                                                                               \
     } while (0)
 
-__global__ void k_work(float* x, int n, uint64_t* stamp, unsigned* arrivals, uint64_t v)
+__global__ void k_work(float* x, int n, uint64_t* stamp, unsigned* arrivals, uint64_t v, uint64_t spinTicks)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) x[i] = x[i] * 0.5f + 1.0f;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < spinTicks) __builtin_amdgcn_s_sleep(2);
     if (stamp == nullptr) return;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -62,14 +64,16 @@ int main()
     hipEvent_t ev;
     CHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     const char* names[] = {"none", "event", "write1", "write2", "kernel1", "fused"};
-    for (int rep = 0; rep < 2; ++rep) {
+    // rep 1: host-bound (tiny kernel); rep 2: GPU-bound (each kernel spins 20 us), where a stamp's GPU-side cost shows
+    for (int rep = 0; rep < 3; ++rep) {
+        const uint64_t spin = rep == 2 ? 2000 : 0;  // 100 MHz ticks
         for (int v = 0; v < 6; ++v) {
             CHK(hipStreamSynchronize(s));
             const auto t0 = std::chrono::steady_clock::now();
             for (int k = 0; k < iters; ++k) {
                 if (v == 3) CHK(hipStreamWriteValue64(s, dev, k, 0));
                 hipLaunchKernelGGL(k_work, dim3(n / 256), dim3(256), 0, s, x, n, v == 5 ? dev + 1 : nullptr, arrivals,
-                                   uint64_t(k));
+                                   uint64_t(k), spin);
                 if (v == 1) CHK(hipEventRecord(ev, s));
                 if (v == 2 || v == 3) CHK(hipStreamWriteValue64(s, dev + 1, k, 0));
                 if (v == 4) hipLaunchKernelGGL(k_stamp, dim3(1), dim3(64), 0, s, dev + 1, uint64_t(k));
@@ -77,10 +81,10 @@ int main()
             const auto t1 = std::chrono::steady_clock::now();
             CHK(hipStreamSynchronize(s));
             const auto t2 = std::chrono::steady_clock::now();
-            if (rep == 1) {
-                std::printf("{\"variant\": \"%s\", \"us_per_call\": %.2f, \"enqueue_us_per_call\": %.2f, "
-                            "\"last_stamp\": %llu}\n",
-                            names[v], std::chrono::duration<double, std::micro>(t2 - t0).count() / iters,
+            if (rep >= 1) {
+                std::printf("{\"regime\": \"%s\", \"variant\": \"%s\", \"us_per_call\": %.2f, "
+                            "\"enqueue_us_per_call\": %.2f, \"last_stamp\": %llu}\n",
+                            rep == 1 ? "host-bound" : "gpu-bound (20 us kernel)", names[v], std::chrono::duration<double, std::micro>(t2 - t0).count() / iters,
                             std::chrono::duration<double, std::micro>(t1 - t0).count() / iters,
                             (unsigned long long)host[1]);
             }
