@@ -114,14 +114,16 @@ uint64_t RcclExecTimeoutMs();
 uint64_t ConnectTimeoutMs();
 
 // The execution bound of a communicator whose transport is Abortable (watchdog.cc has the contract). Begin enqueues
-// a start stamp on the caller's stream before the collective's work, Commit a completion stamp after it: device writes
-// of the call's sequence number into a pinned host ring, which the watchdog thread reads with plain loads (it makes
-// no HIP call, so it can never disturb another thread's stream capture). Past the bound between the two, it aborts.
+// a start stamp on the caller's stream before the collective's work (or, for a small single-stream program, lets the
+// start be inferred), Commit a completion stamp after it: device stores of the call's sequence number into a pinned
+// host ring (k_stamp), which the watchdog thread reads with plain loads (it makes no HIP call, so it can never
+// disturb another thread's stream capture). Past the bound between the two, it aborts.
 class Watchdog {
 public:
     struct Ticket {
         uint64_t seq = 0;
         hipStream_t stream = nullptr;
+        bool stamped = false;
     };
     static constexpr uint64_t kSlots = 4096;  // collectives in flight per communicator that the watchdog follows
     Watchdog(Comm* c, uint64_t boundMs);
@@ -129,7 +131,9 @@ public:
     Watchdog(const Watchdog&) = delete;
     Watchdog& operator=(const Watchdog&) = delete;
     HcclResult Init();
-    HcclResult Begin(hipStream_t s, Ticket* t);
+    // stampStart = false: no start stamp; the collective counts as started once every earlier watched collective of
+    // the communicator has completed (at once if none is outstanding).
+    HcclResult Begin(hipStream_t s, Ticket* t, bool stampStart = true);
     void Commit(Ticket* t);
 
 private:
@@ -139,6 +143,7 @@ private:
     };
     struct Entry {
         uint64_t seq;
+        bool stamped;  // a start stamp was enqueued
         bool started;
         std::chrono::steady_clock::time_point t0;
     };
@@ -160,9 +165,9 @@ private:
 // Brackets one collective's work with the watchdog's events (nothing when wd is null or the stream is capturing).
 class WatchScope {
 public:
-    WatchScope(Watchdog* wd, hipStream_t s) : wd_(wd)
+    WatchScope(Watchdog* wd, hipStream_t s, bool stampStart = true) : wd_(wd)
     {
-        if (wd_ != nullptr && wd_->Begin(s, &t_) != HCCL_SUCCESS) wd_ = nullptr;
+        if (wd_ != nullptr && wd_->Begin(s, &t_, stampStart) != HCCL_SUCCESS) wd_ = nullptr;
     }
     ~WatchScope()
     {
@@ -293,7 +298,8 @@ bool DeferDestroy(Comm* c);
 uint32_t PendingDestroys();
 // HCCL_AMD_TEARDOWN_TRACE=1: time-stamped steps of ~Comm on stderr.
 void TeardownTrace(uint32_t rank, const char* step, bool begin);
-// The injected stall kernel (fault_inject.hip).
+// The watchdog's stamp and the injected stall (watch_kernels.hip).
+HcclResult LaunchStamp(uint64_t* slot, uint64_t seq, hipStream_t stream);
 HcclResult LaunchStall(const uint32_t* word, uint64_t maxMs, hipStream_t stream);
 
 // HCCL_BUFFSIZE (MB, default 200) in bytes; staging per communicator is twice that. Must be equal on every rank: the

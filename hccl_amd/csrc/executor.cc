@@ -411,7 +411,7 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
     // The execution bound (watchdog.cc): this call's work on `user`, bracketed by the watchdog's events. A captured
     // call runs later, from a graph, outside any entry: not tracked.
     HpScope hpTotal(HCCL_AMD_HP_EXECUTE);
-    WatchScope watch(captured ? nullptr : c.watchdog.get(), user);
+    WatchScope watch(captured ? nullptr : c.watchdog.get(), user, !singleStream);
     if (singleStream) return ExecuteSingleStream(c, ops, bufs, dt, op, user, captured);
     const uint64_t es = DataTypeSize(dt);
     // Under stream capture the transport groups go on the capturing stream itself and only the folds on a forked

@@ -6,11 +6,14 @@
 // communicator takes no more work (Selector, op_common.cc:89-97). On this path the waits are inside RCCL's send/recv
 // kernels, which poll until the peer's matching message arrives. A communicator therefore keeps a watchdog thread:
 //   * every collective it runs outside stream capture is bracketed by two device-written stamps on the caller's
-//     stream (hipStreamWriteValue64 into a pinned host ring), which the thread reads with plain loads: it makes no HIP
+//     stream (k_stamp stores into a pinned host ring), which the thread reads with plain loads: it makes no HIP
 //     call, so it cannot invalidate a stream capture running on another thread (an earlier version polled events with
 //     hipEventQuery, and HIP failed a concurrent torch.cuda.graph capture on it even in the relaxed capture mode);
-//   * once the first stamp has landed (the collective's work has started on the GPU), the second must land within
-//     the bound; the thread also polls ncclCommGetAsyncError;
+//   * once the start stamp has landed (the collective's work has started on the GPU), the completion stamp must land
+//     within the bound; the thread also polls ncclCommGetAsyncError. A small single-stream program (<= 1 MiB) has no
+//     start stamp (each stamp costs about 1.8 us of GPU time): it counts as started once every earlier watched
+//     collective of the communicator has completed, so user work queued between two collectives on a stream counts
+//     against the later one's bound;
 //   * past the bound, or on an asynchronous RCCL error, it records the error (HcclGetCommAsyncError reports it at
 //     once), calls ncclCommAbort (RCCL's kernels poll the abort flag and return), and the communicator is failed:
 //     the next collective entry returns the error (HCCL_E_TIMEOUT), every later one HCCL_E_SUSPENDING (Comm::Gate).
@@ -127,7 +130,7 @@ Watchdog::~Watchdog()
     if (host_ != nullptr) (void)hipHostFree(const_cast<Slot*>(host_));
 }
 
-HcclResult Watchdog::Begin(hipStream_t s, Ticket* t)
+HcclResult Watchdog::Begin(hipStream_t s, Ticket* t, bool stampStart)
 {
     const uint64_t seq = ++nextSeq_;
     volatile Slot& slot = host_[seq % kSlots];
@@ -138,22 +141,23 @@ HcclResult Watchdog::Begin(hipStream_t s, Ticket* t)
     }
     slot.start = 0;
     slot.done = 0;
-    HIP_CHK(hipStreamWriteValue64(s, &dev_[seq % kSlots].start, seq, 0));
+    if (stampStart) HCCL_CHK(LaunchStamp(&dev_[seq % kSlots].start, seq, s));
     t->seq = seq;
     t->stream = s;
+    t->stamped = stampStart;
     return HCCL_SUCCESS;
 }
 
 void Watchdog::Commit(Ticket* t)
 {
     if (t->stream == nullptr) return;
-    if (hipStreamWriteValue64(t->stream, &dev_[t->seq % kSlots].done, t->seq, 0) != hipSuccess) {
+    if (LaunchStamp(&dev_[t->seq % kSlots].done, t->seq, t->stream) != HCCL_SUCCESS) {
         HCCL_AMD_ERR("rank %u: watchdog could not enqueue a completion stamp", c_->rank);
         t->stream = nullptr;
         return;
     }
     std::lock_guard<std::mutex> lk(mu_);
-    pending_.push_back({t->seq, false, {}});
+    pending_.push_back({t->seq, t->stamped, false, {}});
     t->stream = nullptr;
 }
 
@@ -181,7 +185,8 @@ void Watchdog::Run()
                 pending_.erase(pending_.begin() + static_cast<std::ptrdiff_t>(i));
                 continue;
             }
-            if (!e.started && slot.start == e.seq) {
+            // started: its start stamp landed, or (no start stamp) every earlier watched collective has completed
+            if (!e.started && (e.stamped ? slot.start == e.seq : i == 0)) {
                 e.started = true;
                 e.t0 = now;
             }
