@@ -40,7 +40,11 @@ extern HcclResult HcclReduceScatter(void* sendBuf, void* recvBuf, uint64_t recvC
 
 /* ReduceScatterV: rank q's block of sendBuf is sendCounts[q] elements at sendDispls[q] (uint64 arrays of rankSize
  * entries); rank r receives the reduce of every rank's block r, sendCounts[r] elements (recvCount must hold them).
- * Replaces /root/reference/include/hccl.h:87-89 (reduce_scatter_v_op.cc:24-83). */
+ * Replaces /root/reference/include/hccl.h:87-89 (reduce_scatter_v_op.cc:24-83).
+ * Per-rank contract: the argument checks are local and run before any collective work, like the reference's. One
+ * addition has no reference counterpart: sendCounts[rank] > recvCount returns HCCL_E_PARA on that rank alone (the
+ * reference would overrun recvBuf). Its peers are not told: they wait in the collective until HCCL_EXEC_TIMEOUT
+ * fails their communicators (HCCL_E_TIMEOUT, then HCCL_E_SUSPENDING), so every rank must pass consistent counts. */
 extern HcclResult HcclReduceScatterV(void* sendBuf, const void* sendCounts, const void* sendDispls, void* recvBuf,
                                      uint64_t recvCount, HcclDataType dataType, HcclReduceOp op, HcclComm comm,
                                      aclrtStream stream);
