@@ -155,6 +155,22 @@ bool Aligned16(const void* p, const void* q)
     return ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(q)) & 15u) == 0;
 }
 
+// Block shares and cache policy of the copy and fold loops (r03 A/B, tools/ipc_variant_ab.py): HCCL_AMD_IPC_TILE_KIB
+// (0 = one contiguous window per block) and HCCL_AMD_IPC_NT (1 = non-temporal loads and stores). Read per call, and
+// equal on every rank (block b pairs with block b of each peer over the same coordinates).
+uint64_t IpcTileBytes()
+{
+    const char* e = std::getenv("HCCL_AMD_IPC_TILE_KIB");
+    if (e == nullptr || *e == '\0') return 0;
+    return std::strtoull(e, nullptr, 10) << 10;
+}
+
+bool IpcNonTemporal()
+{
+    const char* e = std::getenv("HCCL_AMD_IPC_NT");
+    return e != nullptr && std::strcmp(e, "1") == 0;
+}
+
 }  // namespace
 
 // Wall-time bound of one barrier wait, in 100 MHz s_memrealtime ticks. The IPC kernel is the reference's AIV engine,
@@ -592,6 +608,8 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
         const uint64_t widest = g.balanced ? g.group * g.chunkLen + std::min<uint64_t>(g.group, g.rem) : g.chunkLen;
         g.piece = std::max<uint64_t>(V, std::min(slotCap, (widest + V - 1) / V * V));
         g.blockElems = ((g.piece + s.blocks - 1) / s.blocks + V - 1) / V * V;
+        g.tileElems = IpcTileBytes() / es / V * V;  // 0: contiguous windows
+        g.nt = IpcNonTemporal() ? 1u : 0u;
         g.rounds = static_cast<uint32_t>((widest + g.piece - 1) / g.piece);
         g.epochSpan = (single ? 1 : 2) * g.rounds;
     };

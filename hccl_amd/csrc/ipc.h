@@ -107,6 +107,9 @@ struct IpcArgs {
     bool balanced;
     uint64_t piece;
     uint64_t blockElems;
+    uint64_t tileElems;  // 0: block b's share of a piece is one window of blockElems; else tiles of tileElems at
+                         // b, b + B, b + 2B, ... (B = blocks): the same piece coordinates in every round either way
+    uint32_t nt;         // non-temporal loads and stores in the copy and fold loops
     uint32_t rounds;
     uint32_t epochSpan;  // barriers per block in this launch: the device epoch counter advances by this much
     uint64_t outStride;  // kIpcAllGather: elements between consecutive ranks' blocks of the output (sendCount)

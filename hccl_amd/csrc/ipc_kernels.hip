@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <type_traits>
 
 #include "internal.h"
 #include "ipc.h"
@@ -191,10 +192,37 @@ __device__ __forceinline__ Range BlockWindow(const IpcArgs& a, uint64_t len)
     return {lo, min(len, lo + a.blockElems)};
 }
 
+// The block's share of piece coordinates [0, len): f(range) for one window of blockElems (tileElems == 0), or for
+// each tile of tileElems at b, b + B, b + 2B, ... (B = blocks of the launch). Both depend on the block and the piece
+// only, so block b touches the same coordinates in every round, which its per-block barrier relies on.
+template <class F>
+__device__ __forceinline__ void ForBlockShare(const IpcArgs& a, uint64_t len, F&& f)
+{
+    if (a.tileElems == 0) {
+        f(BlockWindow(a, len));
+        return;
+    }
+    const uint64_t step = uint64_t(gridDim.x) * a.tileElems;
+    for (uint64_t lo = uint64_t(blockIdx.x) * a.tileElems; lo < len; lo += step) f(Range{lo, min(len, lo + a.tileElems)});
+}
+
+template <int NT>
+__device__ __forceinline__ void CopyVecs(u32x4* d, const u32x4* s, uint64_t& v, uint64_t vhi)
+{
+    for (; v + (kIpcU - 1) * kIpcBlock < vhi; v += kIpcU * kIpcBlock) {
+        u32x4 x[kIpcU];
+#pragma unroll
+        for (int u = 0; u < kIpcU; ++u) x[u] = ld<NT>(s + v + u * kIpcBlock);
+#pragma unroll
+        for (int u = 0; u < kIpcU; ++u) st<NT>(d + v + u * kIpcBlock, x[u]);
+    }
+    for (; v < vhi; v += kIpcBlock) st<NT>(d + v, ld<NT>(s + v));
+}
+
 // dst[e] = src[e] for e in r. vec = both pointers are 16-B aligned; otherwise every element goes through the scalar
-// loop.
+// loop. nt: non-temporal loads and stores (IpcArgs::nt).
 template <typename S>
-__device__ __forceinline__ void CopyRange(S* dst, const S* src, Range r, bool vec)
+__device__ __forceinline__ void CopyRange(S* dst, const S* src, Range r, bool vec, bool nt)
 {
     constexpr uint64_t V = 16 / sizeof(S);
     // r.lo is vector aligned unless the window is empty at the end of a piece (lo = hi = len); r.hi may be anything
@@ -202,14 +230,11 @@ __device__ __forceinline__ void CopyRange(S* dst, const S* src, Range r, bool ve
     const u32x4* s = reinterpret_cast<const u32x4*>(src);
     u32x4* d = reinterpret_cast<u32x4*>(dst);
     uint64_t v = vlo + threadIdx.x;
-    for (; v + (kIpcU - 1) * kIpcBlock < vhi; v += kIpcU * kIpcBlock) {
-        u32x4 x[kIpcU];
-#pragma unroll
-        for (int u = 0; u < kIpcU; ++u) x[u] = s[v + u * kIpcBlock];
-#pragma unroll
-        for (int u = 0; u < kIpcU; ++u) d[v + u * kIpcBlock] = x[u];
+    if (nt) {
+        CopyVecs<3>(d, s, v, vhi);
+    } else {
+        CopyVecs<0>(d, s, v, vhi);
     }
-    for (; v < vhi; v += kIpcBlock) d[v] = s[v];
     for (uint64_t e = max(vhi * V, r.lo) + threadIdx.x; e < r.hi; e += kIpcBlock) dst[e] = src[e];
 }
 
@@ -375,21 +400,29 @@ __device__ __forceinline__ void FoldSeg(const IpcArgs& a, uint32_t me, uint32_t 
     }
     scalar(r.lo, vb * V);
     uint64_t v = vb + threadIdx.x;
-    for (; v + (kIpcU - 1) * kIpcBlock < ve; v += kIpcU * kIpcBlock) {
-        u32x4 acc[kIpcU];
+    auto body = [&](auto ntTag) {
+        constexpr int NT = decltype(ntTag)::value;
+        for (; v + (kIpcU - 1) * kIpcBlock < ve; v += kIpcU * kIpcBlock) {
+            u32x4 acc[kIpcU];
 #pragma unroll
-        for (int u = 0; u < kIpcU; ++u) acc[u] = reinterpret_cast<const u32x4*>(src(0))[v + u * kIpcBlock];
-        for (uint32_t i = 1; i < n; ++i) {
-            u32x4 x[kIpcU];
+            for (int u = 0; u < kIpcU; ++u) acc[u] = ld<NT>(reinterpret_cast<const u32x4*>(src(0)) + v + u * kIpcBlock);
+            for (uint32_t i = 1; i < n; ++i) {
+                u32x4 x[kIpcU];
 #pragma unroll
-            for (int u = 0; u < kIpcU; ++u) x[u] = reinterpret_cast<const u32x4*>(src(i))[v + u * kIpcBlock];
+                for (int u = 0; u < kIpcU; ++u) x[u] = ld<NT>(reinterpret_cast<const u32x4*>(src(i)) + v + u * kIpcBlock);
 #pragma unroll
-            for (int u = 0; u < kIpcU; ++u) acc[u] = combine<E, OP>(x[u], acc[u]);
+                for (int u = 0; u < kIpcU; ++u) acc[u] = combine<E, OP>(x[u], acc[u]);
+            }
+            for (uint32_t d = 0; d < ndst; ++d) {
+#pragma unroll
+                for (int u = 0; u < kIpcU; ++u) st<NT>(reinterpret_cast<u32x4*>(dsts(d)) + v + u * kIpcBlock, acc[u]);
+            }
         }
-        for (uint32_t d = 0; d < ndst; ++d) {
-#pragma unroll
-            for (int u = 0; u < kIpcU; ++u) reinterpret_cast<u32x4*>(dsts(d))[v + u * kIpcBlock] = acc[u];
-        }
+    };
+    if (a.nt != 0) {
+        body(std::integral_constant<int, 3>{});
+    } else {
+        body(std::integral_constant<int, 0>{});
     }
     for (; v < ve; v += kIpcBlock) {
         u32x4 acc = reinterpret_cast<const u32x4*>(src(0))[v];
@@ -501,24 +534,27 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
         for (uint32_t i = 0; i + 1 < n; ++i) {
             const uint32_t c = (me + 1 + (i + blockIdx.x) % (n - 1)) % n;
             if (kind == kIpcReduceOneShot && c != a.root) continue;
-            const Range r = BlockWindow(a, PieceLen(a, c, kP));
             S* slot = reinterpret_cast<S*>(slotArea(c, epoch + 1)) + uint64_t(me) * a.piece;
-            CopyRange<S>(slot, in + ChunkStart(a, c) + kP, r, ChunkVec<S>(a, c));
+            ForBlockShare(a, PieceLen(a, c, kP), [&](Range r) {
+                CopyRange<S>(slot, in + ChunkStart(a, c) + kP, r, ChunkVec<S>(a, c), a.nt != 0);
+            });
         }
         if (!Barrier(a, fl, ++epoch, waitMax)) break;
         if (kind == kIpcAllGather) {
             // phase 1 of an AllGather: rank q's piece, from my slot q (mine from my input), to output block q
-            const Range r = BlockWindow(a, PieceLen(a, me, kP));
             const S* slots = reinterpret_cast<const S*>(slotArea(me, epoch));
             constexpr uint64_t V = 16 / sizeof(S);
-            for (uint32_t q = 0; q < n; ++q) {
-                const S* src = q == me ? in + kP : slots + uint64_t(q) * a.piece;
-                S* dst = out + uint64_t(q) * a.outStride + kP;
-                if (src != dst) CopyRange<S>(dst, src, r, a.aligned && (uint64_t(q) * a.outStride) % V == 0);
-            }
+            ForBlockShare(a, PieceLen(a, me, kP), [&](Range r) {
+                for (uint32_t q = 0; q < n; ++q) {
+                    const S* src = q == me ? in + kP : slots + uint64_t(q) * a.piece;
+                    S* dst = out + uint64_t(q) * a.outStride + kP;
+                    if (src != dst) {
+                        CopyRange<S>(dst, src, r, a.aligned && (uint64_t(q) * a.outStride) % V == 0, a.nt != 0);
+                    }
+                }
+            });
         } else if (!(kind == kIpcReduceOneShot && me != a.root)) {
             // phase 1: fold my chunk's piece over the slots (my own operand straight from my input)
-            const Range r = BlockWindow(a, PieceLen(a, me, kP));
             const S* own = in + ChunkStart(a, me) + kP;
             const S* slots = reinterpret_cast<const S*>(slotArea(me, epoch));
             // destination 0: my output (or, for a non-root two-shot Reduce rank, the root's result area); the
@@ -533,7 +569,10 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
                 const uint32_t p = d - 1 < me ? d - 1 : d;
                 return static_cast<S*>(a.stgRes[p]) + uint64_t(me) * a.piece;
             };
-            FoldRange<E, OP, kRhd>(a, me, kP, own, slots, dst, kind == kIpcAllReduce ? n : 1u, r, ChunkVec<S>(a, me));
+            ForBlockShare(a, PieceLen(a, me, kP), [&](Range r) {
+                FoldRange<E, OP, kRhd>(a, me, kP, own, slots, dst, kind == kIpcAllReduce ? n : 1u, r,
+                                       ChunkVec<S>(a, me));
+            });
         }
         if (!single && !Barrier(a, fl, ++epoch, waitMax)) break;
         // phase 2: the other chunks' results from my own result area (two-shot AllReduce: every rank; two-shot
@@ -541,9 +580,11 @@ __global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
         if (!oneShot && (kind == kIpcAllReduce || (reduceKind && me == a.root))) {
             for (uint32_t c = 0; c < n; ++c) {
                 if (c == me) continue;
-                const Range r = BlockWindow(a, PieceLen(a, c, kP));
-                CopyRange<S>(out + ChunkStart(a, c) + kP,
-                             static_cast<const S*>(a.stgRes[me]) + uint64_t(c) * a.piece, r, ChunkVec<S>(a, c));
+                ForBlockShare(a, PieceLen(a, c, kP), [&](Range r) {
+                    CopyRange<S>(out + ChunkStart(a, c) + kP,
+                                 static_cast<const S*>(a.stgRes[me]) + uint64_t(c) * a.piece, r, ChunkVec<S>(a, c),
+                                 a.nt != 0);
+                });
             }
         }
     }

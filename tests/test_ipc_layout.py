@@ -51,6 +51,15 @@ def geometry(kind, n, count, es, group=1, vblocks=None):
     return chunks, piece, block, rounds
 
 
+def shares(plen, b, block, tile, blocks=BLOCKS):
+    """ipc_kernels.hip ForBlockShare: block b's ranges of piece coordinates [0, plen) -- one window of `block`
+    elements (tile == 0, BlockWindow), or tiles of `tile` elements at b, b + B, ... (B = blocks)."""
+    if tile == 0:
+        lo = min(plen, b * block)
+        return [(lo, min(plen, lo + block))]
+    return [(lo, min(plen, lo + tile)) for lo in range(b * tile, plen, blocks * tile)]
+
+
 def piece_len(chunks, c, kp, piece):
     cl = chunks[c][1]
     return 0 if kp >= cl else min(piece, cl - kp)
@@ -96,7 +105,7 @@ def fold_segments(kind, n, es, chunk_len, kp, lo, hi, o6):
     return out
 
 
-def check_general(kind, n, count, es, vec, root=0, o6=False, vblocks=None):
+def check_general(kind, n, count, es, vec, root=0, o6=False, vblocks=None, tile=0):
     """The generalised kernel: one-shot kinds push the whole piece (Reduce: to the root only) and fold it without a
     phase 2; O6 folds a window per sub-slice with scalar head and tail around the vector body."""
     v = 16 // es
@@ -113,25 +122,24 @@ def check_general(kind, n, count, es, vec, root=0, o6=False, vblocks=None):
                 for c in range(n):
                     start, cl = chunks[c]
                     plen = 0 if kp >= cl else min(piece, cl - kp)
-                    lo = min(plen, b * block)
-                    hi = min(plen, lo + block)
                     cvec = vec and start % v == 0
-                    if c != me and not (kind == RED1 and c != root):
-                        for a0, a1 in touched(lo, hi, v, cvec):
-                            if a1 > a0:
-                                assert me * piece + a1 <= n * piece
-                                pushed[c][start + kp + a0:start + kp + a1] += 1
-                    if c == me and not (kind == RED1 and me != root):
-                        for s0, s1 in fold_segments(kind, n, es, cl, kp, lo, hi, o6):
-                            for a0, a1 in fold_touched(s0, s1, v, cvec):
-                                if a1 <= a0:
-                                    continue
-                                assert lo <= a0 and a1 <= hi
-                                for q in range(n):
-                                    assert q * piece + a1 <= n * piece
-                                g0, g1 = start + kp + a0, start + kp + a1
-                                assert 0 <= g0 and g1 <= total
-                                cover1[g0:g1] += 1
+                    for lo, hi in shares(plen, b, block, tile):
+                        if c != me and not (kind == RED1 and c != root):
+                            for a0, a1 in touched(lo, hi, v, cvec):
+                                if a1 > a0:
+                                    assert me * piece + a1 <= n * piece
+                                    pushed[c][start + kp + a0:start + kp + a1] += 1
+                        if c == me and not (kind == RED1 and me != root):
+                            for s0, s1 in fold_segments(kind, n, es, cl, kp, lo, hi, o6):
+                                for a0, a1 in fold_touched(s0, s1, v, cvec):
+                                    if a1 <= a0:
+                                        continue
+                                    assert lo <= a0 and a1 <= hi
+                                    for q in range(n):
+                                        assert q * piece + a1 <= n * piece
+                                    g0, g1 = start + kp + a0, start + kp + a1
+                                    assert 0 <= g0 and g1 <= total
+                                    cover1[g0:g1] += 1
         for c in range(n):
             start, cl = chunks[c]
             seg = slice(start, start + cl)
@@ -217,7 +225,7 @@ def test_ipc_allgather_multi_round():
     check_allgather(n, count, 4, vec=True, blocks=default_blocks(n * count * 4))
 
 
-def check(kind, n, count, es, vec, root=0, group=1):
+def check(kind, n, count, es, vec, root=0, group=1, tile=0):
     v = 16 // es
     chunks, piece, block, rounds = geometry(kind, n, count, es, group)
     two_shot = kind in (AR, ARBAL)
@@ -233,10 +241,10 @@ def check(kind, n, count, es, vec, root=0, group=1):
                     start = chunks[c][0]
                     cvec = vec and start % v == 0  # ChunkVec: element-wise unless the chunk start is aligned
                     plen = piece_len(chunks, c, kp, piece)
-                    lo = min(plen, b * block)
-                    hi = min(plen, lo + block)
-                    assert b * block <= lo or lo == hi          # block b's fixed window, whatever the round
-                    for a0, a1 in touched(lo, hi, v, cvec):
+                    for lo, hi, a0, a1 in ((lo, hi, a0, a1) for lo, hi in shares(plen, b, block, tile)
+                                           for a0, a1 in touched(lo, hi, v, cvec)):
+                        # block b's fixed coordinates, whatever the round
+                        assert (b * block <= lo or lo == hi) if tile == 0 else (lo // tile) % BLOCKS == b
                         if a1 <= a0:
                             continue
                         assert lo <= a0 and a1 <= hi
@@ -328,3 +336,24 @@ def test_ipc_reduce_scatter_v_in_bounds_and_exact_cover(layout, n, es):
         blocks = [(sum(counts[:q]), counts[q]) for q in range(n)]
     check_general(RSV, n, 0, es, vec=True, vblocks=blocks)
     check_general(RSV, n, 0, es, vec=False, vblocks=blocks)
+
+
+@pytest.mark.parametrize("tile_vecs", [1, 64, 4096])
+@pytest.mark.parametrize("es", [1, 2, 4, 8])
+@pytest.mark.parametrize("count", [5, 4099, 300007])
+def test_ipc_tiled_block_shares_in_bounds_and_exact_cover(tile_vecs, es, count):
+    """HCCL_AMD_IPC_TILE_KIB: block b's share is the tiles b, b + B, ... of the piece instead of one window; every kind
+    stays in bounds, covers each element once per phase, and block b keeps the same coordinates in every round."""
+    tile = tile_vecs * (16 // es)
+    for kind, n in ((AR, 2), (AR, 8), (RS, 3), (RED, 4)):
+        check(kind, n, count, es, vec=True, root=n - 1, tile=tile)
+    check(ARBAL, 4, count, es, vec=True, group=8, tile=tile)
+    for kind in (AR1, RED1):
+        check_general(kind, 3, count, es, vec=True, root=2, tile=tile)
+    check_general(ARMC, 4, count, es, vec=True, o6=True, tile=tile)
+    check_general(RS, 8, count, es, vec=False, o6=True, tile=tile)
+
+
+def test_ipc_tiled_multi_round():
+    n, count = 2, (36 << 20) + 11  # fp32: 3 rounds of 16 Mi elements
+    check(AR, n, count, 4, vec=True, root=1, tile=4096)

@@ -14,6 +14,7 @@
 #   span_pmc       the same over a self-loop MeshChunk program (RCCL copies + folds)
 #   bench          bench.py default line
 #   profile        tools/profile_round.sh: rocprofv3 trace + FETCH/WRITE of the N=1 bench line, per-kernel summaries
+#   ipc_ab         one-sided kernel: block shares (contiguous / tiles) x cache policy A/B, loopback world
 #   harness        bench.py's N > 1 code path with two ranks sharing the GPU (IPC-only; a crash check, not a result)
 #   counters       the TCC counters this rocprofv3 offers
 set -o pipefail
@@ -125,6 +126,11 @@ step_profile() {
 
 step_harness() {
   run harness_n2 420 bash tools/gpu_harness_n2.sh
+}
+
+step_ipc_ab() {
+  run ipc_ab 400 python3 -u tools/ipc_variant_ab.py
+  grep '^{' "$OUT/ipc_ab.log" > "$OUT/ipc_variant_ab.jsonl" || true
 }
 
 step_counters() {

@@ -1,0 +1,85 @@
+"""A/B of the one-sided kernel's block shares and cache policy (r03): HCCL_AMD_IPC_TILE_KIB (0 = one contiguous
+window per block; else interleaved tiles) x HCCL_AMD_IPC_NT (non-temporal loads and stores), on a loopback world
+(every rank's blocks in one launch on one GPU; each rank driven from its own host thread), two-shot AllReduce fp32
+SUM. Variants are interleaved over rounds; per variant the median per-call time (HIP events on rank 0's stream, the
+world's launch stream) and its algorithmic rate (n x 2(3n-2)/n x bytes per rank per launch). Every variant's output
+is compared bit for bit with the first variant's.
+  python tools/ipc_variant_ab.py > gpurun_out/ipc_variant_ab.jsonl
+"""
+import json
+import os
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import hccl_amd as H  # noqa: E402
+
+VARIANTS = [(0, 0), (0, 1), (16, 0), (16, 1), (64, 1), (256, 1)]
+ROUNDS = int(os.environ.get("AB_ROUNDS", "5"))
+CALLS = int(os.environ.get("AB_CALLS", "4"))
+
+
+def run(n, mib, algo=H.Algo.IPC_TWOSHOT):
+    dev = torch.device("cuda", 0)
+    comms = H.loopback_world(n)
+    for c in comms:
+        c.set_algo(algo)
+    count = (mib << 20) // 4
+    g = torch.Generator(device=dev).manual_seed(11 + n)
+    xs = [torch.rand(count, device=dev, generator=g) for _ in range(n)]
+    ys = [torch.empty_like(x) for x in xs]
+    streams = [torch.cuda.Stream() for _ in range(n)]
+    pool = ThreadPoolExecutor(n)
+
+    def call():
+        list(pool.map(lambda r: comms[r].all_reduce(xs[r], ys[r], H.HcclReduceOp.SUM, streams[r]), range(n)))
+
+    times = {v: [] for v in VARIANTS}
+    ok = {v: True for v in VARIANTS}
+    ref = None
+    for rnd in range(ROUNDS):
+        order = VARIANTS[rnd % len(VARIANTS):] + VARIANTS[:rnd % len(VARIANTS)]
+        for v in order:
+            os.environ["HCCL_AMD_IPC_TILE_KIB"] = str(v[0])
+            os.environ["HCCL_AMD_IPC_NT"] = str(v[1])
+            call()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(streams[0])
+            for _ in range(CALLS):
+                call()
+            e1.record(streams[0])
+            torch.cuda.synchronize()
+            times[v].append(e0.elapsed_time(e1) * 1e3 / CALLS)
+            if ref is None:
+                ref = [y.clone() for y in ys]
+            else:
+                ok[v] = ok[v] and all(bool(torch.equal(a, b)) for a, b in zip(ys, ref))
+    status = comms[0].ipc_status() & 1
+    pool.shutdown()
+    for c in comms:
+        c.destroy()
+    alg = n * 2 * (3 * n - 2) * count * 4 // n
+    for v in VARIANTS:
+        med = float(np.median(times[v]))
+        print(json.dumps({"ranks": n, "mib_per_rank": mib, "algo": algo.name, "tile_kib": v[0], "nt": v[1],
+                          "median_us": round(med, 1), "min_us": round(min(times[v]), 1),
+                          "max_us": round(max(times[v]), 1), "TBps": round(alg / med / 1e6, 3),
+                          "frac": round(alg / med / 1e6 / 8.0, 4), "same_bits": ok[v],
+                          "barrier_timeouts": status}), flush=True)
+
+
+def main():
+    torch.cuda.set_device(0)
+    os.environ.setdefault("HCCL_AMD_IPC_TIMEOUT_MS", "20000")
+    for n, mib in ((2, 512), (4, 256), (8, 128)):
+        run(n, mib)
+
+
+if __name__ == "__main__":
+    main()
