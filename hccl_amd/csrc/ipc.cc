@@ -44,9 +44,10 @@ HcclResult IpcSetup(Comm& c)
     if (s.unavailable) return HCCL_E_NOT_SUPPORT;
     const uint32_t n = c.nRanks, me = c.rank;
     s.blocks = kIpcBlocks;
-    s.stgInBytes = kIpcStagingBytes;
-    s.stgResBytes = kIpcStagingBytes;  // results of a whole round, in round coordinates
-    s.stgAltBytes = kIpcStagingBytes;  // slots of the single-barrier kinds, two areas used alternately
+    const uint64_t area = IpcStagingBytes();
+    s.stgInBytes = area;
+    s.stgResBytes = area;  // results of a whole round, in round coordinates
+    s.stgAltBytes = area;  // slots of the single-barrier kinds, two areas used alternately
     const size_t flagBytes = size_t(kIpcMaxBlocks) * kIpcMaxRanks * sizeof(uint32_t);
     // The fresh uncached pages may carry lines of a freed cached buffer in some XCD's L2: scrub the L2s before the
     // flags are zeroed (ScrubL2), so that no stale line is ever read or written back over them.
@@ -168,7 +169,7 @@ uint64_t IpcTileBytes()
 bool IpcNonTemporal()
 {
     const char* e = std::getenv("HCCL_AMD_IPC_NT");
-    return e != nullptr && std::strcmp(e, "1") == 0;
+    return e == nullptr || std::strcmp(e, "0") != 0;  // default on: 2-3 % at n = 2, 4, 8 (profiles/r03_ipc_variant_ab.jsonl)
 }
 
 }  // namespace
@@ -244,7 +245,17 @@ uint32_t DefaultIpcBlocks(uint64_t bytes)
     if (bytes <= (2ull << 20)) return 32;
     if (bytes <= (32ull << 20)) return 64;
     if (bytes <= (64ull << 20)) return 128;
-    return kIpcMaxBlocks;
+    return 256;
+}
+
+uint64_t IpcStagingBytes()
+{
+    const char* e = std::getenv("HCCL_AMD_IPC_STAGING_MIB");
+    if (e != nullptr && *e != '\0') {
+        const unsigned long long v = std::strtoull(e, nullptr, 10);
+        if (v >= 16 && v <= 2048) return static_cast<uint64_t>(v) << 20;
+    }
+    return kIpcStagingBytes;
 }
 
 // ------------------------------------------------------------------------------------------------ plans
@@ -494,7 +505,7 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
         for (uint32_t q = 0; q < c.nRanks; ++q) callBytes += vCounts[q] * es;
     }
     s.blocks = c.ipcBlocks != 0 ? c.ipcBlocks : DefaultIpcBlocks(callBytes);
-    if (c.transport->SharedDevice()) s.blocks = std::min(s.blocks, kIpcBlocks);
+    if (c.transport->SharedDevice() && c.ipcBlocks == 0) s.blocks = std::min(s.blocks, kIpcBlocks);
     // Co-residency: every block waits at barriers for its peers' blocks, so all blocks on this device must be resident
     // at once (a loopback world puts every rank's blocks on it; in rank mode, the ranks whose processes share this
     // device, counted at set-up by PCI bus id). The count depends only on the kernel, the device and the placement,

@@ -164,12 +164,13 @@ struct IpcState {
 };
 
 constexpr uint32_t kIpcBlocks = 128;     // workgroups per rank and launch in a loopback world (cap)
-constexpr uint32_t kIpcMaxBlocks = 256;  // flags are sized for this many (HcclAmdCommSetIpcBlocks)
+constexpr uint32_t kIpcMaxBlocks = 512;  // flags are sized for this many (HcclAmdCommSetIpcBlocks)
 uint32_t DefaultIpcBlocks(uint64_t bytes);  // workgroups per launch when the communicator sets none (ipc.cc)
 constexpr size_t kIpcStatusBytes = 32;  // status words (IpcArgs::status)
 constexpr int kIpcEpochWord = 4;
 constexpr int kIpcDoneWord = 5;
-constexpr uint64_t kIpcStagingBytes = 128ull << 20;  // slot area per rank; the result area is as large, and so is
-                                                     // each alternate slot area
+constexpr uint64_t kIpcStagingBytes = 128ull << 20;  // slot area per rank (default); the result area is as large,
+                                                     // and so is each alternate slot area
+uint64_t IpcStagingBytes();  // HCCL_AMD_IPC_STAGING_MIB (16 .. 2048) or kIpcStagingBytes; equal on every rank
 
 }  // namespace hccl_amd

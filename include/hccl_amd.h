@@ -194,9 +194,10 @@ extern HcclResult HcclAmdCommInitLoopback(uint32_t nRanks, HcclComm* comms);
 /* Force the schedule family for subsequent collectives on comm (HCCL_AMD_ALGO_AUTO restores the selector). */
 extern HcclResult HcclAmdCommSetAlgo(HcclComm comm, int32_t algo);
 
-/* Workgroups per launch of the one-sided IPC kernel (1..256; 0 restores the default, which grows with the call's
+/* Workgroups per launch of the one-sided IPC kernel (1..512; 0 restores the default, which grows with the call's
  * bytes from 16 to 256). Must be equal on every rank of the communicator (block b synchronises with block b of each
- * peer). A loopback world uses at most 128 per rank. */
+ * peer). A loopback world uses at most 128 per rank unless set here. Either way the launch is capped at the blocks
+ * the device holds at once, divided by the ranks that share it. */
 extern HcclResult HcclAmdCommSetIpcBlocks(HcclComm comm, uint32_t blocks);
 
 /* Pipelining granule (bytes per piece) for subsequent collectives on comm; 0 restores the default. */

@@ -20,6 +20,8 @@ import torch  # noqa: E402
 import hccl_amd as H  # noqa: E402
 
 VARIANTS = [(0, 0), (0, 1), (16, 0), (16, 1), (64, 1), (256, 1)]
+# second sweep: (staging area MiB, workgroups per rank) with nt loads/stores, contiguous windows
+SHAPES = [(128, 128), (128, 256), (512, 128), (512, 256), (512, 512)]
 ROUNDS = int(os.environ.get("AB_ROUNDS", "5"))
 CALLS = int(os.environ.get("AB_CALLS", "4"))
 
@@ -74,11 +76,77 @@ def run(n, mib, algo=H.Algo.IPC_TWOSHOT):
                           "barrier_timeouts": status}), flush=True)
 
 
+def run_shapes(n, mib, algo=H.Algo.IPC_TWOSHOT):
+    """Staging size (rounds per launch) x workgroups per rank: a fresh world per shape (staging is set up per
+    communicator), shapes interleaved over rounds."""
+    dev = torch.device("cuda", 0)
+    count = (mib << 20) // 4
+    g = torch.Generator(device=dev).manual_seed(21 + n)
+    xs = [torch.rand(count, device=dev, generator=g) for _ in range(n)]
+    ys = [torch.empty_like(x) for x in xs]
+    streams = [torch.cuda.Stream() for _ in range(n)]
+    pool = ThreadPoolExecutor(n)
+    os.environ["HCCL_AMD_IPC_TILE_KIB"] = "0"
+    os.environ["HCCL_AMD_IPC_NT"] = "1"
+    worlds = {}
+    for stg, blocks in SHAPES:
+        os.environ["HCCL_AMD_IPC_STAGING_MIB"] = str(stg)
+        comms = H.loopback_world(n)
+        for c in comms:
+            c.set_algo(algo)
+            c.set_ipc_blocks(blocks)
+        list(pool.map(lambda r: comms[r].all_reduce(xs[r], ys[r], H.HcclReduceOp.SUM, streams[r]), range(n)))
+        torch.cuda.synchronize()  # the set-up (staging of this size) happens on the first call
+        worlds[(stg, blocks)] = comms
+    os.environ.pop("HCCL_AMD_IPC_STAGING_MIB")
+    times = {k: [] for k in SHAPES}
+    ok = {k: True for k in SHAPES}
+    ref = None
+    for rnd in range(ROUNDS):
+        order = SHAPES[rnd % len(SHAPES):] + SHAPES[:rnd % len(SHAPES)]
+        for k in order:
+            comms = worlds[k]
+
+            def call():
+                list(pool.map(lambda r: comms[r].all_reduce(xs[r], ys[r], H.HcclReduceOp.SUM, streams[r]), range(n)))
+
+            call()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(streams[0])
+            for _ in range(CALLS):
+                call()
+            e1.record(streams[0])
+            torch.cuda.synchronize()
+            times[k].append(e0.elapsed_time(e1) * 1e3 / CALLS)
+            if ref is None:
+                ref = [y.clone() for y in ys]
+            else:
+                ok[k] = ok[k] and all(bool(torch.equal(a, b)) for a, b in zip(ys, ref))
+    pool.shutdown()
+    alg = n * 2 * (3 * n - 2) * count * 4 // n
+    for k in SHAPES:
+        comms = worlds[k]
+        status = comms[0].ipc_status() & 1
+        for c in comms:
+            c.destroy()
+        med = float(np.median(times[k]))
+        print(json.dumps({"ranks": n, "mib_per_rank": mib, "algo": algo.name, "staging_mib": k[0],
+                          "blocks_per_rank": k[1], "nt": 1, "median_us": round(med, 1),
+                          "min_us": round(min(times[k]), 1), "max_us": round(max(times[k]), 1),
+                          "TBps": round(alg / med / 1e6, 3), "frac": round(alg / med / 1e6 / 8.0, 4),
+                          "same_bits": ok[k], "barrier_timeouts": status}), flush=True)
+
+
 def main():
     torch.cuda.set_device(0)
     os.environ.setdefault("HCCL_AMD_IPC_TIMEOUT_MS", "20000")
-    for n, mib in ((2, 512), (4, 256), (8, 128)):
-        run(n, mib)
+    if os.environ.get("AB_SWEEP", "shapes") == "policy":
+        for n, mib in ((2, 512), (4, 256), (8, 128)):
+            run(n, mib)
+    else:
+        for n, mib in ((2, 512), (4, 256)):
+            run_shapes(n, mib)
 
 
 if __name__ == "__main__":
