@@ -768,6 +768,24 @@ def bench_c3_algos(comm, send, recv, world) -> dict:
                 row["barrier_timeouts"] = st & 1
                 row["longest_wait_polls_log2"] = (st >> 8) & 0xFF
             out[name] = row
+        # the headline's schedule with every call eager (no executor graph: HCCL_AMD_GRAPH_CACHE=0, read per call),
+        # beside the default, which replays one captured graph per repeated call
+        comm.set_algo(H.Algo.RING)
+        comm.set_ipc_blocks(0)
+        saved = os.environ.get("HCCL_AMD_GRAPH_CACHE")
+        os.environ["HCCL_AMD_GRAPH_CACHE"] = "0"
+        try:
+            t = _timed(lambda: comm.all_reduce(send, recv, H.HcclReduceOp.SUM, s), 3, warmup=1)
+            out["RING_EAGER"] = {"ms": round(t * 1e3, 3),
+                                 "busbw_GBps": round(C3_BYTES / t / 1e9 * 2 * (world - 1) / world, 2),
+                                 "ran": H.Algo(comm.last_algo).name, "graph_cache": 0}
+        except H.HcclError as e:
+            out["RING_EAGER"] = {"error": str(e)}
+        finally:
+            if saved is None:
+                os.environ.pop("HCCL_AMD_GRAPH_CACHE", None)
+            else:
+                os.environ["HCCL_AMD_GRAPH_CACHE"] = saved
     finally:
         comm.set_algo(H.Algo.AUTO)
         comm.set_ipc_blocks(0)

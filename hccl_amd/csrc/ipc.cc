@@ -169,7 +169,7 @@ uint64_t IpcTileBytes()
 bool IpcNonTemporal()
 {
     const char* e = std::getenv("HCCL_AMD_IPC_NT");
-    return e == nullptr || std::strcmp(e, "0") != 0;  // default on: 2-3 % at n = 2, 4, 8 (profiles/r03_ipc_variant_ab.jsonl)
+    return e == nullptr || std::strcmp(e, "0") != 0;  // default on: 2-3 % at n = 2, 4, 8 (profiles/r03_ipc_variant_ab_{policy,shapes}.jsonl)
 }
 
 }  // namespace

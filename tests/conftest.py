@@ -25,6 +25,11 @@ def _ensure_built():
 
 _ensure_built()
 
+# The one-sided kernel's staging areas are 512 MiB per rank by default; the IPC tests' multi-round counts were sized
+# for 128 MiB areas (a chunk wider than one area runs several staging rounds), so the suite keeps that size unless a
+# test sets its own (test_gpu_collectives.py::test_ipc_default_staging covers the default). Child processes inherit it.
+os.environ.setdefault("HCCL_AMD_IPC_STAGING_MIB", "128")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an AMD Instinct MI355X (gfx950)")

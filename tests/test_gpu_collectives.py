@@ -128,6 +128,25 @@ def test_ipc_allreduce_o2_and_status(worlds, n, count):
         assert O.equal_bits(O.FP32, outs[r], want[r]), r
 
 
+@pytest.mark.parametrize("n,count", [(2, (80 << 20) + 3), (4, (40 << 20) + 1), (8, 4099)])
+def test_ipc_default_staging(monkeypatch, n, count):
+    """The default 512 MiB staging areas (r03: one round where 128 MiB areas took several, 5-12 % faster,
+    profiles/r03_ipc_variant_ab_{policy,shapes}.jsonl): two-shot IPC AllReduce bit-exact with order O2, barrier status clean."""
+    monkeypatch.delenv("HCCL_AMD_IPC_STAGING_MIB", raising=False)
+    comms = H.loopback_world(n)
+    try:
+        xs = [O.random_operands(O.FP32, count, seed=900 + r, edge=False) for r in range(n)]
+        used, outs = collective(comms, AR, 7, O.FP32, O.SUM, xs, count)
+        assert used == 7
+        assert ipc_status(comms[0]) & 1 == 0
+        want = R.expected(AR, R.ALGO_TWOSHOT, O.FP32, O.SUM, xs, count)
+        for r in range(n):
+            assert O.equal_bits(O.FP32, outs[r], want[r]), r
+    finally:
+        for c in comms:
+            c.destroy()
+
+
 @pytest.mark.parametrize("op_type,n,count", [(RS, 2, (17 << 20) + 5), (RS, 4, 3), (RED, 4, (36 << 20) + 7),
                                               (RED, 3, 5)])
 def test_ipc_reduce_scatter_and_reduce(worlds, op_type, n, count):
