@@ -1023,3 +1023,39 @@ def test_entry_checks_match_reference(worlds):
     assert L.HcclReduce(p, p, 0, FP32, SUM, 0, None, None) == E.HCCL_SUCCESS
     assert L.HcclReduce(p, p, 16, FP32, SUM, 0, c, None) == E.HCCL_E_PTR
     assert L.HcclReduce(p, p, 16, FP32, SUM, 2, c, s) == E.HCCL_E_PARA                # root out of range
+
+
+@pytest.mark.parametrize("algo", [7, 2])  # IPC_TWOSHOT (one kernel on the caller's stream), MESH_TWOSHOT (executor)
+def test_calls_on_two_streams_are_ordered(worlds, algo):
+    """Two AllReduces of one communicator on two different streams, enqueued back to back with no host wait: they
+    share the communicator's staging, so the second must wait for the first (EntryScope, r03). Both results exact."""
+    n, count = 4, (6 << 20) + 5
+    comms = worlds(n)
+    xa = [O.random_operands(O.FP32, count, seed=1300 + r, edge=False) for r in range(n)]
+    xb = [O.random_operands(O.FP32, count, seed=1400 + r, edge=False) for r in range(n)]
+    da = [to_device(O.FP32, x) for x in xa]
+    db = [to_device(O.FP32, x) for x in xb]
+    oa = [torch.empty_like(d) for d in da]
+    ob = [torch.empty_like(d) for d in db]
+    sa = [torch.cuda.Stream() for _ in range(n)]
+    sb = [torch.cuda.Stream() for _ in range(n)]
+    for c in comms:
+        c.set_algo(algo)
+    torch.cuda.synchronize()
+
+    def body(r):
+        comms[r].all_reduce(da[r], oa[r], O.SUM, sa[r])
+        comms[r].all_reduce(db[r], ob[r], O.SUM, sb[r])
+
+    try:
+        run_ranks(n, body)
+        torch.cuda.synchronize()
+    finally:
+        for c in comms:
+            c.set_algo(0)
+    fam = R.ALGO_TWOSHOT
+    wa = R.expected(AR, fam, O.FP32, O.SUM, xa, count)
+    wb = R.expected(AR, fam, O.FP32, O.SUM, xb, count)
+    for r in range(n):
+        assert O.equal_bits(O.FP32, to_host(O.FP32, oa[r]), wa[r]), r
+        assert O.equal_bits(O.FP32, to_host(O.FP32, ob[r]), wb[r]), r

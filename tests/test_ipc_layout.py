@@ -338,9 +338,8 @@ def test_ipc_reduce_scatter_v_in_bounds_and_exact_cover(layout, n, es):
     check_general(RSV, n, 0, es, vec=False, vblocks=blocks)
 
 
-@pytest.mark.parametrize("tile_vecs", [1, 64, 4096])
+@pytest.mark.parametrize("tile_vecs,count", [(1, 5), (1, 4099), (3, 33333), (64, 4099), (64, 300007), (4096, 300007)])
 @pytest.mark.parametrize("es", [1, 2, 4, 8])
-@pytest.mark.parametrize("count", [5, 4099, 300007])
 def test_ipc_tiled_block_shares_in_bounds_and_exact_cover(tile_vecs, es, count):
     """HCCL_AMD_IPC_TILE_KIB: block b's share is the tiles b, b + B, ... of the piece instead of one window; every kind
     stays in bounds, covers each element once per phase, and block b keeps the same coordinates in every round."""
