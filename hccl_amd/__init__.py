@@ -248,6 +248,17 @@ class Comm:
         check("HcclAmdCommIpcStatus", lib.HcclAmdCommIpcStatus(self.handle, ctypes.byref(v)))
         return v.value
 
+    def ipc_trace(self):
+        """Phase stamps of the last one-sided launch (HCCL_AMD_IPC_TRACE=1 at the first IPC call): a uint64 array
+        [16 ranks][512 blocks][8 slots] of 100 MHz ticks and the workgroups per rank of that launch."""
+        import numpy as np
+
+        n = 16 * 512 * 8
+        buf = (ctypes.c_uint64 * n)()
+        b = ctypes.c_uint32(0)
+        check("HcclAmdCommIpcTrace", lib.HcclAmdCommIpcTrace(self.handle, buf, n, ctypes.byref(b)))
+        return np.frombuffer(buf, dtype=np.uint64).reshape(16, 512, 8).copy(), b.value
+
     def async_error(self) -> int:
         """HcclGetCommAsyncError: HCCL_E_TIMEOUT after an IPC barrier timeout, an RCCL asynchronous error, or 0."""
         v = ctypes.c_int(0)

@@ -194,6 +194,7 @@ SIGNATURES = {
     "HcclAmdCommGraphStats": (_res, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     "HcclAmdCommExecute": (_res, [_vp, ctypes.POINTER(HcclAmdIrOp), _u64, _vp, _vp, _i32, _i32, _i32, _vp]),
     "HcclAmdCommIpcStatus": (_res, [_vp, ctypes.POINTER(_u32)]),
+    "HcclAmdCommIpcTrace": (_res, [_vp, ctypes.POINTER(_u64), _u64, ctypes.POINTER(_u32)]),
     "HcclAmdIpcTimeoutMs": (_u64, []),
     "HcclAmdCommInitHostExchange": (_res, [_u32, _u32, _vp, _vp, ctypes.POINTER(_vp)]),
     "HcclAmdRankTableInfo": (_res, [ctypes.c_char_p, _u32, ctypes.POINTER(_u32), ctypes.POINTER(ctypes.c_int32)]),

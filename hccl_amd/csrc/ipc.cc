@@ -1,4 +1,4 @@
-// ipc.cc — host side of the one-sided collectives (ipc_kernels.hip): peer-mapped staging set-up and launch.
+// ipc.cc — host side of the one-sided collectives (ipc_kernel_body.h): peer-mapped staging set-up and launch.
 //
 // Set-up (collective, on the first IPC call of a communicator): every rank allocates uncached staging and a
 // flag array, exports them with hipIpcGetMemHandle, all-gathers the handles over the communicator (ncclAllGather)
@@ -37,6 +37,14 @@ bool ScrubEnabled()
     return e == nullptr || std::strcmp(e, "0") != 0;
 }
 
+// HCCL_AMD_IPC_TRACE=1 (read at set-up): the kernel stamps its phases per block (IpcTraceSlot), read back with
+// HcclAmdCommIpcTrace. Diagnostics for the phase timeline (tools/ipc_phase_trace.py); off by default.
+bool IpcTraceEnabled()
+{
+    const char* e = std::getenv("HCCL_AMD_IPC_TRACE");
+    return e != nullptr && std::strcmp(e, "1") == 0;
+}
+
 HcclResult IpcSetup(Comm& c)
 {
     IpcState& s = c.ipc;
@@ -51,8 +59,14 @@ HcclResult IpcSetup(Comm& c)
     const size_t flagBytes = size_t(kIpcMaxBlocks) * kIpcMaxRanks * sizeof(uint32_t);
     // The fresh uncached pages may carry lines of a freed cached buffer in some XCD's L2: scrub the L2s before the
     // flags are zeroed (ScrubL2), so that no stale line is ever read or written back over them.
-    bool ok = hipExtMallocWithFlags(&s.stg, s.stgInBytes + s.stgResBytes + 2 * s.stgAltBytes,
-                                    hipDeviceMallocUncached) == hipSuccess &&
+    // HCCL_AMD_IPC_STAGING_CACHED=1 (diagnostics, one device only: the r03 A/B of what uncached staging costs) puts
+    // the slot and result areas in ordinary cached memory; the barriers' system-scope release and acquire then carry
+    // the hand-off through the L2s of that one device.
+    const char* cachedEnv = std::getenv("HCCL_AMD_IPC_STAGING_CACHED");
+    const bool cached = cachedEnv != nullptr && std::strcmp(cachedEnv, "1") == 0;
+    const size_t stgBytes = s.stgInBytes + s.stgResBytes + 2 * s.stgAltBytes;
+    bool ok = (cached ? hipMalloc(&s.stg, stgBytes) : hipExtMallocWithFlags(&s.stg, stgBytes, hipDeviceMallocUncached)) ==
+                  hipSuccess &&
               hipExtMallocWithFlags(reinterpret_cast<void**>(&s.flags), flagBytes, hipDeviceMallocUncached) ==
                   hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&s.status), kIpcStatusBytes) == hipSuccess &&
@@ -62,6 +76,12 @@ HcclResult IpcSetup(Comm& c)
               hipDeviceSynchronize() == hipSuccess && (!ScrubEnabled() || ScrubL2(c.reduceStream) == HCCL_SUCCESS) &&
               hipMemset(s.flags, 0, flagBytes) == hipSuccess && hipMemset(s.status, 0, kIpcStatusBytes) == hipSuccess &&
               hipDeviceSynchronize() == hipSuccess;
+    if (ok && IpcTraceEnabled()) {
+        // phase stamps (diagnostics): every rank's and block's row, so a loopback world's one launch fits too
+        const size_t tb = size_t(kIpcMaxRanks) * kIpcMaxBlocks * kIpcTraceSlots * sizeof(uint64_t);
+        ok = hipMalloc(reinterpret_cast<void**>(&s.trace), tb) == hipSuccess && hipMemset(s.trace, 0, tb) == hipSuccess &&
+             hipDeviceSynchronize() == hipSuccess;
+    }
     if (ok) {
         *s.failHost = 0;
     } else {
@@ -166,6 +186,16 @@ uint64_t IpcTileBytes()
     return std::strtoull(e, nullptr, 10) << 10;
 }
 
+// HCCL_AMD_IPC_COPY_U / HCCL_AMD_IPC_FOLD_U: vectors per lane in flight in the copy and fold loops (2, 4 or 8; r03 A/B,
+// tools/ipc_variant_ab.py). Read per call, equal on every rank.
+uint32_t IpcUnroll(const char* name, uint32_t dflt)
+{
+    const char* e = std::getenv(name);
+    if (e == nullptr || *e == '\0') return dflt;
+    const unsigned long v = std::strtoul(e, nullptr, 10);
+    return (v == 2 || v == 4 || v == 8) ? static_cast<uint32_t>(v) : dflt;
+}
+
 bool IpcNonTemporal()
 {
     const char* e = std::getenv("HCCL_AMD_IPC_NT");
@@ -226,6 +256,7 @@ void IpcRelease(Comm& c)
     if (s.stg != nullptr) (void)hipFree(s.stg);
     if (s.flags != nullptr) (void)hipFree(s.flags);
     if (s.status != nullptr) (void)hipFree(s.status);
+    if (s.trace != nullptr) (void)hipFree(s.trace);
     // the word is no longer watched before it is freed (a failure already seen stays in Comm::failCode)
     c.failWord.store(nullptr, std::memory_order_release);
     if (s.failHost != nullptr) (void)hipHostFree(s.failHost);
@@ -535,6 +566,7 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
     a.outStride = count;
     a.altOff = s.stgInBytes + s.stgResBytes;
     a.altBytes = s.stgAltBytes;
+    a.trace = s.trace;
     if (plan.order == kIpcRhd) {
         // the RHD schedule's parts and relabelling (AllReduceRhd): R instances over Chunk(count, R, j) parts
         const std::vector<std::vector<uint32_t>> table = RhdTable(n);
@@ -621,6 +653,8 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
         g.blockElems = ((g.piece + s.blocks - 1) / s.blocks + V - 1) / V * V;
         g.tileElems = IpcTileBytes() / es / V * V;  // 0: contiguous windows
         g.nt = IpcNonTemporal() ? 1u : 0u;
+        g.copyU = IpcUnroll("HCCL_AMD_IPC_COPY_U", 4);
+        g.foldU = IpcUnroll("HCCL_AMD_IPC_FOLD_U", 4);
         g.rounds = static_cast<uint32_t>((widest + g.piece - 1) / g.piece);
         g.epochSpan = (single ? 1 : 2) * g.rounds;
     };
@@ -702,5 +736,20 @@ extern "C" HcclResult HcclAmdCommIpcStatus(HcclComm comm, uint32_t* status)
     uint32_t lg = 0;
     while (lg < 32 && (uint64_t(1) << lg) <= wait) ++lg;  // bit length of the longest wait
     *status = (w[0] & 0xFFu) | (lg << 8);
+    return HCCL_SUCCESS;
+}
+
+extern "C" HcclResult HcclAmdCommIpcTrace(HcclComm comm, uint64_t* stamps, uint64_t cap, uint32_t* blocks)
+{
+    Comm* c = AsComm(comm);
+    if (c == nullptr || stamps == nullptr || blocks == nullptr) return HCCL_E_PTR;
+    *blocks = 0;
+    if (!c->ipc.ready || c->ipc.trace == nullptr) return HCCL_E_NOT_SUPPORT;
+    const uint64_t want = uint64_t(kIpcMaxRanks) * kIpcMaxBlocks * kIpcTraceSlots;
+    if (cap < want) return HCCL_E_PARA;
+    HIP_CHK(hipSetDevice(c->device));
+    HIP_CHK(hipDeviceSynchronize());
+    HIP_CHK(hipMemcpy(stamps, c->ipc.trace, want * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    *blocks = c->ipc.blocks;
     return HCCL_SUCCESS;
 }

@@ -10,6 +10,7 @@
 namespace hccl_amd {
 
 constexpr int kIpcMaxRanks = 16;
+constexpr int kIpcBlock = 256;  // threads per workgroup of the one-sided kernel
 
 enum IpcKind : uint32_t {
     kIpcAllReduce = 0,         // two-shot: owner c folds chunk c, every rank gets every chunk
@@ -110,6 +111,8 @@ struct IpcArgs {
     uint64_t tileElems;  // 0: block b's share of a piece is one window of blockElems; else tiles of tileElems at
                          // b, b + B, b + 2B, ... (B = blocks): the same piece coordinates in every round either way
     uint32_t nt;         // non-temporal loads and stores in the copy and fold loops
+    uint32_t copyU;      // vectors per lane in flight in the copy loops (2, 4, 8)
+    uint32_t foldU;      // vectors per lane and operand in flight in the fold loop (2, 4, 8)
     uint32_t rounds;
     uint32_t epochSpan;  // barriers per block in this launch: the device epoch counter advances by this much
     uint64_t outStride;  // kIpcAllGather: elements between consecutive ranks' blocks of the output (sendCount)
@@ -130,10 +133,43 @@ struct IpcArgs {
     uint32_t alignElems;     // kIpcRhd: HCCL_MIN_SLICE_ALIGN (128 B) in elements
     uint64_t rhdPartStride;  // kIpcRhd: elements per part (the last part may be shorter)
     uint8_t rhdReal[kIpcMaxRanks - 1][kIpcMaxRanks];  // kIpcRhd: per instance j, virtual rank -> real rank
+    uint64_t* trace;  // HCCL_AMD_IPC_TRACE=1: per rank and block, kIpcTraceSlots s_memrealtime stamps of the phases
+                      // (IpcTraceSlot); nullptr = off
+};
+
+// Phase stamps of one block (HCCL_AMD_IPC_TRACE, HcclAmdCommIpcTrace): 100 MHz s_memrealtime ticks, lane 0 of the
+// block. The round stamps are those of the launch's last round. "issued" = lane 0's wave has issued the phase's last
+// access (a barrier's own drain counts toward the barrier).
+enum IpcTraceSlot : uint32_t {
+    kTrEntry = 0,       // kernel entry (after the failed-communicator check)
+    kTrRound = 1,       // start of the round
+    kTrPhase0 = 2,      // phase 0 issued
+    kTrBarrier1 = 3,    // first barrier passed
+    kTrPhase1 = 4,      // phase 1 issued
+    kTrBarrier2 = 5,    // second barrier passed (two-barrier kinds)
+    kTrPhase2 = 6,      // phase 2 issued
+    kTrExit = 7,        // lane 0's stores drained, before the launch's end count
+    kIpcTraceSlots = 8,
 };
 
 HcclResult LaunchIpcCollective(const IpcArgs& a, uint32_t blocks, uint32_t worldRanks, HcclDataType dt,
                               HcclReduceOp op, hipStream_t stream);
+
+// Per-dtype entry points of the kernels (ipc_k_*.hip, one translation unit per dtype group): the launch by op, and the
+// kernel's address for the occupancy query (rhd: the kIpcRhd instantiation).
+#define HCCL_AMD_IPC_DTYPE_DECL(NAME)                                                          \
+    hipError_t LaunchIpc_##NAME(int op, const IpcArgs& a, dim3 grid, hipStream_t s); \
+    const void* IpcKernel_##NAME(int op, bool rhd);
+HCCL_AMD_IPC_DTYPE_DECL(Int8)
+HCCL_AMD_IPC_DTYPE_DECL(Int16)
+HCCL_AMD_IPC_DTYPE_DECL(Int32)
+HCCL_AMD_IPC_DTYPE_DECL(Int64)
+HCCL_AMD_IPC_DTYPE_DECL(Uint64)
+HCCL_AMD_IPC_DTYPE_DECL(Fp16)
+HCCL_AMD_IPC_DTYPE_DECL(Bf16)
+HCCL_AMD_IPC_DTYPE_DECL(Fp32)
+HCCL_AMD_IPC_DTYPE_DECL(Fp64)
+#undef HCCL_AMD_IPC_DTYPE_DECL
 
 // Workgroups of the IPC kernel for (dt, op) that the device holds at once (occupancy x CUs; 0 if unknown). Every
 // block of a launch waits at barriers for its peers' blocks, so the blocks that share a device must all be resident.
@@ -161,6 +197,7 @@ struct IpcState {
     uint64_t stgAltBytes = 0;      // each of the two alternate slot areas of the single-barrier kinds
     uint32_t blocks = 0;
     uint32_t ranksOnDevice = 1;    // rank mode: the most ranks that share one device (by PCI bus id), same on all ranks
+    uint64_t* trace = nullptr;     // HCCL_AMD_IPC_TRACE=1 at set-up: [kIpcMaxRanks][kIpcMaxBlocks][kIpcTraceSlots]
 };
 
 constexpr uint32_t kIpcBlocks = 128;     // workgroups per rank and launch in a loopback world (cap)

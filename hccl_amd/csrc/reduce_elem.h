@@ -1,5 +1,5 @@
 // reduce_elem.h — device-side element rules shared by the reduce kernels (reduce_kernels.hip) and the one-sided
-// IPC AllReduce kernel (ipc_kernels.hip). See reduce_kernels.hip for the reference semantics they restate.
+// IPC AllReduce kernel (ipc_kernel_body.h). See reduce_kernels.hip for the reference semantics they restate.
 #pragma once
 
 #include <hip/hip_runtime.h>

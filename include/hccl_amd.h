@@ -234,6 +234,14 @@ extern HcclResult HcclAmdCommGraphStats(HcclComm comm, uint64_t* launches, uint6
  * AllReduce, in polls (diagnostic; 0 = no block ever waited). */
 extern HcclResult HcclAmdCommIpcStatus(HcclComm comm, uint32_t* status);
 
+/* Phase timeline of the one-sided kernel (diagnostics). With HCCL_AMD_IPC_TRACE=1 set when comm makes its first IPC
+ * call, every launch stamps, per rank and workgroup, 8 s_memrealtime values (100 MHz) of its last staging round:
+ * entry, round start, phase 0 issued, barrier 1 passed, phase 1 issued, barrier 2 passed, phase 2 issued, exit.
+ * Synchronises the device and copies the last launch's stamps into stamps[rank][block][8] (cap >= 16 x 512 x 8
+ * entries; in a loopback world call it on rank 0, which issues the world's launch); *blocks = workgroups per rank of
+ * that launch. HCCL_E_NOT_SUPPORT when tracing is off. */
+extern HcclResult HcclAmdCommIpcTrace(HcclComm comm, uint64_t* stamps, uint64_t cap, uint32_t* blocks);
+
 /* The barrier wait bound of the one-sided kernel in ms, as the next IPC call would take it from the environment:
  * HCCL_AMD_IPC_TIMEOUT_MS if set (1 .. 3600000), else HCCL_EXEC_TIMEOUT by the reference's AIV-mode rule (seconds,
  * at most two decimals; 0, above 1091 or unset = 1091 s). A wait past it fails the communicator (HcclGetCommAsyncError). */

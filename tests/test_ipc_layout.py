@@ -1,4 +1,4 @@
-"""Index model of the one-sided IPC collectives (hccl_amd/csrc/ipc_kernels.hip, geometry from ipc.cc
+"""Index model of the one-sided IPC collectives (hccl_amd/csrc/ipc_kernel_body.h, geometry from ipc.cc
 RunIpcCollective), run on the CPU before any launch. With the kernel's exact loop bounds (vector loop over
 [vlo, vhi), element loop from max(vhi*V, lo) to hi), every phase must
   * stay inside each buffer it touches (input, output, a slot of the owner's staging, a result area), and
@@ -52,7 +52,7 @@ def geometry(kind, n, count, es, group=1, vblocks=None):
 
 
 def shares(plen, b, block, tile, blocks=BLOCKS):
-    """ipc_kernels.hip ForBlockShare: block b's ranges of piece coordinates [0, plen) -- one window of `block`
+    """ipc_kernel_body.h ForBlockShare: block b's ranges of piece coordinates [0, plen) -- one window of `block`
     elements (tile == 0, BlockWindow), or tiles of `tile` elements at b, b + B, ... (B = blocks)."""
     if tile == 0:
         lo = min(plen, b * block)
@@ -73,7 +73,7 @@ def touched(lo, hi, v, vec=True):
 
 
 def sub_starts(length, n, es, rs4k):
-    """Sub-slice starts of a chunk for order O6 (ipc_kernels.hip SubStart), plus the end."""
+    """Sub-slice starts of a chunk for order O6 (ipc_kernel_body.h SubStart), plus the end."""
     parts = n - 1
     if rs4k and parts >= 2:
         al = length * es // parts // 4096 * 4096 // es

@@ -1,4 +1,4 @@
-"""Model check of the IPC kernel's cross-rank protocol (hccl_amd/csrc/ipc_kernels.hip k_ipc_collective, ipc.cc).
+"""Model check of the IPC kernel's cross-rank protocol (hccl_amd/csrc/ipc_kernel_body.h k_ipc_collective, ipc.cc).
 
 Ranks are streams of launches; a launch is `blocks` workgroups, each running the kernel's per-round steps. One step
 runs at a time, and a random scheduler picks which, so many interleavings of blocks and ranks are tried:

@@ -1,4 +1,4 @@
-"""The identity the one-sided RHD kernel (HCCL_AMD_ALGO_IPC_RHD, ipc_kernels.hip RhdFold) rests on — host only.
+"""The identity the one-sided RHD kernel (HCCL_AMD_ALGO_IPC_RHD, ipc_kernel_body.h RhdFold) rests on — host only.
 
 The RHD AllReduce (schedule.cc AllReduceRhd) gives element e of part j, virtual chunk v the value the classic recursive
 halving builds on virtual ranks (each step: dst = partner (op) mine). RhdFold computes it from all n inputs at once as

@@ -17,6 +17,9 @@
 #   ipc_ab         one-sided kernel: block shares (contiguous / tiles) x cache policy A/B, loopback world
 #   harness        bench.py's N > 1 code path with two ranks sharing the GPU (IPC-only; a crash check, not a result)
 #   counters       the TCC counters this rocprofv3 offers
+#   ipc_unroll     one-sided kernel: vectors in flight of the copy and fold loops x workgroups per rank (A/B)
+#   ipc_staging    one-sided kernel: uncached vs cached staging memory (A/B on one device)
+#   phase_trace    per-block phase stamps of the one-sided two-shot kernel, loopback worlds n = 2, 4, 8
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
 REPO=$(pwd)
@@ -131,6 +134,21 @@ step_harness() {
 step_ipc_ab() {
   run ipc_ab 400 python3 -u tools/ipc_variant_ab.py
   grep '^{' "$OUT/ipc_ab.log" > "$OUT/ipc_variant_ab.jsonl" || true
+}
+
+step_ipc_unroll() {
+  AB_SWEEP=unroll run ipc_unroll 400 python3 -u tools/ipc_variant_ab.py
+  grep '^{' "$OUT/ipc_unroll.log" > "$OUT/ipc_variant_ab_unroll.jsonl" || true
+}
+
+step_ipc_staging() {
+  AB_SWEEP=staging run ipc_staging 400 python3 -u tools/ipc_variant_ab.py
+  grep '^{' "$OUT/ipc_staging.log" > "$OUT/ipc_variant_ab_staging.jsonl" || true
+}
+
+step_phase_trace() {
+  run phase_trace 300 python3 -u tools/ipc_phase_trace.py
+  grep '^{' "$OUT/phase_trace.log" > "$OUT/ipc_phase_trace.jsonl" || true
 }
 
 step_counters() {
