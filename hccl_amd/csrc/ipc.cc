@@ -64,6 +64,7 @@ HcclResult IpcSetup(Comm& c)
     // the hand-off through the L2s of that one device.
     const char* cachedEnv = std::getenv("HCCL_AMD_IPC_STAGING_CACHED");
     const bool cached = cachedEnv != nullptr && std::strcmp(cachedEnv, "1") == 0;
+    s.cachedStaging = cached;
     const size_t stgBytes = s.stgInBytes + s.stgResBytes + 2 * s.stgAltBytes;
     bool ok = (cached ? hipMalloc(&s.stg, stgBytes) : hipExtMallocWithFlags(&s.stg, stgBytes, hipDeviceMallocUncached)) ==
                   hipSuccess &&
@@ -194,6 +195,14 @@ uint32_t IpcUnroll(const char* name, uint32_t dflt)
     if (e == nullptr || *e == '\0') return dflt;
     const unsigned long v = std::strtoul(e, nullptr, 10);
     return (v == 2 || v == 4 || v == 8) ? static_cast<uint32_t>(v) : dflt;
+}
+
+// HCCL_AMD_IPC_LIGHT_FENCE=1: barriers without the XCD-wide L2 write-back and invalidate (IpcArgs::fence; r03 A/B).
+// Read per call, equal on every rank.
+bool IpcLightFence()
+{
+    const char* e = std::getenv("HCCL_AMD_IPC_LIGHT_FENCE");
+    return e != nullptr && std::strcmp(e, "1") == 0;
 }
 
 bool IpcNonTemporal()
@@ -655,6 +664,7 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
         g.nt = IpcNonTemporal() ? 1u : 0u;
         g.copyU = IpcUnroll("HCCL_AMD_IPC_COPY_U", 4);
         g.foldU = IpcUnroll("HCCL_AMD_IPC_FOLD_U", 4);
+        g.fence = (IpcLightFence() && !s.cachedStaging) ? 1u : 0u;
         g.rounds = static_cast<uint32_t>((widest + g.piece - 1) / g.piece);
         g.epochSpan = (single ? 1 : 2) * g.rounds;
     };

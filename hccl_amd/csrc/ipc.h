@@ -113,6 +113,8 @@ struct IpcArgs {
     uint32_t nt;         // non-temporal loads and stores in the copy and fold loops
     uint32_t copyU;      // vectors per lane in flight in the copy loops (2, 4, 8)
     uint32_t foldU;      // vectors per lane and operand in flight in the fold loop (2, 4, 8)
+    uint32_t fence;      // barrier fences: 0 = system-scope release (L2 write-back) and acquire (L2 invalidate);
+                         // 1 = light: the drains alone release, an agent-scope acquire (L1) (uncached staging only)
     uint32_t rounds;
     uint32_t epochSpan;  // barriers per block in this launch: the device epoch counter advances by this much
     uint64_t outStride;  // kIpcAllGather: elements between consecutive ranks' blocks of the output (sendCount)
@@ -197,6 +199,7 @@ struct IpcState {
     uint64_t stgAltBytes = 0;      // each of the two alternate slot areas of the single-barrier kinds
     uint32_t blocks = 0;
     uint32_t ranksOnDevice = 1;    // rank mode: the most ranks that share one device (by PCI bus id), same on all ranks
+    bool cachedStaging = false;    // HCCL_AMD_IPC_STAGING_CACHED=1 at set-up (diagnostics): barriers keep full fences
     uint64_t* trace = nullptr;     // HCCL_AMD_IPC_TRACE=1 at set-up: [kIpcMaxRanks][kIpcMaxBlocks][kIpcTraceSlots]
 };
 

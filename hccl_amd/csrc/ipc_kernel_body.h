@@ -79,7 +79,9 @@ __device__ __forceinline__ bool Barrier(const IpcArgs& a, FlagLane fl, uint32_t 
         // wave's counter empty (MI355X_MICROARCH.md, "Compiler hazard"): the release store form lost it in 8 of the
         // 73 instantiations (the epoch load before it is a waited load), so a peer could read the data before it
         // left this XCD's L2. The explicit wait, invisible to that pass, keeps the flag behind the write-back.
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        // IpcArgs::fence = 1 (light): the handed-off bytes are all in uncached staging, whose stores no L2 holds, so
+        // the waves' vmcnt(0) drains above are the release; no XCD-wide write-back.
+        if (a.fence == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(fl.remote, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         uint32_t* mine = fl.mine;
@@ -110,7 +112,12 @@ __device__ __forceinline__ bool Barrier(const IpcArgs& a, FlagLane fl, uint32_t 
         }
         waitMax = max(waitMax, polls);
         if (cut) failed = 1;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        // light: the CU's L1 only (agent scope); the system-scope acquire also invalidates the XCD's whole L2
+        if (a.fence == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        } else {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate has completed before the barrier opens
     }
     __syncthreads();

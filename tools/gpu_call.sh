@@ -19,6 +19,7 @@
 #   counters       the TCC counters this rocprofv3 offers
 #   ipc_unroll     one-sided kernel: vectors in flight of the copy and fold loops x workgroups per rank (A/B)
 #   ipc_staging    one-sided kernel: uncached vs cached staging memory (A/B on one device)
+#   ipc_fence      one-sided kernel: system-scope vs light barrier fences x workgroups per rank (A/B)
 #   phase_trace    per-block phase stamps of the one-sided two-shot kernel, loopback worlds n = 2, 4, 8
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
@@ -144,6 +145,11 @@ step_ipc_unroll() {
 step_ipc_staging() {
   AB_SWEEP=staging run ipc_staging 400 python3 -u tools/ipc_variant_ab.py
   grep '^{' "$OUT/ipc_staging.log" > "$OUT/ipc_variant_ab_staging.jsonl" || true
+}
+
+step_ipc_fence() {
+  AB_SWEEP=fence run ipc_fence 400 python3 -u tools/ipc_variant_ab.py
+  grep '^{' "$OUT/ipc_fence.log" > "$OUT/ipc_variant_ab_fence.jsonl" || true
 }
 
 step_phase_trace() {

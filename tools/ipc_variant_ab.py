@@ -6,7 +6,7 @@ world's launch stream) and its algorithmic rate (n x 2(3n-2)/n x bytes per rank 
 is compared bit for bit with the first variant's.
   python tools/ipc_variant_ab.py > gpurun_out/ipc_variant_ab.jsonl
 AB_SWEEP = shapes (default: staging size x workgroups per rank), policy (tiles x nt), unroll (vectors in flight),
-staging (uncached vs cached staging memory, one device).
+staging (uncached vs cached staging memory, one device), fence (barrier fences x workgroups).
 """
 import json
 import os
@@ -201,6 +201,63 @@ def run_staging(n, mib, algo=H.Algo.IPC_TWOSHOT):
                           "barrier_timeouts": status}), flush=True)
 
 
+# fifth sweep (AB_SWEEP=fence): barrier fences (HCCL_AMD_IPC_LIGHT_FENCE) x workgroups per rank, one world
+FENCES = [(0, 128), (1, 128), (0, 256), (1, 256)]
+
+
+def run_fence(n, mib, algo=H.Algo.IPC_TWOSHOT):
+    """System-scope vs light barrier fences, interleaved over rounds on one world; outputs compared bit for bit."""
+    dev = torch.device("cuda", 0)
+    comms = H.loopback_world(n)
+    for c in comms:
+        c.set_algo(algo)
+    count = max(64, (mib << 20) // 4)
+    g = torch.Generator(device=dev).manual_seed(61 + n)
+    xs = [torch.rand(count, device=dev, generator=g) for _ in range(n)]
+    ys = [torch.empty_like(x) for x in xs]
+    streams = [torch.cuda.Stream() for _ in range(n)]
+    pool = ThreadPoolExecutor(n)
+
+    def call():
+        list(pool.map(lambda r: comms[r].all_reduce(xs[r], ys[r], H.HcclReduceOp.SUM, streams[r]), range(n)))
+
+    times = {v: [] for v in FENCES}
+    ok = {v: True for v in FENCES}
+    ref = None
+    for rnd in range(ROUNDS):
+        order = FENCES[rnd % len(FENCES):] + FENCES[:rnd % len(FENCES)]
+        for v in order:
+            os.environ["HCCL_AMD_IPC_LIGHT_FENCE"] = str(v[0])
+            for c in comms:
+                c.set_ipc_blocks(v[1])
+            call()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(streams[0])
+            for _ in range(CALLS):
+                call()
+            e1.record(streams[0])
+            torch.cuda.synchronize()
+            times[v].append(e0.elapsed_time(e1) * 1e3 / CALLS)
+            if ref is None:
+                ref = [y.clone() for y in ys]
+            else:
+                ok[v] = ok[v] and all(bool(torch.equal(a, b)) for a, b in zip(ys, ref))
+    os.environ.pop("HCCL_AMD_IPC_LIGHT_FENCE")
+    status = comms[0].ipc_status() & 1
+    pool.shutdown()
+    for c in comms:
+        c.destroy()
+    alg = n * 2 * (3 * n - 2) * count * 4 // n
+    for v in FENCES:
+        med = float(np.median(times[v]))
+        print(json.dumps({"ranks": n, "bytes_per_rank": count * 4, "algo": algo.name, "light_fence": v[0],
+                          "blocks_per_rank": v[1], "median_us": round(med, 1), "min_us": round(min(times[v]), 1),
+                          "max_us": round(max(times[v]), 1), "TBps": round(alg / med / 1e6, 3),
+                          "frac": round(alg / med / 1e6 / 8.0, 4), "same_bits": ok[v],
+                          "barrier_timeouts": status}), flush=True)
+
+
 # third sweep (AB_SWEEP=unroll): (copy U, fold U, workgroups per rank), nt on, contiguous windows, one world
 UNROLLS = [(4, 4, 128), (4, 2, 128), (8, 4, 128), (8, 2, 128), (2, 2, 256), (4, 2, 256), (4, 4, 256), (8, 8, 128)]
 
@@ -265,7 +322,10 @@ def run_unroll(n, mib, algo=H.Algo.IPC_TWOSHOT):
 def main():
     torch.cuda.set_device(0)
     os.environ.setdefault("HCCL_AMD_IPC_TIMEOUT_MS", "20000")
-    if os.environ.get("AB_SWEEP") == "staging":
+    if os.environ.get("AB_SWEEP") == "fence":
+        for n, mib in ((2, 512), (4, 256), (8, 64)):
+            run_fence(n, mib)
+    elif os.environ.get("AB_SWEEP") == "staging":
         for n, mib in ((2, 512), (4, 256)):
             run_staging(n, mib)
     elif os.environ.get("AB_SWEEP") == "unroll":
