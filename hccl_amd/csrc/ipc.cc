@@ -205,6 +205,13 @@ bool IpcLightFence()
     return e != nullptr && std::strcmp(e, "1") == 0;
 }
 
+// HCCL_AMD_IPC_THREADS: threads per workgroup, 256 (default) or 512 (r03 A/B). Read per call, equal on every rank.
+uint32_t IpcThreads()
+{
+    const char* e = std::getenv("HCCL_AMD_IPC_THREADS");
+    return (e != nullptr && std::strcmp(e, "512") == 0) ? 512u : static_cast<uint32_t>(kIpcBlock);
+}
+
 bool IpcNonTemporal()
 {
     const char* e = std::getenv("HCCL_AMD_IPC_NT");
@@ -552,7 +559,7 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
     // so ranks of a node agree on it.
     {
         const uint32_t here = c.transport->SharedDevice() ? n : std::max<uint32_t>(1, s.ranksOnDevice);
-        const uint32_t resident = IpcResidentBlocks(dt, op, plan.order == kIpcRhd);
+        const uint32_t resident = IpcResidentBlocks(dt, op, plan.order == kIpcRhd, IpcThreads());
         if (resident != 0) s.blocks = std::max<uint32_t>(1, std::min(s.blocks, resident / here));
     }
     const uint64_t V = 16 / es;
@@ -665,6 +672,7 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
         g.copyU = IpcUnroll("HCCL_AMD_IPC_COPY_U", 4);
         g.foldU = IpcUnroll("HCCL_AMD_IPC_FOLD_U", 4);
         g.fence = (IpcLightFence() && !s.cachedStaging) ? 1u : 0u;
+        g.threads = IpcThreads();
         g.rounds = static_cast<uint32_t>((widest + g.piece - 1) / g.piece);
         g.epochSpan = (single ? 1 : 2) * g.rounds;
     };

@@ -10,7 +10,8 @@
 namespace hccl_amd {
 
 constexpr int kIpcMaxRanks = 16;
-constexpr int kIpcBlock = 256;  // threads per workgroup of the one-sided kernel
+constexpr int kIpcBlock = 256;        // threads per workgroup of the one-sided kernel (default)
+constexpr int kIpcMaxThreads = 512;   // HCCL_AMD_IPC_THREADS may take 512 (r03 A/B)
 
 enum IpcKind : uint32_t {
     kIpcAllReduce = 0,         // two-shot: owner c folds chunk c, every rank gets every chunk
@@ -113,6 +114,7 @@ struct IpcArgs {
     uint32_t nt;         // non-temporal loads and stores in the copy and fold loops
     uint32_t copyU;      // vectors per lane in flight in the copy loops (2, 4, 8)
     uint32_t foldU;      // vectors per lane and operand in flight in the fold loop (2, 4, 8)
+    uint32_t threads;    // threads per workgroup (kIpcBlock, or 512 by HCCL_AMD_IPC_THREADS)
     uint32_t fence;      // barrier fences: 0 = system-scope release (L2 write-back) and acquire (L2 invalidate);
                          // 1 = light: the drains alone release, an agent-scope acquire (L1) (uncached staging only)
     uint32_t rounds;
@@ -175,7 +177,7 @@ HCCL_AMD_IPC_DTYPE_DECL(Fp64)
 
 // Workgroups of the IPC kernel for (dt, op) that the device holds at once (occupancy x CUs; 0 if unknown). Every
 // block of a launch waits at barriers for its peers' blocks, so the blocks that share a device must all be resident.
-uint32_t IpcResidentBlocks(HcclDataType dt, HcclReduceOp op, bool rhd);
+uint32_t IpcResidentBlocks(HcclDataType dt, HcclReduceOp op, bool rhd, uint32_t threads);
 
 // Writes back and invalidates every XCD's L2 at system scope (one maintenance block per CU); synchronous on `stream`.
 HcclResult ScrubL2(hipStream_t stream);

@@ -223,14 +223,14 @@ __device__ __forceinline__ void ForBlockShare(const IpcArgs& a, uint64_t len, F&
 template <int NT, int U>
 __device__ __forceinline__ void CopyVecs(u32x4* d, const u32x4* s, uint64_t& v, uint64_t vhi)
 {
-    for (; v + (U - 1) * kIpcBlock < vhi; v += U * kIpcBlock) {
+    for (; v + (U - 1) * blockDim.x < vhi; v += U * blockDim.x) {
         u32x4 x[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) x[u] = ld<NT>(s + v + u * kIpcBlock);
+        for (int u = 0; u < U; ++u) x[u] = ld<NT>(s + v + u * blockDim.x);
 #pragma unroll
-        for (int u = 0; u < U; ++u) st<NT>(d + v + u * kIpcBlock, x[u]);
+        for (int u = 0; u < U; ++u) st<NT>(d + v + u * blockDim.x, x[u]);
     }
-    for (; v < vhi; v += kIpcBlock) st<NT>(d + v, ld<NT>(s + v));
+    for (; v < vhi; v += blockDim.x) st<NT>(d + v, ld<NT>(s + v));
 }
 
 // Runtime unroll of the copy and fold loops (IpcArgs::copyU / foldU: 2, 4 or 8 vectors per lane in flight; r03 A/B)
@@ -265,7 +265,7 @@ __device__ __forceinline__ void CopyRange(S* dst, const S* src, Range r, bool ve
             CopyVecs<0, U>(d, s, v, vhi);
         }
     });
-    for (uint64_t e = max(vhi * V, r.lo) + threadIdx.x; e < r.hi; e += kIpcBlock) dst[e] = src[e];
+    for (uint64_t e = max(vhi * V, r.lo) + threadIdx.x; e < r.hi; e += blockDim.x) dst[e] = src[e];
 }
 
 // Rank of operand i (0 .. n-1) of a fold of chunk t in the given order; j = the sub-slice (kIpcO6 only).
@@ -380,7 +380,7 @@ __device__ __forceinline__ void TreeSeg(uint32_t n, const RankSrc& rankSrc, cons
     constexpr uint64_t V = 16 / sizeof(S);
     const uint64_t vb = (r.lo + V - 1) / V, ve = r.hi / V;
     auto scalarTree = [&](uint64_t lo, uint64_t hi) {
-        for (uint64_t e = lo + threadIdx.x; e < hi; e += kIpcBlock) {
+        for (uint64_t e = lo + threadIdx.x; e < hi; e += blockDim.x) {
             const S acc = TreeFoldN<E, OP>(n, [&](uint32_t q) { return rankSrc(rankOf(q))[e]; });
             for (uint32_t d = 0; d < ndst; ++d) dsts(d)[e] = acc;
         }
@@ -390,7 +390,7 @@ __device__ __forceinline__ void TreeSeg(uint32_t n, const RankSrc& rankSrc, cons
         return;
     }
     scalarTree(r.lo, vb * V);
-    for (uint64_t v = vb + threadIdx.x; v < ve; v += kIpcBlock) {
+    for (uint64_t v = vb + threadIdx.x; v < ve; v += blockDim.x) {
         const u32x4 acc = TreeFoldN<E, OP>(
             n, [&](uint32_t q) { return reinterpret_cast<const u32x4*>(rankSrc(rankOf(q)))[v]; });
         for (uint32_t d = 0; d < ndst; ++d) reinterpret_cast<u32x4*>(dsts(d))[v] = acc;
@@ -417,7 +417,7 @@ __device__ __forceinline__ void FoldSeg(const IpcArgs& a, uint32_t me, uint32_t 
     }
     auto src = [&](uint32_t i) { return rankSrc(OperandRank(a.order, n, me, j, i)); };
     auto scalar = [&](uint64_t lo, uint64_t hi) {
-        for (uint64_t e = lo + threadIdx.x; e < hi; e += kIpcBlock) {
+        for (uint64_t e = lo + threadIdx.x; e < hi; e += blockDim.x) {
             S acc = src(0)[e];
             for (uint32_t i = 1; i < n; ++i) acc = E::template ap<OP>(src(i)[e], acc);
             for (uint32_t d = 0; d < ndst; ++d) dsts(d)[e] = acc;
@@ -433,20 +433,20 @@ __device__ __forceinline__ void FoldSeg(const IpcArgs& a, uint32_t me, uint32_t 
     auto body = [&](auto ntTag, auto uTag) {
         constexpr int NT = decltype(ntTag)::value;
         constexpr int U = decltype(uTag)::value;
-        for (; v + (U - 1) * kIpcBlock < ve; v += U * kIpcBlock) {
+        for (; v + (U - 1) * blockDim.x < ve; v += U * blockDim.x) {
             u32x4 acc[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) acc[u] = ld<NT>(reinterpret_cast<const u32x4*>(src(0)) + v + u * kIpcBlock);
+            for (int u = 0; u < U; ++u) acc[u] = ld<NT>(reinterpret_cast<const u32x4*>(src(0)) + v + u * blockDim.x);
             for (uint32_t i = 1; i < n; ++i) {
                 u32x4 x[U];
 #pragma unroll
-                for (int u = 0; u < U; ++u) x[u] = ld<NT>(reinterpret_cast<const u32x4*>(src(i)) + v + u * kIpcBlock);
+                for (int u = 0; u < U; ++u) x[u] = ld<NT>(reinterpret_cast<const u32x4*>(src(i)) + v + u * blockDim.x);
 #pragma unroll
                 for (int u = 0; u < U; ++u) acc[u] = combine<E, OP>(x[u], acc[u]);
             }
             for (uint32_t d = 0; d < ndst; ++d) {
 #pragma unroll
-                for (int u = 0; u < U; ++u) st<NT>(reinterpret_cast<u32x4*>(dsts(d)) + v + u * kIpcBlock, acc[u]);
+                for (int u = 0; u < U; ++u) st<NT>(reinterpret_cast<u32x4*>(dsts(d)) + v + u * blockDim.x, acc[u]);
             }
         }
     };
@@ -457,7 +457,7 @@ __device__ __forceinline__ void FoldSeg(const IpcArgs& a, uint32_t me, uint32_t 
             body(std::integral_constant<int, 0>{}, uTag);
         }
     });
-    for (; v < ve; v += kIpcBlock) {
+    for (; v < ve; v += blockDim.x) {
         u32x4 acc = reinterpret_cast<const u32x4*>(src(0))[v];
         for (uint32_t i = 1; i < n; ++i) acc = combine<E, OP>(reinterpret_cast<const u32x4*>(src(i))[v], acc);
         for (uint32_t d = 0; d < ndst; ++d) reinterpret_cast<u32x4*>(dsts(d))[v] = acc;
@@ -524,7 +524,7 @@ __device__ __forceinline__ void FoldRange(const IpcArgs& a, uint32_t me, uint64_
 // its own so that the RHD tree's register use never lowers the occupancy of the others: a loopback world needs every
 // rank's blocks resident at once.
 template <class E, int OP, bool kRhd>
-__global__ __launch_bounds__(kIpcBlock) void k_ipc_collective(IpcArgs a)
+__global__ __launch_bounds__(kIpcMaxThreads) void k_ipc_collective(IpcArgs a)
 {
     const uint32_t kind = kRhd ? uint32_t(kIpcAllReduceOneShot) : a.kind;
     using S = typename E::S;
@@ -641,18 +641,18 @@ hipError_t LaunchIpcT(int op, const IpcArgs& a, dim3 grid, hipStream_t s)
 {
     if (a.order == kIpcRhd) {
         switch (op) {
-            case R_SUM: hipLaunchKernelGGL((k_ipc_collective<E, R_SUM, true>), grid, dim3(kIpcBlock), 0, s, a); break;
-            case R_PROD: hipLaunchKernelGGL((k_ipc_collective<E, R_PROD, true>), grid, dim3(kIpcBlock), 0, s, a); break;
-            case R_MAX: hipLaunchKernelGGL((k_ipc_collective<E, R_MAX, true>), grid, dim3(kIpcBlock), 0, s, a); break;
-            default: hipLaunchKernelGGL((k_ipc_collective<E, R_MIN, true>), grid, dim3(kIpcBlock), 0, s, a); break;
+            case R_SUM: hipLaunchKernelGGL((k_ipc_collective<E, R_SUM, true>), grid, dim3(a.threads), 0, s, a); break;
+            case R_PROD: hipLaunchKernelGGL((k_ipc_collective<E, R_PROD, true>), grid, dim3(a.threads), 0, s, a); break;
+            case R_MAX: hipLaunchKernelGGL((k_ipc_collective<E, R_MAX, true>), grid, dim3(a.threads), 0, s, a); break;
+            default: hipLaunchKernelGGL((k_ipc_collective<E, R_MIN, true>), grid, dim3(a.threads), 0, s, a); break;
         }
         return hipGetLastError();
     }
     switch (op) {
-        case R_SUM: hipLaunchKernelGGL((k_ipc_collective<E, R_SUM, false>), grid, dim3(kIpcBlock), 0, s, a); break;
-        case R_PROD: hipLaunchKernelGGL((k_ipc_collective<E, R_PROD, false>), grid, dim3(kIpcBlock), 0, s, a); break;
-        case R_MAX: hipLaunchKernelGGL((k_ipc_collective<E, R_MAX, false>), grid, dim3(kIpcBlock), 0, s, a); break;
-        default: hipLaunchKernelGGL((k_ipc_collective<E, R_MIN, false>), grid, dim3(kIpcBlock), 0, s, a); break;
+        case R_SUM: hipLaunchKernelGGL((k_ipc_collective<E, R_SUM, false>), grid, dim3(a.threads), 0, s, a); break;
+        case R_PROD: hipLaunchKernelGGL((k_ipc_collective<E, R_PROD, false>), grid, dim3(a.threads), 0, s, a); break;
+        case R_MAX: hipLaunchKernelGGL((k_ipc_collective<E, R_MAX, false>), grid, dim3(a.threads), 0, s, a); break;
+        default: hipLaunchKernelGGL((k_ipc_collective<E, R_MIN, false>), grid, dim3(a.threads), 0, s, a); break;
     }
     return hipGetLastError();
 }

@@ -39,13 +39,13 @@ HcclResult ScrubL2(hipStream_t stream)
     return HCCL_SUCCESS;
 }
 
-uint32_t IpcResidentBlocks(HcclDataType dt, HcclReduceOp op, bool rhd)
+uint32_t IpcResidentBlocks(HcclDataType dt, HcclReduceOp op, bool rhd, uint32_t threads)
 {
-    // per process and (dtype, op, kind of kernel); one device model per node (0 = not yet asked)
-    static std::atomic<uint32_t> cache[32][4][2];
-    const uint32_t di = static_cast<uint32_t>(dt), oi = static_cast<uint32_t>(op);
+    // per process and (dtype, op, kind of kernel, block size); one device model per node (0 = not yet asked)
+    static std::atomic<uint32_t> cache[32][4][2][2];
+    const uint32_t di = static_cast<uint32_t>(dt), oi = static_cast<uint32_t>(op), ti = threads > kIpcBlock ? 1 : 0;
     if (di < 32 && oi < 4) {
-        const uint32_t v = cache[di][oi][rhd ? 1 : 0].load(std::memory_order_relaxed);
+        const uint32_t v = cache[di][oi][rhd ? 1 : 0][ti].load(std::memory_order_relaxed);
         if (v != 0) return v;
     }
     const void* k = nullptr;
@@ -62,13 +62,13 @@ uint32_t IpcResidentBlocks(HcclDataType dt, HcclReduceOp op, bool rhd)
         default: return 0;
     }
     int perCu = 0, cus = 0, dev = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCu, k, kIpcBlock, 0) != hipSuccess || perCu <= 0) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCu, k, static_cast<int>(threads), 0) != hipSuccess || perCu <= 0) return 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
         return 0;
     }
     const uint32_t v = static_cast<uint32_t>(perCu) * static_cast<uint32_t>(cus);
-    if (di < 32 && oi < 4) cache[di][oi][rhd ? 1 : 0].store(v, std::memory_order_relaxed);
+    if (di < 32 && oi < 4) cache[di][oi][rhd ? 1 : 0][ti].store(v, std::memory_order_relaxed);
     return v;
 }
 

@@ -20,6 +20,7 @@
 #   ipc_unroll     one-sided kernel: vectors in flight of the copy and fold loops x workgroups per rank (A/B)
 #   ipc_staging    one-sided kernel: uncached vs cached staging memory (A/B on one device)
 #   ipc_fence      one-sided kernel: system-scope vs light barrier fences x workgroups per rank (A/B)
+#   ipc_light_tests  the one-sided kernel's GPU tests with light barrier fences
 #   phase_trace    per-block phase stamps of the one-sided two-shot kernel, loopback worlds n = 2, 4, 8
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
@@ -150,6 +151,14 @@ step_ipc_staging() {
 step_ipc_fence() {
   AB_SWEEP=fence run ipc_fence 400 python3 -u tools/ipc_variant_ab.py
   grep '^{' "$OUT/ipc_fence.log" > "$OUT/ipc_variant_ab_fence.jsonl" || true
+}
+
+# every one-sided-kernel GPU test with the light barrier fences (HCCL_AMD_IPC_LIGHT_FENCE=1; the rank-mode children
+# inherit it): loopback worlds of every kind and family, rank mode, the random call-sequence stress
+step_ipc_light_tests() {
+  HCCL_AMD_IPC_LIGHT_FENCE=1 HCCL_AMD_RANDOM_DRAWS=1000 run ipc_light_tests 600 python3 -u -m pytest \
+    tests/test_gpu_ipc_ranks.py tests/test_gpu_ipc_stress.py tests/test_gpu_collectives.py -m gpu -k "ipc or IPC or aiv or AIV" \
+    -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
 }
 
 step_phase_trace() {

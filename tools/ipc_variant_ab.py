@@ -201,8 +201,9 @@ def run_staging(n, mib, algo=H.Algo.IPC_TWOSHOT):
                           "barrier_timeouts": status}), flush=True)
 
 
-# fifth sweep (AB_SWEEP=fence): barrier fences (HCCL_AMD_IPC_LIGHT_FENCE) x workgroups per rank, one world
-FENCES = [(0, 128), (1, 128), (0, 256), (1, 256)]
+# fifth sweep (AB_SWEEP=fence): barrier fences (HCCL_AMD_IPC_LIGHT_FENCE) x workgroups per rank x threads per
+# workgroup (HCCL_AMD_IPC_THREADS), one world
+FENCES = [(0, 128, 256), (1, 128, 256), (0, 256, 256), (1, 256, 256), (0, 128, 512), (1, 128, 512), (1, 64, 512)]
 
 
 def run_fence(n, mib, algo=H.Algo.IPC_TWOSHOT):
@@ -228,6 +229,7 @@ def run_fence(n, mib, algo=H.Algo.IPC_TWOSHOT):
         order = FENCES[rnd % len(FENCES):] + FENCES[:rnd % len(FENCES)]
         for v in order:
             os.environ["HCCL_AMD_IPC_LIGHT_FENCE"] = str(v[0])
+            os.environ["HCCL_AMD_IPC_THREADS"] = str(v[2])
             for c in comms:
                 c.set_ipc_blocks(v[1])
             call()
@@ -244,6 +246,7 @@ def run_fence(n, mib, algo=H.Algo.IPC_TWOSHOT):
             else:
                 ok[v] = ok[v] and all(bool(torch.equal(a, b)) for a, b in zip(ys, ref))
     os.environ.pop("HCCL_AMD_IPC_LIGHT_FENCE")
+    os.environ.pop("HCCL_AMD_IPC_THREADS")
     status = comms[0].ipc_status() & 1
     pool.shutdown()
     for c in comms:
@@ -252,7 +255,7 @@ def run_fence(n, mib, algo=H.Algo.IPC_TWOSHOT):
     for v in FENCES:
         med = float(np.median(times[v]))
         print(json.dumps({"ranks": n, "bytes_per_rank": count * 4, "algo": algo.name, "light_fence": v[0],
-                          "blocks_per_rank": v[1], "median_us": round(med, 1), "min_us": round(min(times[v]), 1),
+                          "blocks_per_rank": v[1], "threads": v[2], "median_us": round(med, 1), "min_us": round(min(times[v]), 1),
                           "max_us": round(max(times[v]), 1), "TBps": round(alg / med / 1e6, 3),
                           "frac": round(alg / med / 1e6 / 8.0, 4), "same_bits": ok[v],
                           "barrier_timeouts": status}), flush=True)
