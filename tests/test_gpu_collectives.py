@@ -147,6 +147,70 @@ def test_ipc_default_staging(monkeypatch, n, count):
             c.destroy()
 
 
+@pytest.mark.parametrize("n,count", [(2, (3 << 20) + 5), (4, 1 << 20)])
+def test_ipc_phase_trace(monkeypatch, n, count):
+    """HCCL_AMD_IPC_TRACE=1 (r03): every block of every rank of the world's launch stamps its phases, in order
+    (entry <= round <= phase 0 <= barrier 1 <= phase 1 <= barrier 2 <= phase 2 <= exit), and the output is still the
+    two-shot's bits. Slots beyond the launch's blocks and ranks stay zero."""
+    monkeypatch.setenv("HCCL_AMD_IPC_TRACE", "1")
+    comms = H.loopback_world(n)
+    try:
+        for c in comms:
+            c.set_ipc_blocks(32)
+        xs = [O.random_operands(O.FP32, count, seed=950 + r, edge=False) for r in range(n)]
+        used, outs = collective(comms, AR, 7, O.FP32, O.SUM, xs, count)
+        assert used == 7
+        want = R.expected(AR, R.ALGO_TWOSHOT, O.FP32, O.SUM, xs, count)
+        for r in range(n):
+            assert O.equal_bits(O.FP32, outs[r], want[r]), r
+        st, blocks = comms[0].ipc_trace()
+        assert blocks == 32
+        a = st[:n, :blocks, :].astype(np.int64)
+        assert (a > 0).all(), "a block or rank left a stamp unwritten"
+        assert (np.diff(a, axis=2) >= 0).all(), "phase stamps out of order"
+        assert not st[n:].any() and not st[:n, blocks:].any()
+        # a world without the variable has no trace
+        plain = H.loopback_world(2)
+        monkeypatch.delenv("HCCL_AMD_IPC_TRACE")
+        try:
+            collective(plain, AR, 7, O.FP32, O.SUM, xs[:2], count)
+            with pytest.raises(H.HcclError):
+                plain[0].ipc_trace()
+        finally:
+            for c in plain:
+                c.destroy()
+    finally:
+        for c in comms:
+            c.destroy()
+
+
+@pytest.mark.parametrize("fence,threads", [("1", "256"), ("1", "512"), ("0", "512")])
+@pytest.mark.parametrize("kind", [AR, RS, AG])
+def test_ipc_barrier_variants(monkeypatch, fence, threads, kind):
+    """The one-sided kernel with light barrier fences (HCCL_AMD_IPC_LIGHT_FENCE=1: the waves' drains release, an
+    agent-scope acquire) and with 512-thread workgroups (HCCL_AMD_IPC_THREADS): same bits as the schedule's order over
+    several staging rounds and odd counts, barrier status clean."""
+    monkeypatch.setenv("HCCL_AMD_IPC_LIGHT_FENCE", fence)
+    monkeypatch.setenv("HCCL_AMD_IPC_THREADS", threads)
+    monkeypatch.setenv("HCCL_AMD_IPC_STAGING_MIB", "16")
+    n = 4
+    comms = H.loopback_world(n)
+    try:
+        count = (5 << 20) + 3 if kind == AR else (3 << 20) + 7
+        in_count = count * n if kind == RS else count
+        xs = [O.random_operands(O.FP32, in_count, seed=970 + r, edge=False) for r in range(n)]
+        used, outs = collective(comms, kind, 7, O.FP32, O.SUM, xs, count)
+        assert used == 7
+        assert ipc_status(comms[0]) & 1 == 0
+        algo = R.ALGO_TWOSHOT if kind == AR else R.ALGO_IPC
+        want = R.expected(kind, algo, O.FP32, O.SUM, xs, count)
+        for r in range(n):
+            assert O.equal_bits(O.FP32, outs[r], want[r]), r
+    finally:
+        for c in comms:
+            c.destroy()
+
+
 @pytest.mark.parametrize("op_type,n,count", [(RS, 2, (17 << 20) + 5), (RS, 4, 3), (RED, 4, (36 << 20) + 7),
                                               (RED, 3, 5)])
 def test_ipc_reduce_scatter_and_reduce(worlds, op_type, n, count):

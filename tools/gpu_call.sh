@@ -21,6 +21,8 @@
 #   ipc_staging    one-sided kernel: uncached vs cached staging memory (A/B on one device)
 #   ipc_fence      one-sided kernel: system-scope vs light barrier fences x workgroups per rank (A/B)
 #   ipc_light_tests  the one-sided kernel's GPU tests with light barrier fences
+#   ipc_latency_fence  one-sided kernel latency, rank mode, system vs light fences
+#   phase_trace_variants  the phase trace with light fences and with cached staging
 #   phase_trace    per-block phase stamps of the one-sided two-shot kernel, loopback worlds n = 2, 4, 8
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
@@ -161,9 +163,29 @@ step_ipc_light_tests() {
     -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
 }
 
+# one-sided kernel latency in rank mode (two processes on the GPU), eager and from a graph, system vs light fences
+step_ipc_latency_fence() {
+  : > "$OUT/ipc_latency_fence.jsonl"
+  local port=29561 f
+  for f in 0 1 0 1; do
+    port=$((port + 1))
+    HCCL_AMD_IPC_LIGHT_FENCE=$f run "ipc_latency_fence_$port" 200 python3 -m torch.distributed.run --nnodes=1 \
+      --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $port tools/graph_latency.py --algo IPC \
+      --sizes 1024,65536,1048576,16777216 || return $?
+    grep '^{' "$OUT/ipc_latency_fence_$port.log" >> "$OUT/ipc_latency_fence.jsonl" || true
+  done
+}
+
 step_phase_trace() {
   run phase_trace 300 python3 -u tools/ipc_phase_trace.py
   grep '^{' "$OUT/phase_trace.log" > "$OUT/ipc_phase_trace.jsonl" || true
+}
+
+step_phase_trace_variants() {
+  HCCL_AMD_IPC_LIGHT_FENCE=1 run phase_trace_light 200 python3 -u tools/ipc_phase_trace.py
+  grep '^{' "$OUT/phase_trace_light.log" > "$OUT/ipc_phase_trace_light.jsonl" || true
+  HCCL_AMD_IPC_STAGING_CACHED=1 run phase_trace_cached 200 python3 -u tools/ipc_phase_trace.py
+  grep '^{' "$OUT/phase_trace_cached.log" > "$OUT/ipc_phase_trace_cached.jsonl" || true
 }
 
 step_counters() {

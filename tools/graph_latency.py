@@ -72,7 +72,8 @@ def main():
         if rank == 0:
             print(json.dumps({"algo": H.Algo(comm.last_algo).name, "n": world, "bytes": nbytes, "eager_us": round(float(t[0]) * 1e3, 2),
                               "graph_us": round(float(t[1]) * 1e3, 2), "ok": ok,
-                              "ipc_status_bit0": comm.ipc_status() & 1}), flush=True)
+                              "ipc_status_bit0": comm.ipc_status() & 1,
+                              "light_fence": os.environ.get("HCCL_AMD_IPC_LIGHT_FENCE", "0")}), flush=True)
         del g
     torch.cuda.synchronize()
     dist.barrier()
