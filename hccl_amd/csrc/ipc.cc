@@ -18,13 +18,13 @@ namespace hccl_amd {
 namespace {
 
 struct Exported {
-    hipIpcMemHandle_t stg;
+    hipIpcMemHandle_t area[kIpcAreas];
     hipIpcMemHandle_t flags;
     char busId[32];  // the rank's device: ranks that share one count against its resident blocks together
 };
 
 struct RawPtrs {
-    void* stg;
+    void* area[kIpcAreas];
     uint32_t* flags;
     uint8_t ok;
 };
@@ -65,9 +65,15 @@ HcclResult IpcSetup(Comm& c)
     const char* cachedEnv = std::getenv("HCCL_AMD_IPC_STAGING_CACHED");
     const bool cached = cachedEnv != nullptr && std::strcmp(cachedEnv, "1") == 0;
     s.cachedStaging = cached;
-    const size_t stgBytes = s.stgInBytes + s.stgResBytes + 2 * s.stgAltBytes;
-    bool ok = (cached ? hipMalloc(&s.stg, stgBytes) : hipExtMallocWithFlags(&s.stg, stgBytes, hipDeviceMallocUncached)) ==
-                  hipSuccess &&
+    // Four allocations, one per area, each below 2 GiB: hipIpcOpenMemHandle never returned for a 2 GiB allocation
+    // on this stack (the r03 512 MiB areas in one 2 GiB block hung the rank-mode set-up; tools/probe_ipc_open.py,
+    // profiles/r03_probe_ipc_open.jsonl: 128 MiB .. 1.5 GiB open in < 1 ms, 2 GiB does not return).
+    bool ok = true;
+    for (int k = 0; k < kIpcAreas && ok; ++k) {
+        ok = (cached ? hipMalloc(&s.area[k], area)
+                     : hipExtMallocWithFlags(&s.area[k], area, hipDeviceMallocUncached)) == hipSuccess;
+    }
+    ok = ok &&
               hipExtMallocWithFlags(reinterpret_cast<void**>(&s.flags), flagBytes, hipDeviceMallocUncached) ==
                   hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&s.status), kIpcStatusBytes) == hipSuccess &&
@@ -97,7 +103,7 @@ HcclResult IpcSetup(Comm& c)
         ok = ok && word != nullptr;
         // Every rank thread takes part in the exchange whatever its local outcome (a rank that returned early
         // would leave the others blocked in the rendezvous), and they all agree on the result.
-        RawPtrs mine{s.stg, s.flags, static_cast<uint8_t>(ok ? 1 : 0)};
+        RawPtrs mine{{s.area[0], s.area[1], s.area[2], s.area[3]}, s.flags, static_cast<uint8_t>(ok ? 1 : 0)};
         std::vector<RawPtrs> all(n);
         const HcclResult xr = c.transport->AllGatherHost(&mine, sizeof mine, all.data());
         for (uint32_t r = 0; r < n && xr == HCCL_SUCCESS; ++r) ok = ok && all[r].ok != 0;
@@ -107,7 +113,7 @@ HcclResult IpcSetup(Comm& c)
             return xr != HCCL_SUCCESS ? xr : HCCL_E_MEMORY;
         }
         for (uint32_t r = 0; r < n; ++r) {
-            s.peerStg[r] = all[r].stg;
+            for (int k = 0; k < kIpcAreas; ++k) s.peerArea[k][r] = all[r].area[k];
             s.peerFlags[r] = all[r].flags;
         }
         s.failDev = wdev;
@@ -117,8 +123,8 @@ HcclResult IpcSetup(Comm& c)
         // ranks have every peer mapped or all release and report NOT_SUPPORT (the caller then runs the RCCL
         // two-shot on every rank alike, never a mix of paths that would leave peers waiting).
         Exported mine{};
-        ok = ok && hipIpcGetMemHandle(&mine.stg, s.stg) == hipSuccess &&
-             hipIpcGetMemHandle(&mine.flags, s.flags) == hipSuccess &&
+        for (int k = 0; k < kIpcAreas && ok; ++k) ok = hipIpcGetMemHandle(&mine.area[k], s.area[k]) == hipSuccess;
+        ok = ok && hipIpcGetMemHandle(&mine.flags, s.flags) == hipSuccess &&
              hipDeviceGetPCIBusId(mine.busId, sizeof mine.busId - 1, c.device) == hipSuccess;
         std::vector<Exported> all(n);
         HcclResult xr = c.transport->AllGatherHost(&mine, sizeof mine, all.data());
@@ -139,15 +145,22 @@ HcclResult IpcSetup(Comm& c)
         }
         for (uint32_t r = 0; r < n && ok; ++r) {
             if (r == me) {
-                s.peerStg[r] = s.stg;
+                for (int k = 0; k < kIpcAreas; ++k) s.peerArea[k][r] = s.area[k];
                 s.peerFlags[r] = s.flags;
                 continue;
             }
+            // the peer's areas, then its flags; what opened is closed again if a later one fails
             void* f = nullptr;
-            hipError_t e = hipIpcOpenMemHandle(&s.peerStg[r], all[r].stg, hipIpcMemLazyEnablePeerAccess);
-            if (e == hipSuccess) {
-                e = hipIpcOpenMemHandle(&f, all[r].flags, hipIpcMemLazyEnablePeerAccess);
-                if (e != hipSuccess) (void)hipIpcCloseMemHandle(s.peerStg[r]);
+            int areas = 0;
+            hipError_t e = hipSuccess;
+            while (areas < kIpcAreas) {
+                e = hipIpcOpenMemHandle(&s.peerArea[areas][r], all[r].area[areas], hipIpcMemLazyEnablePeerAccess);
+                if (e != hipSuccess) break;
+                ++areas;
+            }
+            if (e == hipSuccess) e = hipIpcOpenMemHandle(&f, all[r].flags, hipIpcMemLazyEnablePeerAccess);
+            if (e != hipSuccess) {
+                for (int q = 0; q < areas; ++q) (void)hipIpcCloseMemHandle(s.peerArea[q][r]);
             }
             if (e != hipSuccess) {
                 HCCL_AMD_ERR("rank %u: hipIpcOpenMemHandle of rank %u failed: %s", me, r, hipGetErrorString(e));
@@ -264,12 +277,14 @@ void IpcRelease(Comm& c)
     IpcState& s = c.ipc;
     for (uint32_t r = 0; r < kIpcMaxRanks; ++r) {
         if (s.opened[r]) {
-            (void)hipIpcCloseMemHandle(s.peerStg[r]);
+            for (int k = 0; k < kIpcAreas; ++k) (void)hipIpcCloseMemHandle(s.peerArea[k][r]);
             (void)hipIpcCloseMemHandle(s.peerFlags[r]);
             s.opened[r] = false;
         }
     }
-    if (s.stg != nullptr) (void)hipFree(s.stg);
+    for (int k = 0; k < kIpcAreas; ++k) {
+        if (s.area[k] != nullptr) (void)hipFree(s.area[k]);
+    }
     if (s.flags != nullptr) (void)hipFree(s.flags);
     if (s.status != nullptr) (void)hipFree(s.status);
     if (s.trace != nullptr) (void)hipFree(s.trace);
@@ -300,7 +315,8 @@ uint64_t IpcStagingBytes()
     const char* e = std::getenv("HCCL_AMD_IPC_STAGING_MIB");
     if (e != nullptr && *e != '\0') {
         const unsigned long long v = std::strtoull(e, nullptr, 10);
-        if (v >= 16 && v <= 2048) return static_cast<uint64_t>(v) << 20;
+        // below 2 GiB: a 2 GiB allocation's IPC handle never opened (IpcSetup)
+        if (v >= 16 && v <= 1536) return static_cast<uint64_t>(v) << 20;
     }
     return kIpcStagingBytes;
 }
@@ -566,8 +582,10 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
 
     IpcArgs a{};
     for (uint32_t r = 0; r < n; ++r) {
-        a.stgIn[r] = s.peerStg[r];
-        a.stgRes[r] = static_cast<char*>(s.peerStg[r]) + s.stgInBytes;
+        a.stgIn[r] = s.peerArea[kIpcAreaIn][r];
+        a.stgRes[r] = s.peerArea[kIpcAreaRes][r];
+        a.stgAlt[0][r] = s.peerArea[kIpcAreaAlt0][r];
+        a.stgAlt[1][r] = s.peerArea[kIpcAreaAlt1][r];
         a.flags[r] = s.peerFlags[r];
     }
     a.n = n;
@@ -580,8 +598,6 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
     a.failHost = s.failDev;
     a.callSeq = ++s.callSeq;  // equal on every rank of a loopback world (each runs this once per call)
     a.outStride = count;
-    a.altOff = s.stgInBytes + s.stgResBytes;
-    a.altBytes = s.stgAltBytes;
     a.trace = s.trace;
     if (plan.order == kIpcRhd) {
         // the RHD schedule's parts and relabelling (AllReduceRhd): R instances over Chunk(count, R, j) parts

@@ -10,6 +10,13 @@
 namespace hccl_amd {
 
 constexpr int kIpcMaxRanks = 16;
+// Staging areas of a rank, each its own allocation (and IPC handle): slots, results, and the two alternate slot areas
+// of the single-barrier kinds.
+constexpr int kIpcAreas = 4;
+constexpr int kIpcAreaIn = 0;
+constexpr int kIpcAreaRes = 1;
+constexpr int kIpcAreaAlt0 = 2;
+constexpr int kIpcAreaAlt1 = 3;
 constexpr int kIpcBlock = 256;        // threads per workgroup of the one-sided kernel (default)
 constexpr int kIpcMaxThreads = 512;   // HCCL_AMD_IPC_THREADS may take 512 (r03 A/B)
 
@@ -86,13 +93,14 @@ __host__ __device__ constexpr bool SingleBarrierKind(uint32_t kind)
 // [k*piece, (k+1)*piece). Block b always handles piece coordinates [b*blockElems, (b+1)*blockElems), so every round
 // of a launch touches the same slot and result addresses per block and the per-block barrier is sound.
 // Staging: owner c's slot q = stgIn[c] + q*piece; results of chunk c at stgRes[p] + c*piece. The single-barrier kinds
-// (SingleBarrierKind) put their slots in one of two alternate areas instead, at stgIn[c] + altOff + (e & 1)*altBytes
-// for the round whose barrier has epoch e (see k_ipc_collective).
+// (SingleBarrierKind) put their slots in one of two alternate areas instead, stgAlt[e & 1][c] + q*piece for the round
+// whose barrier has epoch e (see k_ipc_collective).
 struct IpcArgs {
     const void* in[kIpcMaxRanks];
     void* out[kIpcMaxRanks];
     void* stgIn[kIpcMaxRanks];
     void* stgRes[kIpcMaxRanks];
+    void* stgAlt[2][kIpcMaxRanks];
     uint32_t* flags[kIpcMaxRanks];  // [blocks][n] per rank
     uint32_t n;
     int32_t me;
@@ -120,8 +128,6 @@ struct IpcArgs {
     uint32_t rounds;
     uint32_t epochSpan;  // barriers per block in this launch: the device epoch counter advances by this much
     uint64_t outStride;  // kIpcAllGather: elements between consecutive ranks' blocks of the output (sendCount)
-    uint64_t altOff;    // byte offset of the alternate slot areas from stgIn[c] (same layout on every rank)
-    uint64_t altBytes;  // bytes of one alternate area
     uint64_t timeoutTicks;  // per barrier wait, in s_memrealtime ticks (100 MHz)
     uint32_t* failHost;  // host-visible word (pinned, coherent): set to 1 by the block whose barrier times out, read by
                          // the host at every collective entry (Comm::Gate) and by HcclGetCommAsyncError
@@ -186,14 +192,14 @@ HcclResult ScrubL2(hipStream_t stream);
 struct IpcState {
     bool ready = false;
     bool unavailable = false;      // set-up failed on some rank: every later call reports NOT_SUPPORT
-    void* stg = nullptr;           // own staging, uncached: [in area][result area][alternate area 0][area 1]
+    void* area[kIpcAreas] = {};    // own staging areas, uncached (kIpcAreaIn, kIpcAreaRes, kIpcAreaAlt0, kIpcAreaAlt1)
     uint32_t* flags = nullptr;     // own flags, uncached, zeroed
     uint32_t* status = nullptr;    // device words: [0] bit 0 = barrier timeout, [2..3] = tagged longest wait (IpcArgs)
     uint32_t callSeq = 0;          // IPC calls issued on the communicator (tags the wait diagnostic)
     uint32_t* failHost = nullptr;  // pinned host word the kernel sets on a barrier timeout (hipHostMalloc, coherent)
     uint32_t* failDev = nullptr;   // the device address the launches write (IpcArgs::failHost): of failHost, or in a
                                    // loopback world of the world's word (Transport::SharedFailWord)
-    void* peerStg[kIpcMaxRanks] = {};
+    void* peerArea[kIpcAreas][kIpcMaxRanks] = {};
     uint32_t* peerFlags[kIpcMaxRanks] = {};
     bool opened[kIpcMaxRanks] = {};
     uint64_t stgInBytes = 0;
@@ -216,6 +222,6 @@ constexpr int kIpcDoneWord = 5;
 // round where 128 MiB areas took 2-4, 5-12 % faster at n = 2 and 4 (tools/ipc_variant_ab.py,
 // profiles/r03_ipc_variant_ab_{policy,shapes}.jsonl); each round costs two cross-rank barriers and three phase fills and drains.
 constexpr uint64_t kIpcStagingBytes = 512ull << 20;
-uint64_t IpcStagingBytes();  // HCCL_AMD_IPC_STAGING_MIB (16 .. 2048) or kIpcStagingBytes; equal on every rank
+uint64_t IpcStagingBytes();  // HCCL_AMD_IPC_STAGING_MIB (16 .. 1536) or kIpcStagingBytes; equal on every rank
 
 }  // namespace hccl_amd

@@ -550,8 +550,7 @@ __global__ __launch_bounds__(kIpcMaxThreads) void k_ipc_collective(IpcArgs a)
     // later two-shot call never stores over a fold that runs after the last barrier.
     const bool single = SingleBarrierKind(kind);
     auto slotArea = [&](uint32_t c, uint32_t e) -> char* {
-        char* base = static_cast<char*>(a.stgIn[c]);
-        return single ? base + a.altOff + (e & 1u) * a.altBytes : base;
+        return static_cast<char*>(single ? a.stgAlt[e & 1u][c] : a.stgIn[c]);
     };
     // Epochs come from the device counter (Arrive / EndLaunch), so the next launch in stream order, a call or a graph
     // replay alike, starts where this one ended. Every rank runs the same launch sequence, so the counters agree.

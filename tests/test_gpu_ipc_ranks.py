@@ -316,3 +316,71 @@ def test_ipc_lost_peer_fails_the_communicator():
     assert r0["rs_rc"] == H.HcclResult.HCCL_E_SUSPENDING, r0
     assert r0["async_later"] == H.HcclResult.HCCL_E_TIMEOUT, r0
     assert r0["after_s"] < 1.0, r0  # the gate enqueues nothing
+
+
+def _default_staging_main(rank, n, port, q):
+    # the default staging (four 512 MiB areas per rank, each its own allocation and handle): in r03 the areas were
+    # one 2 GiB allocation, whose handle hipIpcOpenMemHandle never opened, so the rank-mode set-up hung
+    os.environ.pop("HCCL_AMD_IPC_STAGING_MIB", None)
+    os.environ["HCCL_AMD_IPC_TIMEOUT_MS"] = "20000"
+    try:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n,
+                                timeout=datetime.timedelta(seconds=120))
+        torch.cuda.set_device(0)
+        import hccl_amd as H
+
+        def all_gather(b):
+            out = [None] * n
+            dist.all_gather_object(out, b)
+            return out
+
+        comm = H.comm_init_host_exchange(n, rank, all_gather)
+        comm.set_algo(H.Algo.IPC_TWOSHOT)
+        s = torch.cuda.Stream()
+        res = []
+        for count in (1025, (300 << 20) // 4 + 3):  # one staging round, and one 300 MiB call
+            x = torch.arange(count, device="cuda", dtype=torch.int32) % 1000 + rank
+            y = torch.empty_like(x)
+            torch.cuda.synchronize()  # x was made on the current stream; the collective runs on s
+            comm.all_reduce(x, y, H.HcclReduceOp.SUM, s)
+            s.synchronize()
+            want = (torch.arange(count, device="cuda", dtype=torch.int32) % 1000) * n + n * (n - 1) // 2
+            bad = (y != want).nonzero()
+            res.append((H.Algo(comm.last_algo).name, bad.numel() == 0, comm.ipc_status() & 1))
+            if bad.numel():
+                res.append(("mismatches", int(bad.numel()), int(bad[0]), int(bad[-1]), count))
+        dist.barrier()
+        comm.destroy()
+        dist.destroy_process_group()
+        q.put((rank, "ok", res))
+    except Exception:  # noqa: BLE001
+        q.put((rank, traceback.format_exc(), None))
+        time.sleep(10)
+
+
+@pytest.mark.timeout(200)
+def test_ipc_rank_mode_default_staging():
+    """Rank mode with the default staging areas (no HCCL_AMD_IPC_STAGING_MIB): the set-up opens every peer's four
+    area handles and the two-shot AllReduce is exact, without a barrier timeout."""
+    n = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_default_staging_main, args=(r, n, port, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    try:
+        got = {}
+        for _ in procs:
+            rank, msg, res = q.get(timeout=150)
+            got[rank] = (msg, res)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(n):
+        assert got[r][0] == "ok", f"rank {r}:\n{got[r][0]}"
+        assert got[r][1] == [("IPC_TWOSHOT", True, 0)] * 2, got[r][1]

@@ -8,6 +8,8 @@ import json
 import os
 import sys
 
+import time
+
 import torch
 import torch.distributed as dist
 
@@ -15,6 +17,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import hccl_amd as H  # noqa: E402
 
 K = 100
+T0 = time.time()
+
+
+def progress(rank, what):
+    print(f"[graph_latency] rank {rank} +{time.time() - T0:.1f}s {what}", file=sys.stderr, flush=True)
 
 
 def main():
@@ -32,15 +39,23 @@ def main():
         dist.all_gather_object(out, b)
         return out
 
+    progress(rank, "process group up")
     comm = H.comm_init_host_exchange(world, rank, all_gather)
+    progress(rank, "communicator up")
     comm.set_algo(H.Algo[args.algo])
     s = torch.cuda.Stream()
     for nbytes in [int(v) for v in args.sizes.split(",")]:
         x = torch.ones(nbytes // 2, dtype=torch.float16, device="cuda")
         y = torch.empty_like(x)
-        for _ in range(10):
+        torch.cuda.synchronize()  # x is made on the current stream; the collectives run on s
+        for i in range(10):
             comm.all_reduce(x, y, H.HcclReduceOp.SUM, s)
+            if i == 0:
+                progress(rank, f"{nbytes} B: first call enqueued ({H.Algo(comm.last_algo).name})")
+                s.synchronize()
+                progress(rank, f"{nbytes} B: first call done, ipc status {comm.ipc_status()}")
         torch.cuda.synchronize()
+        progress(rank, f"{nbytes} B: warm")
         dist.barrier()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
@@ -49,14 +64,17 @@ def main():
         e1.record(s)
         torch.cuda.synchronize()
         eager = e0.elapsed_time(e1) / K
+        progress(rank, f"{nbytes} B: eager timed")
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=torch.cuda.Stream()):
             cs = torch.cuda.current_stream()
             for _ in range(K):
                 comm.all_reduce(x, y, H.HcclReduceOp.SUM, cs)
         torch.cuda.synchronize()
+        progress(rank, f"{nbytes} B: captured")
         g.replay()
         torch.cuda.synchronize()
+        progress(rank, f"{nbytes} B: replayed once")
         dist.barrier()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         cur = torch.cuda.current_stream()
