@@ -200,22 +200,16 @@ uint64_t IpcTileBytes()
     return std::strtoull(e, nullptr, 10) << 10;
 }
 
-// HCCL_AMD_IPC_COPY_U / HCCL_AMD_IPC_FOLD_U: vectors per lane in flight in the copy and fold loops (2, 4 or 8; r03 A/B,
-// tools/ipc_variant_ab.py). Read per call, equal on every rank.
-uint32_t IpcUnroll(const char* name, uint32_t dflt)
-{
-    const char* e = std::getenv(name);
-    if (e == nullptr || *e == '\0') return dflt;
-    const unsigned long v = std::strtoul(e, nullptr, 10);
-    return (v == 2 || v == 4 || v == 8) ? static_cast<uint32_t>(v) : dflt;
-}
-
-// HCCL_AMD_IPC_LIGHT_FENCE=1: barriers without the XCD-wide L2 write-back and invalidate (IpcArgs::fence; r03 A/B).
-// Read per call, equal on every rank.
+// Barrier fences (IpcArgs::fence). Every byte a barrier hands over lives in uncached staging, which no L2 holds: a
+// store's vmcnt drain is its release, and the reader's loads go to memory. So by default the barriers skip the
+// system-scope release and acquire, which write back and invalidate the whole XCD's L2 for every block and stall the
+// blocks still streaming there (r03: 3-13 % per call in loopback worlds, profiles/r03_ipc_variant_ab_fence.jsonl;
+// the IPC GPU tests, rank mode and stress included, bit-exact with them). HCCL_AMD_IPC_LIGHT_FENCE=0 restores the
+// system-scope fences. Read per call, equal on every rank.
 bool IpcLightFence()
 {
     const char* e = std::getenv("HCCL_AMD_IPC_LIGHT_FENCE");
-    return e != nullptr && std::strcmp(e, "1") == 0;
+    return e == nullptr || std::strcmp(e, "0") != 0;
 }
 
 // HCCL_AMD_IPC_THREADS: threads per workgroup, 256 (default) or 512 (r03 A/B). Read per call, equal on every rank.
@@ -685,8 +679,6 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
         g.blockElems = ((g.piece + s.blocks - 1) / s.blocks + V - 1) / V * V;
         g.tileElems = IpcTileBytes() / es / V * V;  // 0: contiguous windows
         g.nt = IpcNonTemporal() ? 1u : 0u;
-        g.copyU = IpcUnroll("HCCL_AMD_IPC_COPY_U", 4);
-        g.foldU = IpcUnroll("HCCL_AMD_IPC_FOLD_U", 4);
         g.fence = (IpcLightFence() && !s.cachedStaging) ? 1u : 0u;
         g.threads = IpcThreads();
         g.rounds = static_cast<uint32_t>((widest + g.piece - 1) / g.piece);

@@ -120,11 +120,10 @@ struct IpcArgs {
     uint64_t tileElems;  // 0: block b's share of a piece is one window of blockElems; else tiles of tileElems at
                          // b, b + B, b + 2B, ... (B = blocks): the same piece coordinates in every round either way
     uint32_t nt;         // non-temporal loads and stores in the copy and fold loops
-    uint32_t copyU;      // vectors per lane in flight in the copy loops (2, 4, 8)
-    uint32_t foldU;      // vectors per lane and operand in flight in the fold loop (2, 4, 8)
     uint32_t threads;    // threads per workgroup (kIpcBlock, or 512 by HCCL_AMD_IPC_THREADS)
-    uint32_t fence;      // barrier fences: 0 = system-scope release (L2 write-back) and acquire (L2 invalidate);
-                         // 1 = light: the drains alone release, an agent-scope acquire (L1) (uncached staging only)
+    uint32_t fence;      // barrier fences: 1 = light (default): the waves' drains release the uncached staging, an
+                         // agent-scope acquire (L1); 0 = system-scope release (XCD-wide L2 write-back) and acquire
+                         // (L2 invalidate), forced for cached staging
     uint32_t rounds;
     uint32_t epochSpan;  // barriers per block in this launch: the device epoch counter advances by this much
     uint64_t outStride;  // kIpcAllGather: elements between consecutive ranks' blocks of the output (sendCount)

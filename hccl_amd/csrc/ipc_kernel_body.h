@@ -24,8 +24,10 @@
 // Every round of one launch has the same geometry (the host launches a shorter last round separately), so block b
 // of every rank touches the same slot and result addresses in every round and only waits for block b of its peers;
 // nothing in a GPU waits for another block of the same GPU. Every storing wave drains (s_waitcnt vmcnt(0)) before the
-// workgroup barrier, one wave then releases at system scope (L2 write-back) and stores the flags with system-scope
-// release stores; flags are polled with system-scope relaxed loads and followed by an acquire. Every wait is bounded
+// workgroup barrier; since every handed-over byte is in uncached staging that drain is the release (IpcArgs::fence 1,
+// the default; fence 0 adds the system-scope L2 write-back), and one wave stores the flags with system-scope stores;
+// flags are polled with system-scope relaxed loads and followed by an acquire (agent scope: the CU's L1; fence 0:
+// system scope). Every wait is bounded
 // in wall time (s_memrealtime, HCCL_AMD_IPC_TIMEOUT_MS): on timeout the kernel sets status bit 0 and finishes (wrong
 // data, never a hang); the bit is sticky for the communicator, so later launches return at once. World mode (me < 0) runs all
 // n ranks of a loopback world as blockIdx.y of one launch on one GPU, which is how the protocol is tested without a
@@ -220,36 +222,25 @@ __device__ __forceinline__ void ForBlockShare(const IpcArgs& a, uint64_t len, F&
     for (uint64_t lo = uint64_t(blockIdx.x) * a.tileElems; lo < len; lo += step) f(Range{lo, min(len, lo + a.tileElems)});
 }
 
-template <int NT, int U>
+constexpr int kIpcU = 4;  // vectors per lane in flight (r03 A/B of 2, 4, 8: profiles/r03_ipc_variant_ab_unroll.jsonl)
+
+template <int NT>
 __device__ __forceinline__ void CopyVecs(u32x4* d, const u32x4* s, uint64_t& v, uint64_t vhi)
 {
-    for (; v + (U - 1) * blockDim.x < vhi; v += U * blockDim.x) {
-        u32x4 x[U];
+    for (; v + (kIpcU - 1) * blockDim.x < vhi; v += kIpcU * blockDim.x) {
+        u32x4 x[kIpcU];
 #pragma unroll
-        for (int u = 0; u < U; ++u) x[u] = ld<NT>(s + v + u * blockDim.x);
+        for (int u = 0; u < kIpcU; ++u) x[u] = ld<NT>(s + v + u * blockDim.x);
 #pragma unroll
-        for (int u = 0; u < U; ++u) st<NT>(d + v + u * blockDim.x, x[u]);
+        for (int u = 0; u < kIpcU; ++u) st<NT>(d + v + u * blockDim.x, x[u]);
     }
     for (; v < vhi; v += blockDim.x) st<NT>(d + v, ld<NT>(s + v));
-}
-
-// Runtime unroll of the copy and fold loops (IpcArgs::copyU / foldU: 2, 4 or 8 vectors per lane in flight; r03 A/B)
-template <class F>
-__device__ __forceinline__ void WithU(uint32_t u, F&& f)
-{
-    if (u == 2) {
-        f(std::integral_constant<int, 2>{});
-    } else if (u == 8) {
-        f(std::integral_constant<int, 8>{});
-    } else {
-        f(std::integral_constant<int, 4>{});
-    }
 }
 
 // dst[e] = src[e] for e in r. vec = both pointers are 16-B aligned; otherwise every element goes through the scalar
 // loop. nt: non-temporal loads and stores (IpcArgs::nt).
 template <typename S>
-__device__ __forceinline__ void CopyRange(S* dst, const S* src, Range r, bool vec, bool nt, uint32_t cu)
+__device__ __forceinline__ void CopyRange(S* dst, const S* src, Range r, bool vec, bool nt)
 {
     constexpr uint64_t V = 16 / sizeof(S);
     // r.lo is vector aligned unless the window is empty at the end of a piece (lo = hi = len); r.hi may be anything
@@ -257,14 +248,11 @@ __device__ __forceinline__ void CopyRange(S* dst, const S* src, Range r, bool ve
     const u32x4* s = reinterpret_cast<const u32x4*>(src);
     u32x4* d = reinterpret_cast<u32x4*>(dst);
     uint64_t v = vlo + threadIdx.x;
-    WithU(cu, [&](auto uTag) {
-        constexpr int U = decltype(uTag)::value;
-        if (nt) {
-            CopyVecs<3, U>(d, s, v, vhi);
-        } else {
-            CopyVecs<0, U>(d, s, v, vhi);
-        }
-    });
+    if (nt) {
+        CopyVecs<3>(d, s, v, vhi);
+    } else {
+        CopyVecs<0>(d, s, v, vhi);
+    }
     for (uint64_t e = max(vhi * V, r.lo) + threadIdx.x; e < r.hi; e += blockDim.x) dst[e] = src[e];
 }
 
@@ -430,9 +418,9 @@ __device__ __forceinline__ void FoldSeg(const IpcArgs& a, uint32_t me, uint32_t 
     }
     scalar(r.lo, vb * V);
     uint64_t v = vb + threadIdx.x;
-    auto body = [&](auto ntTag, auto uTag) {
+    auto body = [&](auto ntTag) {
         constexpr int NT = decltype(ntTag)::value;
-        constexpr int U = decltype(uTag)::value;
+        constexpr int U = kIpcU;
         for (; v + (U - 1) * blockDim.x < ve; v += U * blockDim.x) {
             u32x4 acc[U];
 #pragma unroll
@@ -450,13 +438,11 @@ __device__ __forceinline__ void FoldSeg(const IpcArgs& a, uint32_t me, uint32_t 
             }
         }
     };
-    WithU(a.foldU, [&](auto uTag) {
-        if (a.nt != 0) {
-            body(std::integral_constant<int, 3>{}, uTag);
-        } else {
-            body(std::integral_constant<int, 0>{}, uTag);
-        }
-    });
+    if (a.nt != 0) {
+        body(std::integral_constant<int, 3>{});
+    } else {
+        body(std::integral_constant<int, 0>{});
+    }
     for (; v < ve; v += blockDim.x) {
         u32x4 acc = reinterpret_cast<const u32x4*>(src(0))[v];
         for (uint32_t i = 1; i < n; ++i) acc = combine<E, OP>(reinterpret_cast<const u32x4*>(src(i))[v], acc);
@@ -570,7 +556,7 @@ __global__ __launch_bounds__(kIpcMaxThreads) void k_ipc_collective(IpcArgs a)
             if (kind == kIpcReduceOneShot && c != a.root) continue;
             S* slot = reinterpret_cast<S*>(slotArea(c, epoch + 1)) + uint64_t(me) * a.piece;
             ForBlockShare(a, PieceLen(a, c, kP), [&](Range r) {
-                CopyRange<S>(slot, in + ChunkStart(a, c) + kP, r, ChunkVec<S>(a, c), a.nt != 0, a.copyU);
+                CopyRange<S>(slot, in + ChunkStart(a, c) + kP, r, ChunkVec<S>(a, c), a.nt != 0);
             });
         }
         Stamp(a, me, kTrPhase0);
@@ -585,7 +571,7 @@ __global__ __launch_bounds__(kIpcMaxThreads) void k_ipc_collective(IpcArgs a)
                     const S* src = q == me ? in + kP : slots + uint64_t(q) * a.piece;
                     S* dst = out + uint64_t(q) * a.outStride + kP;
                     if (src != dst) {
-                        CopyRange<S>(dst, src, r, a.aligned && (uint64_t(q) * a.outStride) % V == 0, a.nt != 0, a.copyU);
+                        CopyRange<S>(dst, src, r, a.aligned && (uint64_t(q) * a.outStride) % V == 0, a.nt != 0);
                     }
                 }
             });
@@ -621,7 +607,7 @@ __global__ __launch_bounds__(kIpcMaxThreads) void k_ipc_collective(IpcArgs a)
                 ForBlockShare(a, PieceLen(a, c, kP), [&](Range r) {
                     CopyRange<S>(out + ChunkStart(a, c) + kP,
                                  static_cast<const S*>(a.stgRes[me]) + uint64_t(c) * a.piece, r, ChunkVec<S>(a, c),
-                                 a.nt != 0, a.copyU);
+                                 a.nt != 0);
                 });
             }
         }

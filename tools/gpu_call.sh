@@ -17,10 +17,9 @@
 #   ipc_ab         one-sided kernel: block shares (contiguous / tiles) x cache policy A/B, loopback world
 #   harness        bench.py's N > 1 code path with two ranks sharing the GPU (IPC-only; a crash check, not a result)
 #   counters       the TCC counters this rocprofv3 offers
-#   ipc_unroll     one-sided kernel: vectors in flight of the copy and fold loops x workgroups per rank (A/B)
 #   ipc_staging    one-sided kernel: uncached vs cached staging memory (A/B on one device)
 #   ipc_fence      one-sided kernel: system-scope vs light barrier fences x workgroups per rank (A/B)
-#   ipc_light_tests  the one-sided kernel's GPU tests with light barrier fences
+#   ipc_system_fence_tests  the one-sided kernel's GPU tests with the system-scope barrier fences
 #   ipc_latency_fence  one-sided kernel latency, rank mode, system vs light fences
 #   phase_trace_variants  the phase trace with light fences and with cached staging
 #   phase_trace    per-block phase stamps of the one-sided two-shot kernel, loopback worlds n = 2, 4, 8
@@ -140,11 +139,6 @@ step_ipc_ab() {
   grep '^{' "$OUT/ipc_ab.log" > "$OUT/ipc_variant_ab.jsonl" || true
 }
 
-step_ipc_unroll() {
-  AB_SWEEP=unroll run ipc_unroll 400 python3 -u tools/ipc_variant_ab.py
-  grep '^{' "$OUT/ipc_unroll.log" > "$OUT/ipc_variant_ab_unroll.jsonl" || true
-}
-
 step_ipc_staging() {
   AB_SWEEP=staging run ipc_staging 400 python3 -u tools/ipc_variant_ab.py
   grep '^{' "$OUT/ipc_staging.log" > "$OUT/ipc_variant_ab_staging.jsonl" || true
@@ -155,10 +149,10 @@ step_ipc_fence() {
   grep '^{' "$OUT/ipc_fence.log" > "$OUT/ipc_variant_ab_fence.jsonl" || true
 }
 
-# every one-sided-kernel GPU test with the light barrier fences (HCCL_AMD_IPC_LIGHT_FENCE=1; the rank-mode children
-# inherit it): loopback worlds of every kind and family, rank mode, the random call-sequence stress
-step_ipc_light_tests() {
-  HCCL_AMD_IPC_LIGHT_FENCE=1 HCCL_AMD_RANDOM_DRAWS=1000 run ipc_light_tests 600 python3 -u -m pytest \
+# every one-sided-kernel GPU test with the system-scope barrier fences (HCCL_AMD_IPC_LIGHT_FENCE=0; the rank-mode
+# children inherit it; light fences are the default since r03): loopback worlds, rank mode, the random stress
+step_ipc_system_fence_tests() {
+  HCCL_AMD_IPC_LIGHT_FENCE=0 HCCL_AMD_RANDOM_DRAWS=1000 run ipc_system_fence_tests 600 python3 -u -m pytest \
     tests/test_gpu_ipc_ranks.py tests/test_gpu_ipc_stress.py tests/test_gpu_collectives.py -m gpu -k "ipc or IPC or aiv or AIV" \
     -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
 }

@@ -5,8 +5,10 @@ SUM. Variants are interleaved over rounds; per variant the median per-call time 
 world's launch stream) and its algorithmic rate (n x 2(3n-2)/n x bytes per rank per launch). Every variant's output
 is compared bit for bit with the first variant's.
   python tools/ipc_variant_ab.py > gpurun_out/ipc_variant_ab.jsonl
-AB_SWEEP = shapes (default: staging size x workgroups per rank), policy (tiles x nt), unroll (vectors in flight),
-staging (uncached vs cached staging memory, one device), fence (barrier fences x workgroups).
+AB_SWEEP = shapes (default: staging size x workgroups per rank), policy (tiles x nt),
+staging (uncached vs cached staging memory, one device), fence (barrier fences x workgroups x threads).
+The r03 unroll sweep (profiles/r03_ipc_variant_ab_unroll.jsonl) found the fixed 4 vectors in flight best; its
+knobs are gone.
 """
 import json
 import os
@@ -261,67 +263,6 @@ def run_fence(n, mib, algo=H.Algo.IPC_TWOSHOT):
                           "barrier_timeouts": status}), flush=True)
 
 
-# third sweep (AB_SWEEP=unroll): (copy U, fold U, workgroups per rank), nt on, contiguous windows, one world
-UNROLLS = [(4, 4, 128), (4, 2, 128), (8, 4, 128), (8, 2, 128), (2, 2, 256), (4, 2, 256), (4, 4, 256), (8, 8, 128)]
-
-
-def run_unroll(n, mib, algo=H.Algo.IPC_TWOSHOT):
-    """HCCL_AMD_IPC_COPY_U x HCCL_AMD_IPC_FOLD_U x workgroups per rank, interleaved over rounds on one world."""
-    dev = torch.device("cuda", 0)
-    comms = H.loopback_world(n)
-    for c in comms:
-        c.set_algo(algo)
-    count = (mib << 20) // 4
-    g = torch.Generator(device=dev).manual_seed(41 + n)
-    xs = [torch.rand(count, device=dev, generator=g) for _ in range(n)]
-    ys = [torch.empty_like(x) for x in xs]
-    streams = [torch.cuda.Stream() for _ in range(n)]
-    pool = ThreadPoolExecutor(n)
-    os.environ["HCCL_AMD_IPC_TILE_KIB"] = "0"
-    os.environ["HCCL_AMD_IPC_NT"] = "1"
-
-    def call():
-        list(pool.map(lambda r: comms[r].all_reduce(xs[r], ys[r], H.HcclReduceOp.SUM, streams[r]), range(n)))
-
-    times = {v: [] for v in UNROLLS}
-    ok = {v: True for v in UNROLLS}
-    ref = None
-    for rnd in range(ROUNDS):
-        order = UNROLLS[rnd % len(UNROLLS):] + UNROLLS[:rnd % len(UNROLLS)]
-        for v in order:
-            os.environ["HCCL_AMD_IPC_COPY_U"] = str(v[0])
-            os.environ["HCCL_AMD_IPC_FOLD_U"] = str(v[1])
-            for c in comms:
-                c.set_ipc_blocks(v[2])
-            call()
-            torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(streams[0])
-            for _ in range(CALLS):
-                call()
-            e1.record(streams[0])
-            torch.cuda.synchronize()
-            times[v].append(e0.elapsed_time(e1) * 1e3 / CALLS)
-            if ref is None:
-                ref = [y.clone() for y in ys]
-            else:
-                ok[v] = ok[v] and all(bool(torch.equal(a, b)) for a, b in zip(ys, ref))
-    status = comms[0].ipc_status() & 1
-    pool.shutdown()
-    for c in comms:
-        c.destroy()
-    for k in ("HCCL_AMD_IPC_COPY_U", "HCCL_AMD_IPC_FOLD_U"):
-        os.environ.pop(k)
-    alg = n * 2 * (3 * n - 2) * count * 4 // n
-    for v in UNROLLS:
-        med = float(np.median(times[v]))
-        print(json.dumps({"ranks": n, "mib_per_rank": mib, "algo": algo.name, "copy_u": v[0], "fold_u": v[1],
-                          "blocks_per_rank": v[2], "median_us": round(med, 1), "min_us": round(min(times[v]), 1),
-                          "max_us": round(max(times[v]), 1), "TBps": round(alg / med / 1e6, 3),
-                          "frac": round(alg / med / 1e6 / 8.0, 4), "same_bits": ok[v],
-                          "barrier_timeouts": status}), flush=True)
-
-
 def main():
     torch.cuda.set_device(0)
     os.environ.setdefault("HCCL_AMD_IPC_TIMEOUT_MS", "20000")
@@ -331,9 +272,6 @@ def main():
     elif os.environ.get("AB_SWEEP") == "staging":
         for n, mib in ((2, 512), (4, 256)):
             run_staging(n, mib)
-    elif os.environ.get("AB_SWEEP") == "unroll":
-        for n, mib in ((2, 512), (4, 256)):
-            run_unroll(n, mib)
     elif os.environ.get("AB_SWEEP", "shapes") == "policy":
         for n, mib in ((2, 512), (4, 256), (8, 128)):
             run(n, mib)
