@@ -18,13 +18,13 @@ namespace hccl_amd {
 namespace {
 
 struct Exported {
-    hipIpcMemHandle_t area[kIpcAreas];
+    hipIpcMemHandle_t stg;
     hipIpcMemHandle_t flags;
     char busId[32];  // the rank's device: ranks that share one count against its resident blocks together
 };
 
 struct RawPtrs {
-    void* area[kIpcAreas];
+    void* stg;
     uint32_t* flags;
     uint8_t ok;
 };
@@ -45,6 +45,16 @@ bool IpcTraceEnabled()
     return e != nullptr && std::strcmp(e, "1") == 0;
 }
 
+// The four areas inside one staging allocation at base (every rank has the same layout).
+void AreasOf(const IpcState& s, void* base, void* areas[kIpcAreas])
+{
+    char* b = static_cast<char*>(base);
+    areas[kIpcAreaIn] = b;
+    areas[kIpcAreaRes] = b + s.stgInBytes;
+    areas[kIpcAreaAlt0] = b + s.stgInBytes + s.stgResBytes;
+    areas[kIpcAreaAlt1] = b + s.stgInBytes + s.stgResBytes + s.stgAltBytes;
+}
+
 HcclResult IpcSetup(Comm& c)
 {
     IpcState& s = c.ipc;
@@ -55,7 +65,9 @@ HcclResult IpcSetup(Comm& c)
     const uint64_t area = IpcStagingBytes();
     s.stgInBytes = area;
     s.stgResBytes = area;  // results of a whole round, in round coordinates
-    s.stgAltBytes = area;  // slots of the single-barrier kinds, two areas used alternately
+    // slots of the single-barrier kinds, two areas used alternately: as large as the others, within the one
+    // allocation's bound below (the default 512 MiB areas leave them 511.5 MiB)
+    s.stgAltBytes = std::min<uint64_t>(area, (kIpcStagingMaxBytes - 2 * area) / 2 / (64ull << 10) * (64ull << 10));
     const size_t flagBytes = size_t(kIpcMaxBlocks) * kIpcMaxRanks * sizeof(uint32_t);
     // The fresh uncached pages may carry lines of a freed cached buffer in some XCD's L2: scrub the L2s before the
     // flags are zeroed (ScrubL2), so that no stale line is ever read or written back over them.
@@ -65,14 +77,17 @@ HcclResult IpcSetup(Comm& c)
     const char* cachedEnv = std::getenv("HCCL_AMD_IPC_STAGING_CACHED");
     const bool cached = cachedEnv != nullptr && std::strcmp(cachedEnv, "1") == 0;
     s.cachedStaging = cached;
-    // Four allocations, one per area, each below 2 GiB: hipIpcOpenMemHandle never returned for a 2 GiB allocation
-    // on this stack (the r03 512 MiB areas in one 2 GiB block hung the rank-mode set-up; tools/probe_ipc_open.py,
-    // profiles/r03_probe_ipc_open.jsonl: 128 MiB .. 1.5 GiB open in < 1 ms, 2 GiB does not return).
-    bool ok = true;
-    for (int k = 0; k < kIpcAreas && ok; ++k) {
-        ok = (cached ? hipMalloc(&s.area[k], area)
-                     : hipExtMallocWithFlags(&s.area[k], area, hipDeviceMallocUncached)) == hipSuccess;
-    }
+    // One allocation [in][results][alternate 0][alternate 1], below 2 GiB: hipIpcOpenMemHandle never returned for a
+    // 2 GiB allocation on this stack (the r03 512 MiB areas in one 2 GiB block hung the rank-mode set-up;
+    // tools/probe_ipc_open.py, profiles/r03_probe_ipc_open*.jsonl: up to 2047 MiB opens in < 1 ms and is written
+    // through whole, 2048 MiB does not return). Four allocations of one area each set up fine but changed which pages a
+    // later executor run reused, and the GPU suite's 4-rank loopback run after an IPC call then read stale 128-B lines
+    // (DESIGN.md §5b); the one block keeps the layout every earlier round ran.
+    const uint64_t stgBytes = s.stgInBytes + s.stgResBytes + 2 * s.stgAltBytes;
+    void* base = nullptr;
+    bool ok = (cached ? hipMalloc(&base, stgBytes) : hipExtMallocWithFlags(&base, stgBytes, hipDeviceMallocUncached)) ==
+              hipSuccess;
+    if (ok) AreasOf(s, base, s.area);
     ok = ok &&
               hipExtMallocWithFlags(reinterpret_cast<void**>(&s.flags), flagBytes, hipDeviceMallocUncached) ==
                   hipSuccess &&
@@ -103,7 +118,7 @@ HcclResult IpcSetup(Comm& c)
         ok = ok && word != nullptr;
         // Every rank thread takes part in the exchange whatever its local outcome (a rank that returned early
         // would leave the others blocked in the rendezvous), and they all agree on the result.
-        RawPtrs mine{{s.area[0], s.area[1], s.area[2], s.area[3]}, s.flags, static_cast<uint8_t>(ok ? 1 : 0)};
+        RawPtrs mine{s.area[0], s.flags, static_cast<uint8_t>(ok ? 1 : 0)};
         std::vector<RawPtrs> all(n);
         const HcclResult xr = c.transport->AllGatherHost(&mine, sizeof mine, all.data());
         for (uint32_t r = 0; r < n && xr == HCCL_SUCCESS; ++r) ok = ok && all[r].ok != 0;
@@ -113,7 +128,9 @@ HcclResult IpcSetup(Comm& c)
             return xr != HCCL_SUCCESS ? xr : HCCL_E_MEMORY;
         }
         for (uint32_t r = 0; r < n; ++r) {
-            for (int k = 0; k < kIpcAreas; ++k) s.peerArea[k][r] = all[r].area[k];
+            void* areas[kIpcAreas];
+            AreasOf(s, all[r].stg, areas);
+            for (int k = 0; k < kIpcAreas; ++k) s.peerArea[k][r] = areas[k];
             s.peerFlags[r] = all[r].flags;
         }
         s.failDev = wdev;
@@ -123,8 +140,8 @@ HcclResult IpcSetup(Comm& c)
         // ranks have every peer mapped or all release and report NOT_SUPPORT (the caller then runs the RCCL
         // two-shot on every rank alike, never a mix of paths that would leave peers waiting).
         Exported mine{};
-        for (int k = 0; k < kIpcAreas && ok; ++k) ok = hipIpcGetMemHandle(&mine.area[k], s.area[k]) == hipSuccess;
-        ok = ok && hipIpcGetMemHandle(&mine.flags, s.flags) == hipSuccess &&
+        ok = ok && hipIpcGetMemHandle(&mine.stg, s.area[0]) == hipSuccess &&
+             hipIpcGetMemHandle(&mine.flags, s.flags) == hipSuccess &&
              hipDeviceGetPCIBusId(mine.busId, sizeof mine.busId - 1, c.device) == hipSuccess;
         std::vector<Exported> all(n);
         HcclResult xr = c.transport->AllGatherHost(&mine, sizeof mine, all.data());
@@ -149,18 +166,18 @@ HcclResult IpcSetup(Comm& c)
                 s.peerFlags[r] = s.flags;
                 continue;
             }
-            // the peer's areas, then its flags; what opened is closed again if a later one fails
+            // the peer's staging, then its flags; the staging is closed again if the flags fail
             void* f = nullptr;
-            int areas = 0;
-            hipError_t e = hipSuccess;
-            while (areas < kIpcAreas) {
-                e = hipIpcOpenMemHandle(&s.peerArea[areas][r], all[r].area[areas], hipIpcMemLazyEnablePeerAccess);
-                if (e != hipSuccess) break;
-                ++areas;
+            void* peer = nullptr;
+            hipError_t e = hipIpcOpenMemHandle(&peer, all[r].stg, hipIpcMemLazyEnablePeerAccess);
+            if (e == hipSuccess) {
+                e = hipIpcOpenMemHandle(&f, all[r].flags, hipIpcMemLazyEnablePeerAccess);
+                if (e != hipSuccess) (void)hipIpcCloseMemHandle(peer);
             }
-            if (e == hipSuccess) e = hipIpcOpenMemHandle(&f, all[r].flags, hipIpcMemLazyEnablePeerAccess);
-            if (e != hipSuccess) {
-                for (int q = 0; q < areas; ++q) (void)hipIpcCloseMemHandle(s.peerArea[q][r]);
+            if (e == hipSuccess) {
+                void* areas[kIpcAreas];
+                AreasOf(s, peer, areas);
+                for (int k = 0; k < kIpcAreas; ++k) s.peerArea[k][r] = areas[k];
             }
             if (e != hipSuccess) {
                 HCCL_AMD_ERR("rank %u: hipIpcOpenMemHandle of rank %u failed: %s", me, r, hipGetErrorString(e));
@@ -200,16 +217,18 @@ uint64_t IpcTileBytes()
     return std::strtoull(e, nullptr, 10) << 10;
 }
 
-// Barrier fences (IpcArgs::fence). Every byte a barrier hands over lives in uncached staging, which no L2 holds: a
-// store's vmcnt drain is its release, and the reader's loads go to memory. So by default the barriers skip the
-// system-scope release and acquire, which write back and invalidate the whole XCD's L2 for every block and stall the
-// blocks still streaming there (r03: 3-13 % per call in loopback worlds, profiles/r03_ipc_variant_ab_fence.jsonl;
-// the IPC GPU tests, rank mode and stress included, bit-exact with them). HCCL_AMD_IPC_LIGHT_FENCE=0 restores the
-// system-scope fences. Read per call, equal on every rank.
+// Barrier fences (IpcArgs::fence), HCCL_AMD_IPC_LIGHT_FENCE=1 (opt-in, r03 A/B). Every byte a barrier hands over
+// lives in uncached staging, which no L2 holds, so the waves' vmcnt drains alone order the data before the flag, and
+// an agent-scope acquire (the CU's L1) suffices for the reader: the light barriers skip the system-scope release and
+// acquire, which write back and invalidate the whole XCD L2 for every block. That is 3-13 % per call in loopback worlds
+// (profiles/r03_ipc_variant_ab_fence.jsonl), and the IPC GPU tests pass bit-exact with it. It stays off by default:
+// in the GPU suite's order, the loopback executor run that follows a light-fence IPC call in
+// test_gpu_collectives.py::test_ipc_follows_auto_family read stale 128-B lines (one or several) in 3 of 4 runs, and
+// never with the system-scope fences; the cause is not found. Read per call, equal on every rank.
 bool IpcLightFence()
 {
     const char* e = std::getenv("HCCL_AMD_IPC_LIGHT_FENCE");
-    return e == nullptr || std::strcmp(e, "0") != 0;
+    return e != nullptr && std::strcmp(e, "1") == 0;
 }
 
 // HCCL_AMD_IPC_THREADS: threads per workgroup, 256 (default) or 512 (r03 A/B). Read per call, equal on every rank.
@@ -271,14 +290,12 @@ void IpcRelease(Comm& c)
     IpcState& s = c.ipc;
     for (uint32_t r = 0; r < kIpcMaxRanks; ++r) {
         if (s.opened[r]) {
-            for (int k = 0; k < kIpcAreas; ++k) (void)hipIpcCloseMemHandle(s.peerArea[k][r]);
+            (void)hipIpcCloseMemHandle(s.peerArea[0][r]);  // the peer's one staging allocation
             (void)hipIpcCloseMemHandle(s.peerFlags[r]);
             s.opened[r] = false;
         }
     }
-    for (int k = 0; k < kIpcAreas; ++k) {
-        if (s.area[k] != nullptr) (void)hipFree(s.area[k]);
-    }
+    if (s.area[0] != nullptr) (void)hipFree(s.area[0]);  // the areas are parts of this one allocation
     if (s.flags != nullptr) (void)hipFree(s.flags);
     if (s.status != nullptr) (void)hipFree(s.status);
     if (s.trace != nullptr) (void)hipFree(s.trace);
@@ -309,8 +326,8 @@ uint64_t IpcStagingBytes()
     const char* e = std::getenv("HCCL_AMD_IPC_STAGING_MIB");
     if (e != nullptr && *e != '\0') {
         const unsigned long long v = std::strtoull(e, nullptr, 10);
-        // below 2 GiB: a 2 GiB allocation's IPC handle never opened (IpcSetup)
-        if (v >= 16 && v <= 1536) return static_cast<uint64_t>(v) << 20;
+        // the staging allocation stays below 2 GiB (IpcSetup): areas of at most 1000 MiB
+        if (v >= 16 && v <= 1000) return static_cast<uint64_t>(v) << 20;
     }
     return kIpcStagingBytes;
 }

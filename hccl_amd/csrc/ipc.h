@@ -10,7 +10,7 @@
 namespace hccl_amd {
 
 constexpr int kIpcMaxRanks = 16;
-// Staging areas of a rank, each its own allocation (and IPC handle): slots, results, and the two alternate slot areas
+// Staging areas of a rank, parts of one allocation (one IPC handle): slots, results, and the two alternate slot areas
 // of the single-barrier kinds.
 constexpr int kIpcAreas = 4;
 constexpr int kIpcAreaIn = 0;
@@ -121,9 +121,9 @@ struct IpcArgs {
                          // b, b + B, b + 2B, ... (B = blocks): the same piece coordinates in every round either way
     uint32_t nt;         // non-temporal loads and stores in the copy and fold loops
     uint32_t threads;    // threads per workgroup (kIpcBlock, or 512 by HCCL_AMD_IPC_THREADS)
-    uint32_t fence;      // barrier fences: 1 = light (default): the waves' drains release the uncached staging, an
-                         // agent-scope acquire (L1); 0 = system-scope release (XCD-wide L2 write-back) and acquire
-                         // (L2 invalidate), forced for cached staging
+    uint32_t fence;      // barrier fences: 0 (default) = system-scope release (XCD-wide L2 write-back) and acquire
+                         // (L2 invalidate); 1 = light (HCCL_AMD_IPC_LIGHT_FENCE=1): the waves' drains release the
+                         // uncached staging, an agent-scope acquire (L1); never with cached staging
     uint32_t rounds;
     uint32_t epochSpan;  // barriers per block in this launch: the device epoch counter advances by this much
     uint64_t outStride;  // kIpcAllGather: elements between consecutive ranks' blocks of the output (sendCount)
@@ -191,7 +191,8 @@ HcclResult ScrubL2(hipStream_t stream);
 struct IpcState {
     bool ready = false;
     bool unavailable = false;      // set-up failed on some rank: every later call reports NOT_SUPPORT
-    void* area[kIpcAreas] = {};    // own staging areas, uncached (kIpcAreaIn, kIpcAreaRes, kIpcAreaAlt0, kIpcAreaAlt1)
+    void* area[kIpcAreas] = {};    // own staging areas, uncached, in one allocation at area[0] (kIpcAreaIn, kIpcAreaRes,
+                                   // kIpcAreaAlt0, kIpcAreaAlt1)
     uint32_t* flags = nullptr;     // own flags, uncached, zeroed
     uint32_t* status = nullptr;    // device words: [0] bit 0 = barrier timeout, [2..3] = tagged longest wait (IpcArgs)
     uint32_t callSeq = 0;          // IPC calls issued on the communicator (tags the wait diagnostic)
@@ -221,6 +222,8 @@ constexpr int kIpcDoneWord = 5;
 // round where 128 MiB areas took 2-4, 5-12 % faster at n = 2 and 4 (tools/ipc_variant_ab.py,
 // profiles/r03_ipc_variant_ab_{policy,shapes}.jsonl); each round costs two cross-rank barriers and three phase fills and drains.
 constexpr uint64_t kIpcStagingBytes = 512ull << 20;
-uint64_t IpcStagingBytes();  // HCCL_AMD_IPC_STAGING_MIB (16 .. 1536) or kIpcStagingBytes; equal on every rank
+uint64_t IpcStagingBytes();  // HCCL_AMD_IPC_STAGING_MIB (16 .. 1000) or kIpcStagingBytes; equal on every rank
+// Bound of the one staging allocation of a rank (IpcSetup): a 2 GiB allocation's IPC handle never opened.
+constexpr uint64_t kIpcStagingMaxBytes = 2047ull << 20;
 
 }  // namespace hccl_amd
