@@ -272,7 +272,7 @@ def fold_roofline(dev, stream, n: int = 8, reps: int = 10) -> dict:
             "kernel_avg_us": round(kavg * 1e6, 1), "kernel_median_us": round(float(np.median(per)) * 1e6, 1),
             "achieved_GBps": round(nbytes / kavg / 1e9, 1), "peak_GBps": HBM_PEAK_GBPS,
             "frac": round(nbytes / kavg / 1e9 / HBM_PEAK_GBPS, 4),
-            "traffic": load_pmc_traffic("r03b_pmc_fold_n8.json") or load_pmc_traffic("r02b_pmc_fold_n8.json"),
+            "traffic": load_pmc_traffic("r03c_pmc_fold_n8.json") or load_pmc_traffic("r03b_pmc_fold_n8.json"),
             "result_ok": ok}
 
 
@@ -285,6 +285,10 @@ def ipc_two_shot_roofline(dev, n: int = 2, mib: int = 512, reps: int = 10) -> di
     against torch's add in the two-shot order O2 (acc = x0; acc = x1 + acc)."""
     from concurrent.futures import ThreadPoolExecutor
 
+    # phase stamps on (read at the world's IPC set-up): each launch's own span, first block in to last block out, is
+    # the kernel's duration; the HIP events between calls also hold the loopback world's cross-stream hand-offs
+    prev_trace = os.environ.get("HCCL_AMD_IPC_TRACE")
+    os.environ["HCCL_AMD_IPC_TRACE"] = "1"
     comms = H.loopback_world(n)
     count = (mib << 20) // 4
     g = torch.Generator(device=dev).manual_seed(0x5EED0009)
@@ -302,13 +306,24 @@ def ipc_two_shot_roofline(dev, n: int = 2, mib: int = 512, reps: int = 10) -> di
 
         call()  # set-up (staging, peer pointers) on the first call
         torch.cuda.synchronize()
+        if prev_trace is None:
+            os.environ.pop("HCCL_AMD_IPC_TRACE")
+        else:
+            os.environ["HCCL_AMD_IPC_TRACE"] = prev_trace
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
         evs[0].record(streams[0])
         for k in range(reps):
             call()
             evs[k + 1].record(streams[0])  # the world's launch runs on rank 0's stream
         torch.cuda.synchronize()
-        per = [evs[k].elapsed_time(evs[k + 1]) / 1e3 for k in range(reps)]
+        per_call = [evs[k].elapsed_time(evs[k + 1]) / 1e3 for k in range(reps)]
+        per = []
+        for _ in range(reps):
+            call()
+            torch.cuda.synchronize()
+            st, blocks = comms[0].ipc_trace()
+            a = st[:n, :blocks, :].astype(np.int64)
+            per.append(float(a[:, :, 7].max() - a[:, :, 0].min()) * 1e-8)  # s_memrealtime: 100 MHz
         want = torch.add(xs[1], xs[0]) if n == 2 else None
         ok = want is not None and all(bool(torch.equal(y, want)) for y in ys)
         ran = H.Algo(comms[0].last_algo).name
@@ -322,9 +337,13 @@ def ipc_two_shot_roofline(dev, n: int = 2, mib: int = 512, reps: int = 10) -> di
     return {"kernel": "k_ipc_collective<EFp<float>, SUM> (two-shot AllReduce, loopback world)", "ranks": n,
             "bytes_per_rank": count * 4, "ran": ran, "algorithmic_bytes_per_launch": nbytes,
             "kernel_avg_us": round(kavg * 1e6, 1), "kernel_median_us": round(float(np.median(per)) * 1e6, 1),
+            "kernel_timing": "each launch's span from its blocks' s_memrealtime stamps (first entry to last exit; "
+                             "HCCL_AMD_IPC_TRACE), one launch per call",
+            "call_to_call_avg_us": round(float(np.mean(per_call)) * 1e6, 1),
             "achieved_GBps": round(nbytes / kavg / 1e9, 1), "peak_GBps": HBM_PEAK_GBPS,
             "frac": round(nbytes / kavg / 1e9 / HBM_PEAK_GBPS, 4),
-            "traffic": load_pmc_traffic("r03b_pmc_ipc_two_shot.json"), "barrier_timeouts": timeouts,
+            "traffic": load_pmc_traffic("r03c_pmc_ipc_two_shot.json") or load_pmc_traffic("r03b_pmc_ipc_two_shot.json"),
+            "barrier_timeouts": timeouts,
             "result_ok": ok}
 
 
@@ -387,7 +406,7 @@ def bench_local(args) -> dict:
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": load_pmc_traffic("r03b_pmc_local_reduce.json") or load_pmc_traffic("r02b_pmc_local_reduce.json"),
+            "traffic": load_pmc_traffic("r03c_pmc_local_reduce.json") or load_pmc_traffic("r03b_pmc_local_reduce.json"),
             "kernel": "k_reduce2<EFp<float>, SUM>",
             "algorithmic_bytes_per_launch": bytes_step,
             "kernel_avg_us": round(kavg * 1e6, 2),
