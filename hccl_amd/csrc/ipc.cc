@@ -217,18 +217,17 @@ uint64_t IpcTileBytes()
     return std::strtoull(e, nullptr, 10) << 10;
 }
 
-// Barrier fences (IpcArgs::fence), HCCL_AMD_IPC_LIGHT_FENCE=1 (opt-in, r03 A/B). Every byte a barrier hands over
-// lives in uncached staging, which no L2 holds, so the waves' vmcnt drains alone order the data before the flag, and
-// an agent-scope acquire (the CU's L1) suffices for the reader: the light barriers skip the system-scope release and
-// acquire, which write back and invalidate the whole XCD L2 for every block. That is 3-13 % per call in loopback worlds
-// (profiles/r03_ipc_variant_ab_fence.jsonl), and the IPC GPU tests pass bit-exact with it. It stays off by default:
-// in the GPU suite's order, the loopback executor run that follows a light-fence IPC call in
-// test_gpu_collectives.py::test_ipc_follows_auto_family read stale 128-B lines (one or several) in 3 of 4 runs, and
-// never with the system-scope fences; the cause is not found. Read per call, equal on every rank.
+// Barrier fences (IpcArgs::fence). Every byte a barrier hands over lives in uncached staging, which no L2 holds: the
+// storing waves' vmcnt drains order the data before the flag (a store completes at memory), and an agent-scope acquire
+// (the CU's L1) suffices for the reader, whose loads go to memory. So by default the barriers skip the system-scope
+// release and acquire, which write back and invalidate the whole XCD L2 for every block and stall the blocks still
+// streaming there: 3-13 % per call in loopback worlds (profiles/r03_ipc_variant_ab_fence.jsonl); the whole GPU suite
+// passes with either. HCCL_AMD_IPC_LIGHT_FENCE=0 restores the system-scope fences. Read per call,
+// equal on every rank.
 bool IpcLightFence()
 {
     const char* e = std::getenv("HCCL_AMD_IPC_LIGHT_FENCE");
-    return e != nullptr && std::strcmp(e, "1") == 0;
+    return e == nullptr || std::strcmp(e, "0") != 0;
 }
 
 // HCCL_AMD_IPC_THREADS: threads per workgroup, 256 (default) or 512 (r03 A/B). Read per call, equal on every rank.

@@ -121,9 +121,9 @@ struct IpcArgs {
                          // b, b + B, b + 2B, ... (B = blocks): the same piece coordinates in every round either way
     uint32_t nt;         // non-temporal loads and stores in the copy and fold loops
     uint32_t threads;    // threads per workgroup (kIpcBlock, or 512 by HCCL_AMD_IPC_THREADS)
-    uint32_t fence;      // barrier fences: 0 (default) = system-scope release (XCD-wide L2 write-back) and acquire
-                         // (L2 invalidate); 1 = light (HCCL_AMD_IPC_LIGHT_FENCE=1): the waves' drains release the
-                         // uncached staging, an agent-scope acquire (L1); never with cached staging
+    uint32_t fence;      // barrier fences: 1 = light (default): the waves' drains release the uncached staging, an
+                         // agent-scope acquire (L1); 0 = system-scope release (XCD-wide L2 write-back) and acquire
+                         // (L2 invalidate): HCCL_AMD_IPC_LIGHT_FENCE=0, and always with cached staging
     uint32_t rounds;
     uint32_t epochSpan;  // barriers per block in this launch: the device epoch counter advances by this much
     uint64_t outStride;  // kIpcAllGather: elements between consecutive ranks' blocks of the output (sendCount)

@@ -24,9 +24,10 @@
 // Every round of one launch has the same geometry (the host launches a shorter last round separately), so block b
 // of every rank touches the same slot and result addresses in every round and only waits for block b of its peers;
 // nothing in a GPU waits for another block of the same GPU. Every storing wave drains (s_waitcnt vmcnt(0)) before the
-// workgroup barrier, one wave then releases at system scope (L2 write-back) and stores the flags with system-scope
-// stores; flags are polled with system-scope relaxed loads and followed by a system-scope acquire (IpcArgs::fence 0, the
-// default; fence 1 drops both: see IpcLightFence in ipc.cc). Every wait is bounded
+// workgroup barrier; since every handed-over byte is in uncached staging that drain is the release (IpcArgs::fence 1,
+// the default; fence 0 adds the system-scope L2 write-back), and one wave stores the flags with system-scope stores;
+// flags are polled with system-scope relaxed loads and followed by an acquire (agent scope: the CU's L1; fence 0:
+// system scope; IpcLightFence in ipc.cc). Every wait is bounded
 // in wall time (s_memrealtime, HCCL_AMD_IPC_TIMEOUT_MS): on timeout the kernel sets status bit 0 and finishes (wrong
 // data, never a hang); the bit is sticky for the communicator, so later launches return at once. World mode (me < 0) runs all
 // n ranks of a loopback world as blockIdx.y of one launch on one GPU, which is how the protocol is tested without a

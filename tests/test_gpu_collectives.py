@@ -184,12 +184,13 @@ def test_ipc_phase_trace(monkeypatch, n, count):
             c.destroy()
 
 
-@pytest.mark.parametrize("fence,threads", [("1", "256"), ("1", "512"), ("0", "512")])
+@pytest.mark.parametrize("fence,threads", [("0", "256"), ("1", "512"), ("0", "512")])
 @pytest.mark.parametrize("kind", [AR, RS, AG])
 def test_ipc_barrier_variants(monkeypatch, fence, threads, kind):
-    """The one-sided kernel with light barrier fences (HCCL_AMD_IPC_LIGHT_FENCE=1: the waves' drains as the release, an
-    agent-scope acquire; opt-in) and with 512-thread workgroups (HCCL_AMD_IPC_THREADS): same bits as the schedule's
-    order over several staging rounds and odd counts, barrier status clean."""
+    """The one-sided kernel with the system-scope barrier fences (HCCL_AMD_IPC_LIGHT_FENCE=0; the light fences, the
+    waves' drains as the release and an agent-scope acquire, are the default the rest of the suite runs) and with
+    512-thread workgroups (HCCL_AMD_IPC_THREADS): same bits as the schedule's order over several staging rounds and odd
+    counts, barrier status clean."""
     monkeypatch.setenv("HCCL_AMD_IPC_LIGHT_FENCE", fence)
     monkeypatch.setenv("HCCL_AMD_IPC_THREADS", threads)
     monkeypatch.setenv("HCCL_AMD_IPC_STAGING_MIB", "16")

@@ -19,7 +19,7 @@
 #   counters       the TCC counters this rocprofv3 offers
 #   ipc_staging    one-sided kernel: uncached vs cached staging memory (A/B on one device)
 #   ipc_fence      one-sided kernel: system-scope vs light barrier fences x workgroups per rank (A/B)
-#   ipc_light_tests  the one-sided kernel's GPU tests with the opt-in light barrier fences
+#   ipc_system_fence_tests  the one-sided kernel's GPU tests with the system-scope barrier fences
 #   ipc_latency_fence  one-sided kernel latency, rank mode, system vs light fences
 #   phase_trace_variants  the phase trace with light fences and with cached staging
 #   phase_trace    per-block phase stamps of the one-sided two-shot kernel, loopback worlds n = 2, 4, 8
@@ -149,10 +149,10 @@ step_ipc_fence() {
   grep '^{' "$OUT/ipc_fence.log" > "$OUT/ipc_variant_ab_fence.jsonl" || true
 }
 
-# every one-sided-kernel GPU test with the light barrier fences (HCCL_AMD_IPC_LIGHT_FENCE=1, opt-in; the rank-mode
-# children inherit it): loopback worlds, rank mode, the random stress
-step_ipc_light_tests() {
-  HCCL_AMD_IPC_LIGHT_FENCE=1 HCCL_AMD_RANDOM_DRAWS=1000 run ipc_light_tests 600 python3 -u -m pytest \
+# every one-sided-kernel GPU test with the system-scope barrier fences (HCCL_AMD_IPC_LIGHT_FENCE=0; the rank-mode
+# children inherit it; light fences are the default): loopback worlds, rank mode, the random stress
+step_ipc_system_fence_tests() {
+  HCCL_AMD_IPC_LIGHT_FENCE=0 HCCL_AMD_RANDOM_DRAWS=1000 run ipc_system_fence_tests 600 python3 -u -m pytest \
     tests/test_gpu_ipc_ranks.py tests/test_gpu_ipc_stress.py tests/test_gpu_collectives.py -m gpu -k "ipc or IPC or aiv or AIV" \
     -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
 }
