@@ -164,6 +164,27 @@ def executor_plan(ops, nops: int, elem_size: int, bases=(1 << 40, 2 << 40, 3 << 
             for u in units[:n.value]]
 
 
+def l2_maintain(stream=None) -> None:
+    """HcclAmdL2Maintain: system-scope write-back + invalidate of every XCD's L2, then wait (diagnostics)."""
+    check("HcclAmdL2Maintain", lib.HcclAmdL2Maintain(_stream(stream)))
+
+
+def diag_read_by_xcc(ptr: int, expect: torch.Tensor, non_temporal: bool = False, stream=None):
+    """HcclAmdDiagReadByXcc over expect.numel() 4-byte words at device address ptr: per XCC id, the mismatching and the
+    zero words summed over that XCD's workgroups (every workgroup reads the whole range), as two lists of 8."""
+    out = torch.zeros(768, dtype=torch.int32, device=expect.device)
+    words = expect.numel() * expect.element_size() // 4
+    check("HcclAmdDiagReadByXcc", lib.HcclAmdDiagReadByXcc(ptr, _ptr(expect), words, 1 if non_temporal else 0,
+                                                           _ptr(out), _stream(stream)))
+    torch.cuda.synchronize()
+    o = out.view(256, 3).cpu().tolist()
+    bad, zero = [0] * 8, [0] * 8
+    for b, z, x in o:
+        bad[x & 7] += b
+        zero[x & 7] += z
+    return bad, zero
+
+
 def ring_table(n_ranks: int) -> List[List[int]]:
     """The directed rings of HCCL_AMD_ALGO_RING (HcclAmdRingTable), as rank lists."""
     r = lib.HcclAmdRingTable(n_ranks, None, 0)
@@ -220,6 +241,13 @@ class Comm:
         dt = hccl_dtype(send) if dtype is None else int(dtype)
         check("HcclAmdCommExecute", lib.HcclAmdCommExecute(self.handle, ops, nops, _ptr(send), _ptr(recv), dt, int(op),
                                                            1 if single_stream else 0, _stream(stream)))
+
+    def scratch(self) -> tuple:
+        """(device address, bytes) of the communicator's executor staging (HcclAmdCommScratch; diagnostics)."""
+        p = ctypes.c_void_p(0)
+        b = ctypes.c_uint64(0)
+        check("HcclAmdCommScratch", lib.HcclAmdCommScratch(self.handle, ctypes.byref(p), ctypes.byref(b)))
+        return p.value or 0, b.value
 
     def compile_stats(self) -> tuple:
         """(hits, misses) of the communicator's compiled-collective cache (HcclAmdCommCompileStats)."""

@@ -203,6 +203,9 @@ SIGNATURES = {
     "HcclAmdLastBootstrap": (_res, [ctypes.POINTER(_u64), ctypes.POINTER(ctypes.c_int32)]),
     "HcclAmdBootstrapExchangeId": (_res, [ctypes.c_char_p, _u32, _vp]),
     "HcclAmdCommPendingDestroys": (_u32, []),
+    "HcclAmdCommScratch": (_res, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_u64)]),
+    "HcclAmdL2Maintain": (_res, [_vp]),
+    "HcclAmdDiagReadByXcc": (_res, [_vp, _vp, _u64, _i32, _vp, _vp]),
     "HcclAmdHostProfile": (_res, [ctypes.POINTER(_u64), ctypes.POINTER(_u64), _u32, _i32]),
 }
 

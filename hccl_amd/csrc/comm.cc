@@ -535,7 +535,7 @@ public:
                 result = HCCL_E_INTERNAL;
             } else {
                 ok = hipStreamWaitEvent(stream, e->ready, 0) == hipSuccess &&
-                     hipMemcpyAsync(o.ptr, e->src, o.bytes, hipMemcpyDeviceToDevice, stream) == hipSuccess &&
+                     LaunchCopyBytes(o.ptr, e->src, o.bytes, stream) == HCCL_SUCCESS &&
                      hipEventCreateWithFlags(&done, hipEventDisableTiming) == hipSuccess &&
                      hipEventRecord(done, stream) == hipSuccess;
                 if (!ok) result = HCCL_E_RUNTIME;

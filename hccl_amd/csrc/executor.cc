@@ -188,7 +188,7 @@ static HcclResult ExecuteSingleStream(Comm& c, const std::vector<HcclAmdIrOp>& o
         if (o.kind == HCCL_AMD_IR_COPY) {
             HpScope hp(HCCL_AMD_HP_COPY);
             const void* src = reinterpret_cast<const void*>(addr(o.srcBuf[0], o.srcOff[0]));
-            if (src != dst) HIP_CHK(hipMemcpyAsync(dst, src, o.count * es, hipMemcpyDeviceToDevice, user));
+            HCCL_CHK(LaunchCopyBytes(dst, src, o.count * es, user));
         } else if (o.kind == HCCL_AMD_IR_REDUCE) {
             HpScope hp(HCCL_AMD_HP_FOLD);
             const size_t m = BatchRun(ops, i, es, bufs);
@@ -463,9 +463,7 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
             HpScope hp(o.kind == HCCL_AMD_IR_COPY ? HCCL_AMD_HP_COPY : HCCL_AMD_HP_FOLD);
             if (o.kind == HCCL_AMD_IR_COPY) {
                 const void* src = reinterpret_cast<const void*>(addr(o.srcBuf[0], o.srcOff[0]));
-                if (src != dst) {
-                    HIP_CHK(hipMemcpyAsync(dst, src, o.count * es, hipMemcpyDeviceToDevice, streams[x]));
-                }
+                HCCL_CHK(LaunchCopyBytes(dst, src, o.count * es, streams[x]));
             } else if (o.kind == HCCL_AMD_IR_REDUCE) {
                 HCCL_CHK(LaunchFolds(ops, u.first, u.count, es, bufs, dt, op, streams[x]));
             } else {

@@ -44,6 +44,11 @@ struct FoldSeg {
 HcclResult LaunchReduceNBatch(const FoldSeg* segs, uint32_t nseg, uint32_t nsrc, HcclDataType dt, HcclReduceOp op,
                               hipStream_t stream);
 
+// dst = src over `bytes` bytes on `stream`: this library's copy kernel, or hipMemcpyAsync with
+// HCCL_AMD_DEVICE_COPY=memcpy (reduce_kernels.hip; DESIGN.md §5b, device copies).
+HcclResult LaunchCopyBytes(void* dst, const void* src, uint64_t bytes, hipStream_t stream);
+bool DeviceCopyByKernel();
+
 // HCCL_EXEC_TIMEOUT in the reference's format (ParseExecTimeout, alg_env_config.cc:75-110): false when unset or
 // malformed, else *seconds (>= 0, <= UINT32_MAX, at most two decimals).
 bool ParseExecTimeoutSeconds(const char* env, double* seconds);

@@ -219,15 +219,21 @@ uint64_t IpcTileBytes()
 
 // Barrier fences (IpcArgs::fence). Every byte a barrier hands over lives in uncached staging, which no L2 holds: the
 // storing waves' vmcnt drains order the data before the flag (a store completes at memory), and an agent-scope acquire
-// (the CU's L1) suffices for the reader, whose loads go to memory. So by default the barriers skip the system-scope
-// release and acquire, which write back and invalidate the whole XCD L2 for every block and stall the blocks still
-// streaming there: 3-13 % per call in loopback worlds (profiles/r03_ipc_variant_ab_fence.jsonl); the whole GPU suite
-// passes with either. HCCL_AMD_IPC_LIGHT_FENCE=0 restores the system-scope fences. Read per call,
-// equal on every rank.
-bool IpcLightFence()
+// (the CU's L1) suffices for the reader, whose loads go to memory. The user buffers are never handed over inside the
+// kernel (each element is read and written by the lane that owns it); across kernels they are ordered by the ordinary
+// kernel boundaries, which make plain and non-temporal stores visible to the next kernel on every XCD
+// (tools/coherence_probe.hip, profiles/r04_coherence_probe.jsonl). The light fences skip the system-scope release and
+// acquire, which write back and invalidate the whole XCD L2 for every block: 3-13 % per call in loopback worlds
+// (profiles/r03_ipc_variant_ab_fence.jsonl). Default: light in a loopback world (one device, the argument above and
+// tests/test_gpu_collectives.py cover it), system scope in rank mode, whose stores cross to other devices' staging
+// through imported mappings that no test on this pool has exercised over xGMI. HCCL_AMD_IPC_LIGHT_FENCE=1
+// or 0 forces either. The r03 stale-operand failure blamed on the light fences was the loopback link's
+// hipMemcpyAsync, with either setting. Read per call, equal on every rank.
+bool IpcLightFence(bool sharedDevice)
 {
     const char* e = std::getenv("HCCL_AMD_IPC_LIGHT_FENCE");
-    return e == nullptr || std::strcmp(e, "0") != 0;
+    if (e == nullptr || *e == '\0') return sharedDevice;
+    return std::strcmp(e, "0") != 0;
 }
 
 // HCCL_AMD_IPC_THREADS: threads per workgroup, 256 (default) or 512 (r03 A/B). Read per call, equal on every rank.
@@ -695,7 +701,7 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
         g.blockElems = ((g.piece + s.blocks - 1) / s.blocks + V - 1) / V * V;
         g.tileElems = IpcTileBytes() / es / V * V;  // 0: contiguous windows
         g.nt = IpcNonTemporal() ? 1u : 0u;
-        g.fence = (IpcLightFence() && !s.cachedStaging) ? 1u : 0u;
+        g.fence = (IpcLightFence(c.transport->SharedDevice()) && !s.cachedStaging) ? 1u : 0u;
         g.threads = IpcThreads();
         g.rounds = static_cast<uint32_t>((widest + g.piece - 1) / g.piece);
         g.epochSpan = (single ? 1 : 2) * g.rounds;

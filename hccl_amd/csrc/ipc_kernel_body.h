@@ -25,7 +25,8 @@
 // of every rank touches the same slot and result addresses in every round and only waits for block b of its peers;
 // nothing in a GPU waits for another block of the same GPU. Every storing wave drains (s_waitcnt vmcnt(0)) before the
 // workgroup barrier; since every handed-over byte is in uncached staging that drain is the release (IpcArgs::fence 1,
-// the default; fence 0 adds the system-scope L2 write-back), and one wave stores the flags with system-scope stores;
+// the loopback world's default; fence 0, rank mode's default, adds the system-scope L2 write-back), and one wave stores
+// the flags with system-scope stores;
 // flags are polled with system-scope relaxed loads and followed by an acquire (agent scope: the CU's L1; fence 0:
 // system scope; IpcLightFence in ipc.cc). Every wait is bounded
 // in wall time (s_memrealtime, HCCL_AMD_IPC_TIMEOUT_MS): on timeout the kernel sets status bit 0 and finishes (wrong

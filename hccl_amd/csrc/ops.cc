@@ -88,10 +88,7 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     if (c.nRanks == 1) {
         // SingleRankProc (op_common.cc:3042-3098): copy in -> out unless they are the same buffer.
         c.lastAlgo = HCCL_AMD_ALGO_AUTO;
-        if (sendBuf != recvBuf) {
-            HIP_CHK(hipMemcpyAsync(recvBuf, sendBuf, count * es, hipMemcpyDeviceToDevice, stream));
-        }
-        return HCCL_SUCCESS;
+        return LaunchCopyBytes(recvBuf, sendBuf, count * es, stream);
     }
     ScheduleParams p;
     p.opType = opType;
@@ -480,7 +477,19 @@ int32_t HcclAmdCommLastAlgo(HcclComm comm)
     return c == nullptr ? -1 : c->lastAlgo;
 }
 
-HcclResult HcclAmdCommExecute(HcclComm comm, const HcclAmdIrOp* ops, uint64_t numOps, void* sendBuf, void* recvBuf,
+HcclResult HcclAmdCommScratch(HcclComm comm, void** ptr, uint64_t* bytes)
+{
+    Comm* c = AsComm(comm);
+    if (c == nullptr || ptr == nullptr || bytes == nullptr) return HCCL_E_PTR;
+    std::lock_guard<std::mutex> lk(c->mu);
+    *ptr = c->scratch;
+    *bytes = c->scratch != nullptr ? c->scratchBytes : 0;
+    return HCCL_SUCCESS;
+}
+
+HcclResult HcclAmdL2Maintain(aclrtStream stream) { return ScrubL2(static_cast<hipStream_t>(stream)); }
+
+HcclResult HcclAmdCommExecute(HcclComm comm,const HcclAmdIrOp* ops, uint64_t numOps, void* sendBuf, void* recvBuf,
                               HcclDataType dataType, HcclReduceOp op, int32_t singleStream, aclrtStream stream)
 {
     Comm* c = AsComm(comm);

@@ -667,8 +667,7 @@ HcclResult LaunchReduceN(void* out, const void* const* srcs, uint32_t n, uint64_
         if (out == srcs[0]) return HCCL_SUCCESS;
         uint32_t es = DataTypeSize(dt);
         if (es == 0) return HCCL_E_NOT_SUPPORT;
-        HIP_CHK(hipMemcpyAsync(out, srcs[0], count * es, hipMemcpyDeviceToDevice, stream));
-        return HCCL_SUCCESS;
+        return LaunchCopyBytes(out, srcs[0], count * es, stream);
     }
     if (n == 2) {
         // acc = srcs[1] (op) srcs[0]
@@ -798,6 +797,57 @@ HcclResult LaunchReduceNBatch(const FoldSeg* segs, uint32_t nseg, uint32_t nsrc,
         HCCL_AMD_ERR("batched reduce launch failed: %s", hipGetErrorString(e));
         return HCCL_E_RUNTIME;
     }
+    return HCCL_SUCCESS;
+}
+
+
+// ------------------------------------------------------------------------------------------------ device copies
+
+namespace {
+
+// dst[0, bytes) = src[0, bytes): 16-B vectors over the aligned body (plain loads and stores, grid-stride), bytes at
+// the ragged ends. A kernel of this library, so the copy's stores are ordered before the next kernel of the stream by
+// the ordinary end-of-kernel release like every other kernel here (device copies).
+__global__ __launch_bounds__(256) void k_copy_bytes(unsigned char* dst, const unsigned char* src, uint64_t head,
+                                                    uint64_t nvec, uint64_t bytes)
+{
+    const uint64_t tid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    const u32x4* s = reinterpret_cast<const u32x4*>(src + head);
+    u32x4* d = reinterpret_cast<u32x4*>(dst + head);
+    for (uint64_t i = tid; i < nvec; i += stride) d[i] = s[i];
+    for (uint64_t i = tid; i < head; i += stride) dst[i] = src[i];
+    for (uint64_t i = head + nvec * 16 + tid; i < bytes; i += stride) dst[i] = src[i];
+}
+
+}  // namespace
+
+bool DeviceCopyByKernel()
+{
+    const char* e = std::getenv("HCCL_AMD_DEVICE_COPY");  // read per call: tests switch it
+    return e == nullptr || std::strcmp(e, "memcpy") != 0;
+}
+
+HcclResult LaunchCopyBytes(void* dst, const void* src, uint64_t bytes, hipStream_t stream)
+{
+    if (bytes == 0 || dst == src) return HCCL_SUCCESS;
+    if (!DeviceCopyByKernel()) {
+        HIP_CHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream));
+        return HCCL_SUCCESS;
+    }
+    const uintptr_t a = reinterpret_cast<uintptr_t>(dst), b = reinterpret_cast<uintptr_t>(src);
+    uint64_t head = 0, nvec = 0;
+    if ((a & 15u) == (b & 15u)) {
+        head = std::min<uint64_t>(bytes, (16 - (a & 15u)) & 15u);
+        nvec = (bytes - head) / 16;
+    } else {
+        head = bytes;  // no common 16-B phase: bytewise
+    }
+    const uint64_t work = nvec != 0 ? nvec : bytes;
+    const uint64_t blocks = std::min<uint64_t>(2048, std::max<uint64_t>(1, (work + 4 * 256 - 1) / (4 * 256)));
+    hipLaunchKernelGGL(k_copy_bytes, dim3(uint32_t(blocks)), dim3(256), 0, stream, static_cast<unsigned char*>(dst),
+                       static_cast<const unsigned char*>(src), head, nvec, bytes);
+    HIP_CHK(hipGetLastError());
     return HCCL_SUCCESS;
 }
 

@@ -277,6 +277,21 @@ extern HcclResult HcclAmdHostProfile(uint64_t* ns, uint64_t* calls, uint32_t n, 
 /* Communicators whose HcclCommDestroy is waiting for the graphs captured on them to be destroyed. */
 extern uint32_t HcclAmdCommPendingDestroys(void);
 
+/* The executor staging of comm (diagnostics): *ptr = its device address (NULL until allocated), *bytes = its size. */
+extern HcclResult HcclAmdCommScratch(HcclComm comm, void** ptr, uint64_t* bytes);
+
+/* Enqueues on `stream` a system-scope write-back and invalidate of every XCD's L2 of the current device (one
+ * workgroup per CU runs buffer_wbl2 sc0 sc1 / buffer_inv sc0 sc1) and waits for it. Diagnostics: a kernel launched
+ * after it reads every line from memory. */
+extern HcclResult HcclAmdL2Maintain(aclrtStream stream);
+
+/* Enqueues on `stream` a read of `words` 4-byte words at device address p by 256 workgroups (dealt over the XCDs),
+ * each reading the whole range with plain loads (nonTemporal = 0) or non-temporal loads (1) and comparing it with the
+ * device array `expect`. out (device, 768 uint32) receives {mismatching words, zero words, XCC id} per workgroup.
+ * Diagnostics: which XCDs see stale or unwritten lines of a buffer. */
+extern HcclResult HcclAmdDiagReadByXcc(const void* p, const void* expect, uint64_t words, int32_t nonTemporal,
+                                       void* out, aclrtStream stream);
+
 /* Blocking host all-gather supplied by the caller's bootstrap (a TCP store, MPI, torch.distributed gloo ...):
  * gathers `bytes` bytes from every rank into all[nRanks * bytes] in rank order; returns 0 on success. */
 typedef int32_t (*HcclAmdHostAllGatherFn)(void* ctx, const void* mine, uint64_t bytes, void* all);

@@ -58,7 +58,9 @@ def run_ranks(n, fn):
     assert not errs, errs
 
 
-def collective(comms, op_type, algo, dtype, op, xs, count, root=0, piece_bytes=0, inplace=False):
+def collective(comms, op_type, algo, dtype, op, xs, count, root=0, piece_bytes=0, inplace=False, keep=None):
+    """keep: a dict that receives the run's device buffers (keep["tensors"] = True keeps them alive, otherwise only
+    their addresses are recorded and the blocks go back to torch's cache as usual)."""
     n = len(comms)
     sends = [to_device(dtype, x) for x in xs]
     zeros = np.zeros(count * n if op_type == AG else count, O.NP_STORAGE[dtype])
@@ -83,6 +85,11 @@ def collective(comms, op_type, algo, dtype, op, xs, count, root=0, piece_bytes=0
     torch.cuda.synchronize()
     used = comms[0].last_algo
     outs = [to_host(dtype, r)[:count * n if op_type == AG else count] for r in recvs]
+    if keep is not None:
+        keep["send_ptrs"] = [hex(s.data_ptr()) for s in sends]
+        keep["recv_ptrs"] = [hex(r.data_ptr()) for r in recvs]
+        if keep.get("tensors"):
+            keep["sends"], keep["recvs"] = sends, recvs
     for c in comms:
         c.set_algo(0)
         c.set_piece_bytes(0)
@@ -281,12 +288,20 @@ def test_ipc_follows_auto_family(monkeypatch, op_type, n, count, buffsize):
         in_count = count * n if op_type == RS else count
         xs = [O.random_operands(O.FP32, in_count, seed=520 + r, edge=False) for r in range(n)]
         family = H.select_algo(op_type, n, count * 4, False)
-        used, outs = collective(comms, op_type, 9, O.FP32, O.SUM, xs, count, root=root)
+        ipc_run = {}
+        used, outs = collective(comms, op_type, 9, O.FP32, O.SUM, xs, count, root=root, keep=ipc_run)
         assert used == 9
         assert ipc_status(comms[0]) & 1 == 0
-        used_auto, outs_auto = collective(comms, op_type, 0, O.FP32, O.SUM, xs, count, root=root)
+        auto_run = {"tensors": True}
+        used_auto, outs_auto = collective(comms, op_type, 0, O.FP32, O.SUM, xs, count, root=root, keep=auto_run)
         assert used_auto == family
         want = R.expected(op_type, family, O.FP32, O.SUM, xs, count, root=root)
+        diag = None
+        if op_type != RED and any((outs_auto[r].view(np.uint32) != want[r].view(np.uint32)).any() for r in range(n)):
+            from tests._stale_diag import diagnose
+            diag = diagnose(comms, op_type, family, xs, count, root, want, outs_auto, auto_run["sends"],
+                            auto_run["recvs"], history={"ipc_run": ipc_run, "auto_send_ptrs": auto_run["send_ptrs"],
+                                                        "auto_recv_ptrs": auto_run["recv_ptrs"]})
         for r in range(n):
             if op_type == RED and r != root:
                 assert not outs[r].any(), "non-root recvBuf written"
@@ -303,7 +318,8 @@ def test_ipc_follows_auto_family(monkeypatch, op_type, n, count, buffsize):
             assert not len(diff), (f"auto run, rank {r}: {len(diff)} elements differ from the closed form, first "
                                    f"{diff[:6].tolist()} last {diff[-3:].tolist()}; got {outs_auto[r][diff[:3]]!r} "
                                    f"want {want[r][diff[:3]]!r}; per rank "
-                                   f"{[int(np.count_nonzero(outs_auto[q].view(np.uint32) != want[q].view(np.uint32))) for q in range(n)]}")
+                                   f"{[int(np.count_nonzero(outs_auto[q].view(np.uint32) != want[q].view(np.uint32))) for q in range(n)]}"
+                                   f"; diagnosis {diag}")
     finally:
         torch.cuda.synchronize()
         for c in comms:

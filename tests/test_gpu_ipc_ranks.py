@@ -60,8 +60,10 @@ def _inputs(dtype, count, n, seed):
     return [O.random_operands(dtype, count, seed * 1000 + r) for r in range(n)]
 
 
-def _rank_main(rank, n, port, q):
+def _rank_main(rank, n, port, q, fence=None):
     os.environ["HCCL_AMD_IPC_TIMEOUT_MS"] = "20000"  # a lost peer shows as a status bit, never a hang
+    if fence is not None:
+        os.environ["HCCL_AMD_IPC_LIGHT_FENCE"] = fence
     os.makedirs("gpurun_out", exist_ok=True)
     progress = open(f"gpurun_out/ipc_ranks_n{n}_r{rank}.log", "w", buffering=1)
     try:
@@ -179,13 +181,15 @@ def _rank_main(rank, n, port, q):
         time.sleep(10)  # peers' kernels are bounded: let them drain before this process's memory goes away
 
 
-@pytest.mark.parametrize("n", [2, 4])
-def test_ipc_collectives_rank_mode(n):
+@pytest.mark.parametrize("n,fence", [(2, None), (4, None), (2, "1")])
+def test_ipc_collectives_rank_mode(n, fence):
+    """Rank mode with its default system-scope barrier fences, and once (n = 2) with the light fences forced
+    (HCCL_AMD_IPC_LIGHT_FENCE=1, the loopback world's default)."""
     import sched_ref as R
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, n, port, q)) for r in range(n)]
+    procs = [ctx.Process(target=_rank_main, args=(r, n, port, q, fence)) for r in range(n)]
     for p in procs:
         p.start()
     try:
