@@ -851,9 +851,12 @@ def bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
 
 
 def _failed_line(args, world: int, rank: int, code: int, after_s: float, fallback) -> dict:
-    """The line of an N > 1 run whose headline loop failed (a rank's communicator timed out or errored)."""
+    """The line of an N > 1 run whose headline loop failed (a rank's communicator timed out or errored). Every rank
+    then exits with EXIT_FAILED after rank 0 printed it, so the failure shows in the run's exit code too."""
     import torch.distributed as dist
 
+    global _EXIT_CODE
+    _EXIT_CODE = EXIT_FAILED
     try:
         name = H.HcclResult(code).name
     except ValueError:
@@ -1087,6 +1090,11 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
 
 _PRINTED = threading.Event()
 _PRINT_LOCK = threading.Lock()
+# Exit codes besides 0: the headline loop failed on some rank (the line carries "error"), or the extras watchdog
+# stopped the run (the line carries "watchdog"). The JSON line is printed first either way.
+EXIT_FAILED = 3
+EXIT_WATCHDOG = 4
+_EXIT_CODE = 0
 
 
 def emit(res: dict) -> None:
@@ -1100,7 +1108,8 @@ def emit(res: dict) -> None:
 
 class _Watchdog:
     """Ends a rank whose secondary configs overrun `seconds`: rank 0 first prints the result (headline plus what
-    finished) with a note naming the stage that overran. Every rank arms it at the same point, so they stop together."""
+    finished) with a note naming the stage that overran, then every rank exits with EXIT_WATCHDOG. Every rank arms it
+    at the same point, so they stop together."""
 
     def __init__(self, seconds: float, rank: int, res: dict):
         self.seconds, self.rank, self.res, self.current = seconds, rank, res, "start"
@@ -1124,7 +1133,7 @@ class _Watchdog:
             emit(self.res)
         sys.stdout.flush()
         sys.stderr.flush()
-        os._exit(0)
+        os._exit(EXIT_WATCHDOG)
 
 
 def main():
@@ -1157,6 +1166,8 @@ def main():
         res = bench_local(args)
     if res is not None:
         emit(res)
+    sys.stdout.flush()
+    sys.exit(_EXIT_CODE)
 
 
 if __name__ == "__main__":

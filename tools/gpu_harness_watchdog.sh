@@ -1,6 +1,6 @@
 #!/bin/bash
 # r02: bench.py's N > 1 watchdog in the one-GPU harness: secondary configs stopped at a short deadline (DEADLINE, default 0.5 s) must still print
-# the headline line (with "watchdog") and end every rank with status 0. A crash check, not a result.
+# the headline line (with "watchdog") and end every rank with EXIT_WATCHDOG (4; r04: failures show in the exit code).
 set -uo pipefail
 mkdir -p gpurun_out
 HCCL_AMD_BENCH_EXTRAS_DEADLINE_S=${DEADLINE:-0.5} HCCL_AMD_BENCH_HOST_EXCHANGE=1 timeout -k 10 300 python -m torch.distributed.run \
