@@ -837,7 +837,45 @@ def _transport_info() -> dict:
     except Exception as e:  # noqa: BLE001
         ver = f"unknown ({type(e).__name__})"
     env = {k: v for k, v in sorted(os.environ.items()) if k.startswith(("NCCL_", "RCCL_", "HCCL_"))}
-    return {"rccl_version": ver, "env": env}
+    return {"rccl_version": ver, "env": env, "p2p_channels": _p2p_channels_info()}
+
+
+_RCCL_INIT_LOG = None  # NCCL_DEBUG_FILE pattern set by _capture_rccl_init (None: not captured)
+
+
+def _capture_rccl_init(rank: int) -> None:
+    """Before the first RCCL communicator: RCCL's INIT-subsystem log to a file of its own (only when the caller set no
+    NCCL_DEBUG), so the line can report the p2p channels RCCL actually set up (VERDICT r03 next #3)."""
+    global _RCCL_INIT_LOG
+    if "NCCL_DEBUG" in os.environ or "NCCL_DEBUG_FILE" in os.environ:
+        return
+    import tempfile
+    _RCCL_INIT_LOG = os.path.join(tempfile.gettempdir(), f"hccl_amd_rccl_init_r{rank}.%p.log")
+    os.environ["NCCL_DEBUG"] = "INFO"
+    os.environ["NCCL_DEBUG_SUBSYS"] = "INIT"
+    os.environ["NCCL_DEBUG_FILE"] = _RCCL_INIT_LOG
+
+
+def _p2p_channels_info() -> dict:
+    """The per-peer p2p channels the library configured (HcclAmdRcclP2pChannels) and what RCCL's INIT log reported
+    for this rank's communicators ("p2p channels:%d, p2p channels per peer:%d")."""
+    import re
+    out = {}
+    try:
+        per, mn = H.rccl_p2p_channels()
+        out["configured"] = {"NCCL_NCHANNELS_PER_PEER": per, "NCCL_MIN_P2P_NCHANNELS": mn}
+    except Exception as e:  # noqa: BLE001
+        out["configured"] = {"error": f"{type(e).__name__}: {e}"}
+    if _RCCL_INIT_LOG is not None:
+        path = _RCCL_INIT_LOG.replace("%p", str(os.getpid()))
+        try:
+            txt = open(path).read()
+            rep = [{"p2p_channels": int(a), "per_peer": int(b)}
+                   for a, b in re.findall(r"p2p channels:(\d+), p2p channels per peer:(\d+)", txt)]
+            out["rccl_reported"] = rep[:4]
+        except OSError as e:
+            out["rccl_reported"] = {"error": str(e)}
+    return out
 
 
 def bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
@@ -905,6 +943,8 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
         dist.broadcast_object_list(obj, src=0)
         return H.comm_init_root_info(world, obj[0], rank)
 
+    if not harness:
+        _capture_rccl_init(rank)
     comm = new_comm()
     count = C3_BYTES // 4
     g = torch.Generator(device=dev).manual_seed(0x5EED0003 + rank)

@@ -164,6 +164,15 @@ def executor_plan(ops, nops: int, elem_size: int, bases=(1 << 40, 2 << 40, 3 << 
             for u in units[:n.value]]
 
 
+def rccl_p2p_channels() -> tuple:
+    """(NCCL_NCHANNELS_PER_PEER, NCCL_MIN_P2P_NCHANNELS) this process's RCCL communicators were created with
+    (HcclAmdRcclP2pChannels; zeros before the first one)."""
+    per = ctypes.c_uint32(0)
+    mn = ctypes.c_uint32(0)
+    check("HcclAmdRcclP2pChannels", lib.HcclAmdRcclP2pChannels(ctypes.byref(per), ctypes.byref(mn)))
+    return per.value, mn.value
+
+
 def l2_maintain(stream=None) -> None:
     """HcclAmdL2Maintain: system-scope write-back + invalidate of every XCD's L2, then wait (diagnostics)."""
     check("HcclAmdL2Maintain", lib.HcclAmdL2Maintain(_stream(stream)))

@@ -205,6 +205,7 @@ SIGNATURES = {
     "HcclAmdCommPendingDestroys": (_u32, []),
     "HcclAmdCommScratch": (_res, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_u64)]),
     "HcclAmdL2Maintain": (_res, [_vp]),
+    "HcclAmdRcclP2pChannels": (_res, [ctypes.POINTER(_u32), ctypes.POINTER(_u32)]),
     "HcclAmdDiagReadByXcc": (_res, [_vp, _vp, _u64, _i32, _vp, _vp]),
     "HcclAmdHostProfile": (_res, [ctypes.POINTER(_u64), ctypes.POINTER(_u64), _u32, _i32]),
 }

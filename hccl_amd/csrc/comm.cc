@@ -3,8 +3,12 @@
 
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <string>
 
 namespace hccl_amd {
 
@@ -210,6 +214,11 @@ public:
     {
         std::lock_guard<std::mutex> lk(mu_);
         if (comm_ == nullptr) return;
+        if (localTeardown_) {
+            (void)ncclCommAbort(comm_);  // a deferred teardown: no peer takes part any more
+            comm_ = nullptr;
+            return;
+        }
         // ncclCommFinalize flushes this rank's outstanding work; bounded like any other wait on a peer
         ncclResult_t r = WaitSettled(comm_, ncclCommFinalize(comm_), RcclExecTimeoutMs());
         if (r == ncclSuccess) {
@@ -238,10 +247,24 @@ public:
     }
     const char* Name() const override { return "rccl"; }
     bool Abortable() const override { return true; }
-    void Abort() override
+    void SetLocalTeardown() override
     {
         std::lock_guard<std::mutex> lk(mu_);
-        AbortLocked();
+        localTeardown_ = true;
+    }
+    // From the watchdog thread. The communicator is taken out under the lock and aborted outside it: RCCL's abort
+    // raises the kernels' abort flag at once but then waits for the graphs holding its plans (the executor graph cache,
+    // a user's captured graph) to go, and a thread entering Group / AllGatherHost meanwhile must get
+    // HCCL_E_SUSPENDING instead of waiting on the lock.
+    void Abort() override
+    {
+        ncclComm_t c = nullptr;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            c = comm_;
+            comm_ = nullptr;
+        }
+        if (c != nullptr) (void)ncclCommAbort(c);
     }
     HcclResult AsyncError() override
     {
@@ -316,6 +339,7 @@ private:
     }
     std::mutex mu_;
     ncclComm_t comm_;
+    bool localTeardown_ = false;
 };
 
 }  // namespace
@@ -330,8 +354,63 @@ HcclResult RcclGetUniqueId(void* id128)
     return HCCL_SUCCESS;
 }
 
+namespace {
+
+uint32_t g_p2pPerPeer = 0;  // what RCCL was configured with (0 = not yet)
+uint32_t g_p2pMin = 0;
+
+uint32_t EnvU32(const char* name, uint32_t dflt)
+{
+    const char* e = std::getenv(name);
+    if (e == nullptr || *e == '\0') return dflt;
+    const unsigned long v = std::strtoul(e, nullptr, 10);
+    return v == 0 ? dflt : static_cast<uint32_t>(std::min<unsigned long>(v, 64));
+}
+
+uint32_t Pow2Up(uint32_t x)
+{
+    uint32_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+}  // namespace
+
+// Per-peer p2p channels of RCCL. The schedules move their data with grouped ncclSend/ncclRecv,
+// one message per peer per step, and RCCL's p2p kernel streams about 43 GB/s per channel
+// (profiles/r02_rccl_p2p_channels_selfloop.jsonl: 176 / 345 / 650 GB/s at 4 / 8 / 16 channels per peer), below one
+// 76.8 GB/s xGMI link per direction (cost_model.cc:78-79 prices the reference's links the same way). Left to RCCL's
+// topology defaults a peer may get fewer channels than its link needs; the reference sizes its channels per link
+// explicitly (alg_param.h:434-448). So before the process's first RCCL communicator: NCCL_NCHANNELS_PER_PEER =
+// HCCL_AMD_P2P_CHANNELS_PER_PEER (default 4, about twice a link) and NCCL_MIN_P2P_NCHANNELS = per peer x (n - 1)
+// rounded up to a power of two (at most 64), so every peer's channels are distinct. A value the user already set wins.
+// RCCL reads these once per process, so the first communicator's size decides; HcclAmdRcclP2pChannels reports them.
+void ConfigureRcclP2pChannels(uint32_t nRanks)
+{
+    static std::once_flag once;
+    std::call_once(once, [nRanks] {
+        const uint32_t per = Pow2Up(EnvU32("HCCL_AMD_P2P_CHANNELS_PER_PEER", 4));
+        if (std::getenv("NCCL_NCHANNELS_PER_PEER") == nullptr) {
+            setenv("NCCL_NCHANNELS_PER_PEER", std::to_string(per).c_str(), 0);
+        }
+        if (std::getenv("NCCL_MIN_P2P_NCHANNELS") == nullptr) {
+            const uint32_t mn = std::min<uint32_t>(64, Pow2Up(per * std::max<uint32_t>(1, nRanks - 1)));
+            setenv("NCCL_MIN_P2P_NCHANNELS", std::to_string(mn).c_str(), 0);
+        }
+        g_p2pPerPeer = EnvU32("NCCL_NCHANNELS_PER_PEER", 0);
+        g_p2pMin = EnvU32("NCCL_MIN_P2P_NCHANNELS", 0);
+    });
+}
+
+void RcclP2pChannels(uint32_t* perPeer, uint32_t* minP2p)
+{
+    *perPeer = g_p2pPerPeer;
+    *minP2p = g_p2pMin;
+}
+
 std::unique_ptr<Transport> MakeRcclTransport(void* uniqueId, uint32_t nRanks, uint32_t rank, HcclResult* err)
 {
+    ConfigureRcclP2pChannels(nRanks);
     ncclUniqueId id;
     std::memcpy(&id, uniqueId, sizeof id);
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
@@ -358,6 +437,7 @@ HcclResult MakeRcclTransportsAll(uint32_t ndev, const int32_t* devices, std::vec
 {
     // ncclCommInitAll's steps, with the communicators' config: one unique id, ncclCommInitRankConfig per device in a
     // group.
+    ConfigureRcclP2pChannels(ndev);
     ncclUniqueId id;
     HCCL_CHK(FromNccl(ncclGetUniqueId(&id), "ncclGetUniqueId"));
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;

@@ -49,6 +49,9 @@ public:
     virtual bool Abortable() const { return false; }
     // ncclCommAbort: in-flight device work returns, later groups fail. Callable from any thread.
     virtual void Abort() {}
+    // The teardown will run later, on one rank alone (a destroy deferred behind live graphs): it must not wait on
+    // peers (RCCL: abort instead of finalize).
+    virtual void SetLocalTeardown() {}
     // Loopback world: the pinned failure word all its ranks share (the world's single IPC launch writes it), owned by
     // the world so that it outlives every rank's communicator; *dev receives its device address. nullptr elsewhere.
     virtual uint32_t* SharedFailWord(uint32_t** dev)
@@ -62,6 +65,9 @@ std::unique_ptr<Transport> MakeRcclTransport(void* uniqueId, uint32_t nRanks, ui
 // One RCCL communicator per listed device, all in this process (ncclCommInitAll); (*out)[r] is rank r.
 HcclResult MakeRcclTransportsAll(uint32_t ndev, const int32_t* devices, std::vector<std::unique_ptr<Transport>>* out);
 HcclResult RcclGetUniqueId(void* id128);
+// RCCL's per-peer p2p channels, set in the environment before the process's first RCCL communicator (comm.cc).
+void ConfigureRcclP2pChannels(uint32_t nRanks);
+void RcclP2pChannels(uint32_t* perPeer, uint32_t* minP2p);
 
 class LoopbackWorld;
 std::unique_ptr<Transport> MakeLoopbackTransport(std::shared_ptr<LoopbackWorld> world, uint32_t rank);
@@ -219,6 +225,7 @@ struct Comm {
     // Graphs captured on this communicator that are still alive (NoteCapture); HcclCommDestroy defers the teardown
     // until they are gone (DeferDestroy).
     std::atomic<int32_t> graphRefs{0};
+    bool ipcQuiesced = false;  // the IPC teardown rendezvous already ran (at HcclCommDestroy of a deferred destroy)
     unsigned long long lastCaptureId = 0;
 
     // Fault injection for the timeout tests (HCCL_AMD_INJECT_STALL_GROUP=k): before the k-th transport group the link

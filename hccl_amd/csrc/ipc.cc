@@ -276,7 +276,8 @@ uint64_t IpcTimeoutTicks()
 
 void IpcQuiesce(Comm& c)
 {
-    if (!c.ipc.ready) return;
+    if (!c.ipc.ready || c.ipcQuiesced) return;
+    c.ipcQuiesced = true;
     // Peers store into this rank's staging and flags: unmapping or freeing them while any peer's kernel may still
     // run would fault that peer. Wait for this device, then for every rank to get here (each has waited for its own).
     (void)hipDeviceSynchronize();

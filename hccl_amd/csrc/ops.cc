@@ -487,6 +487,13 @@ HcclResult HcclAmdCommScratch(HcclComm comm, void** ptr, uint64_t* bytes)
     return HCCL_SUCCESS;
 }
 
+HcclResult HcclAmdRcclP2pChannels(uint32_t* perPeer, uint32_t* minP2pChannels)
+{
+    if (perPeer == nullptr || minP2pChannels == nullptr) return HCCL_E_PTR;
+    RcclP2pChannels(perPeer, minP2pChannels);
+    return HCCL_SUCCESS;
+}
+
 HcclResult HcclAmdL2Maintain(aclrtStream stream) { return ScrubL2(static_cast<hipStream_t>(stream)); }
 
 HcclResult HcclAmdCommExecute(HcclComm comm,const HcclAmdIrOp* ops, uint64_t numOps, void* sendBuf, void* recvBuf,

@@ -171,6 +171,7 @@ void RelaxCaptureMode()
 
 void Watchdog::Run()
 {
+    RelaxCaptureMode();  // Fire's abort makes HIP calls from this thread
     std::unique_lock<std::mutex> lk(mu_);
     while (!stop_) {
         // a 10 ms poll: no wake-up is paid per collective, and the bound is seconds
@@ -337,9 +338,17 @@ void WaitForReaperAtExit()
 bool DeferDestroy(Comm* c)
 {
     if (!EnvFlag("HCCL_AMD_DEFER_DESTROY", true)) return false;  // diagnostics: tear down at once, as before r03
+    if (c->graphRefs.load(std::memory_order_acquire) == 0) return false;
+    // The collective steps of the teardown run now, on this rank's destroy, as on every peer's: the IPC
+    // rendezvous (after it no peer stores into this rank's staging, nor this rank into theirs), and the transport is
+    // told that its own teardown, later and alone, must not wait on peers. Only the local frees the live graphs
+    // depend on are deferred. (A graph replayed after its communicator's destroy is the caller's error.)
+    TeardownTrace(c->rank, "IPC quiesce (destroy time)", true);
+    IpcQuiesce(*c);
+    if (c->transport != nullptr) c->transport->SetLocalTeardown();
     Reaper& r = TheReaper();
     std::lock_guard<std::mutex> lk(r.mu);
-    if (c->graphRefs.load(std::memory_order_acquire) == 0) return false;
+    if (c->graphRefs.load(std::memory_order_acquire) == 0) return false;  // the last graph went meanwhile
     TeardownTrace(c->rank, "destroy deferred (graphs)", true);
     r.pending.push_back(c);
     if (!r.started) {

@@ -455,3 +455,80 @@ def test_executor_graph_cache_replays_bit_exact():
     assert not [r for r in results if r[-1] == "mismatch"], results
     launches = [r[2] for r in results if len(r) == 3 and r[1] == "graph_launches"]
     assert launches and all(x >= 3 for x in launches), results
+
+
+def _p2p_channels_worker(per_peer, log_dir, q):
+    """One 1-rank RCCL communicator (this process's first): the channel settings the library gave RCCL, what RCCL's
+    INIT log reports, and the self-loop send/recv rate of one 256 MiB message."""
+    try:
+        import re
+        import sys
+        import time
+        sys.path.insert(0, ROOT)
+        if per_peer is not None:
+            os.environ["HCCL_AMD_P2P_CHANNELS_PER_PEER"] = str(per_peer)
+        os.environ["NCCL_DEBUG"] = "INFO"
+        os.environ["NCCL_DEBUG_SUBSYS"] = "INIT"
+        os.environ["NCCL_DEBUG_FILE"] = os.path.join(log_dir, f"rccl_init_{per_peer}.%p.log")
+        import torch
+        import hccl_amd as H
+        torch.cuda.set_device(0)
+        comm = H.comm_init_root_info(1, H.get_root_info(), 0)
+        configured = H.rccl_p2p_channels()
+        n_el = 64 << 20
+        arr = (H.HcclAmdIrOp * 2)(_ir(H.IrKind.SEND, n_el, srcs=[(0, 0)], peer=0, group=0),
+                                  _ir(H.IrKind.RECV, n_el, dst=(1, 0), peer=0, group=0))
+        x = torch.rand(n_el, device="cuda")
+        y = torch.zeros_like(x)
+        s = torch.cuda.Stream()
+        for _ in range(3):
+            comm.execute(arr, 2, x, y, H.HcclReduceOp.SUM, False, s)
+        torch.cuda.synchronize()
+        reps = 10
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            comm.execute(arr, 2, x, y, H.HcclReduceOp.SUM, False, s)
+        torch.cuda.synchronize()
+        gbps = reps * n_el * 4 / (time.perf_counter() - t0) / 1e9
+        ok = torch.equal(x, y)
+        comm.destroy()
+        reported = None
+        for name in os.listdir(log_dir):
+            if name.startswith(f"rccl_init_{per_peer}."):
+                m = re.search(r"p2p channels:(\d+), p2p channels per peer:(\d+)", open(os.path.join(log_dir, name)).read())
+                if m:
+                    reported = (int(m.group(1)), int(m.group(2)))
+        q.put(("ok", {"per_peer_env": per_peer, "configured": configured, "rccl_reported": reported,
+                      "self_loop_GBps": round(gbps, 1), "exact": ok}))
+    except Exception as e:  # noqa: BLE001
+        q.put(("err", f"{type(e).__name__}: {e}\n{traceback.format_exc()}"))
+
+
+def test_rccl_p2p_channels_configured(tmp_path):
+    """the library sets RCCL's per-peer p2p channels before the process's first communicator
+    (default 4 per peer, NCCL_MIN_P2P_NCHANNELS per peer x (n-1) rounded up), and RCCL honours them: its INIT log
+    reports the per-peer count, and the self-loop message rate scales with it (about 43 GB/s per channel, r02)."""
+    rows = []
+    for per_peer in (None, 8):
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        p = ctx.Process(target=_p2p_channels_worker, args=(per_peer, str(tmp_path), q))
+        p.start()
+        try:
+            status, row = q.get(timeout=300)
+        finally:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+        assert status == "ok", row
+        rows.append(row)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "rccl_p2p_channels_configured.jsonl"), "w") as f:
+        for row in rows:
+            f.write(__import__("json").dumps(row) + "\n")
+    default, eight = rows
+    assert default["exact"] and eight["exact"]
+    assert tuple(default["configured"]) == (4, 4) and tuple(eight["configured"]) == (8, 8), rows
+    if default["rccl_reported"] is not None and eight["rccl_reported"] is not None:
+        assert default["rccl_reported"][1] == 4 and eight["rccl_reported"][1] == 8, rows
+    assert eight["self_loop_GBps"] > 1.5 * default["self_loop_GBps"], rows

@@ -121,6 +121,69 @@ def test_rccl_exec_timeout_aborts_and_fails_the_communicator():
     assert res["destroyed_s"] <= 2.0 + 5.0 + 5.0, res
 
 
+def _stall_after_graph_worker(q, env):
+    """the watchdog fires while the communicator's executor graph cache holds a graph (RCCL plans): the
+    abort must not block the next entries or the destroy. Program A (the 8-rank ring program over the self loop) runs
+    three times: eager, captured into the executor graph cache, replayed from it. The injected stall sits at the first
+    transport group after A's eager run, so it stalls program B's first (eager) run with A's graph alive."""
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        import torch
+        import hccl_amd as H
+        from hccl_amd._lib import HcclError, HcclResult
+        from tests.test_gpu_rccl import self_looped
+        count = 7 * 8 * 64 * 512
+        arr, nops, _ = self_looped(H.OpType.ALLREDUCE, int(H.Algo.RING), 8, 0, count, H.HcclDataType.FP32)
+        groups = len({arr[k].group for k in range(nops) if arr[k].kind in (int(H.IrKind.SEND), int(H.IrKind.RECV))})
+        os.environ.update(env)
+        os.environ["HCCL_AMD_INJECT_STALL_GROUP"] = str(groups + 1)
+        torch.cuda.set_device(0)
+        comm = H.comm_init_root_info(1, H.get_root_info(), 0)
+        x = torch.rand(count, device="cuda")
+        y = torch.empty_like(x)
+        s = torch.cuda.Stream()
+        for _ in range(3):
+            comm.execute(arr, nops, x, y, H.HcclReduceOp.SUM, False, s)
+        torch.cuda.synchronize()
+        res = {"groups_a": groups, "graphs": comm.graph_stats()}
+        arr_b, nops_b, _ = self_looped(H.OpType.ALLREDUCE, int(H.Algo.RING), 8, 0, count // 2, H.HcclDataType.FP32)
+        t0 = time.time()
+        comm.execute(arr_b, nops_b, x, y, H.HcclReduceOp.SUM, False, s)  # its first group stalls
+        while comm.async_error() == 0 and time.time() - t0 < 12:
+            time.sleep(0.05)
+        res["async_error"] = HcclResult(comm.async_error()).name
+        res["detected_s"] = time.time() - t0
+        codes = []
+        for _ in range(2):
+            try:
+                comm.execute(arr, nops, x, y, H.HcclReduceOp.SUM, False, s)
+                codes.append("HCCL_SUCCESS")
+            except HcclError as e:
+                codes.append(HcclResult(e.code).name)
+        res["next_entries"] = codes
+        res["next_entries_s"] = time.time() - t0
+        torch.cuda.synchronize()
+        res["drained_s"] = time.time() - t0
+        comm.destroy()
+        res["destroyed_s"] = time.time() - t0
+        q.put(("ok", res))
+    except Exception as e:  # noqa: BLE001
+        q.put(("err", f"{type(e).__name__}: {e}\n{traceback.format_exc()}"))
+
+
+def test_rccl_exec_timeout_with_a_cached_executor_graph():
+    res = _child(_stall_after_graph_worker, {"HCCL_EXEC_TIMEOUT": "2", "HCCL_AMD_TEARDOWN_TRACE": "1"}, wait=120,
+                 clean_exit=True)
+    print(res)
+    assert res["graphs"][1] >= 1, res  # A's graph was captured and is held by the cache
+    assert res["async_error"] == "HCCL_E_TIMEOUT", res
+    assert 2.0 <= res["detected_s"] <= 2.0 + 5.0, res
+    assert res["next_entries"] == ["HCCL_E_TIMEOUT", "HCCL_E_SUSPENDING"], res
+    assert res["next_entries_s"] <= 2.0 + 5.0 + 1.0, res
+    assert res["destroyed_s"] <= 2.0 + 5.0 + 10.0, res
+
+
 def _connect_worker(q, env):
     try:
         os.environ.update(env)
