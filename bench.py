@@ -272,7 +272,7 @@ def fold_roofline(dev, stream, n: int = 8, reps: int = 10) -> dict:
             "kernel_avg_us": round(kavg * 1e6, 1), "kernel_median_us": round(float(np.median(per)) * 1e6, 1),
             "achieved_GBps": round(nbytes / kavg / 1e9, 1), "peak_GBps": HBM_PEAK_GBPS,
             "frac": round(nbytes / kavg / 1e9 / HBM_PEAK_GBPS, 4),
-            "traffic": load_pmc_traffic("r03d_pmc_fold_n8.json") or load_pmc_traffic("r03c_pmc_fold_n8.json"),
+            "traffic": load_pmc_traffic("r04_pmc_fold_n8.json") or load_pmc_traffic("r03d_pmc_fold_n8.json"),
             "result_ok": ok}
 
 
@@ -342,7 +342,7 @@ def ipc_two_shot_roofline(dev, n: int = 2, mib: int = 512, reps: int = 10) -> di
             "call_to_call_avg_us": round(float(np.mean(per_call)) * 1e6, 1),
             "achieved_GBps": round(nbytes / kavg / 1e9, 1), "peak_GBps": HBM_PEAK_GBPS,
             "frac": round(nbytes / kavg / 1e9 / HBM_PEAK_GBPS, 4),
-            "traffic": load_pmc_traffic("r03d_pmc_ipc_two_shot.json") or load_pmc_traffic("r03c_pmc_ipc_two_shot.json"),
+            "traffic": load_pmc_traffic("r04_pmc_ipc_two_shot.json") or load_pmc_traffic("r03d_pmc_ipc_two_shot.json"),
             "barrier_timeouts": timeouts,
             "result_ok": ok}
 
@@ -406,7 +406,7 @@ def bench_local(args) -> dict:
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": load_pmc_traffic("r03d_pmc_local_reduce.json") or load_pmc_traffic("r03c_pmc_local_reduce.json"),
+            "traffic": load_pmc_traffic("r04_pmc_local_reduce.json") or load_pmc_traffic("r03d_pmc_local_reduce.json"),
             "kernel": "k_reduce2<EFp<float>, SUM>",
             "algorithmic_bytes_per_launch": bytes_step,
             "kernel_avg_us": round(kavg * 1e6, 2),
@@ -852,13 +852,14 @@ def _capture_rccl_init(rank: int) -> None:
     import tempfile
     _RCCL_INIT_LOG = os.path.join(tempfile.gettempdir(), f"hccl_amd_rccl_init_r{rank}.%p.log")
     os.environ["NCCL_DEBUG"] = "INFO"
-    os.environ["NCCL_DEBUG_SUBSYS"] = "INIT"
+    os.environ["NCCL_DEBUG_SUBSYS"] = "INIT"  # not COLL: that logs every call and would load the timed loop
     os.environ["NCCL_DEBUG_FILE"] = _RCCL_INIT_LOG
 
 
 def _p2p_channels_info() -> dict:
     """The per-peer p2p channels the library configured (HcclAmdRcclP2pChannels) and what RCCL's INIT log reported
-    for this rank's communicators ("p2p channels:%d, p2p channels per peer:%d")."""
+    for this rank's communicators ("%d p2p channels, %d p2p channels per peer"; RCCL reports twice the per-peer
+    setting: 8 for NCCL_NCHANNELS_PER_PEER=4, profiles/r04_rccl_init_log_probe.txt)."""
     import re
     out = {}
     try:
@@ -871,7 +872,7 @@ def _p2p_channels_info() -> dict:
         try:
             txt = open(path).read()
             rep = [{"p2p_channels": int(a), "per_peer": int(b)}
-                   for a, b in re.findall(r"p2p channels:(\d+), p2p channels per peer:(\d+)", txt)]
+                   for a, b in re.findall(r"(\d+) p2p channels, (\d+) p2p channels per peer", txt)]
             out["rccl_reported"] = rep[:4]
         except OSError as e:
             out["rccl_reported"] = {"error": str(e)}

@@ -80,9 +80,8 @@ HcclResult IpcSetup(Comm& c)
     // One allocation [in][results][alternate 0][alternate 1], below 2 GiB: hipIpcOpenMemHandle never returned for a
     // 2 GiB allocation on this stack (the r03 512 MiB areas in one 2 GiB block hung the rank-mode set-up;
     // tools/probe_ipc_open.py, profiles/r03_probe_ipc_open*.jsonl: up to 2047 MiB opens in < 1 ms and is written
-    // through whole, 2048 MiB does not return). Four allocations of one area each set up fine but changed which pages a
-    // later executor run reused, and the GPU suite's 4-rank loopback run after an IPC call then read stale 128-B lines
-    // (DESIGN.md §5b); the one block keeps the layout every earlier round ran.
+    // through whole, 2048 MiB does not return). (The stale lines r03 saw after changing this layout were the loopback
+    // link's hipMemcpyAsync, not the layout: DESIGN.md §5b, root cause.)
     const uint64_t stgBytes = s.stgInBytes + s.stgResBytes + 2 * s.stgAltBytes;
     void* base = nullptr;
     bool ok = (cached ? hipMalloc(&base, stgBytes) : hipExtMallocWithFlags(&base, stgBytes, hipDeviceMallocUncached)) ==

@@ -183,7 +183,8 @@ __device__ __forceinline__ void FoldTile(u32x4 (&acc)[U], const SrcPack& srcs, i
 }
 
 // One ordered fold over `nvec` 16-B vectors (plus scalar edges), worked by `nblocks` workgroups, this one `bid`.
-template <class E, int OP, int U, int NT, int MODE = 0, int NS = 0>
+// ORD 0: tiles dealt round-robin over the grid; ORD 1: each workgroup folds one contiguous run of tiles.
+template <class E, int OP, int U, int NT, int MODE = 0, int NS = 0, int ORD = 0>
 __device__ __forceinline__ void ReduceNBody(typename E::S* out, const SrcPack& srcs, int nsrc, uint64_t nvec,
                                             Edges edges, uint32_t bid, uint32_t nblocks)
 {
@@ -191,7 +192,11 @@ __device__ __forceinline__ void ReduceNBody(typename E::S* out, const SrcPack& s
     constexpr uint64_t kTile = uint64_t(kBlock) * U;
     u32x4* vout = reinterpret_cast<u32x4*>(out + edges.head);
     const uint64_t fullTiles = nvec / kTile;
-    for (uint64_t t = bid; t < fullTiles; t += nblocks) {
+    const uint64_t per = ORD == 0 ? 0 : (fullTiles + nblocks - 1) / nblocks;
+    const uint64_t tBegin = ORD == 0 ? bid : uint64_t(bid) * per;
+    const uint64_t tEnd = ORD == 0 ? fullTiles : (tBegin + per < fullTiles ? tBegin + per : fullTiles);
+    const uint64_t tStep = ORD == 0 ? nblocks : 1;
+    for (uint64_t t = tBegin; t < tEnd; t += tStep) {
         const uint64_t base = t * kTile + threadIdx.x;
         u32x4 acc[U];
         FoldTile<E, OP, U, NT, MODE, NS>(acc, srcs, nsrc, edges, base);
@@ -230,11 +235,11 @@ __device__ __forceinline__ void ReduceNBody(typename E::S* out, const SrcPack& s
     }
 }
 
-template <class E, int OP, int U, int NT, int MODE = 0, int NS = 0>
+template <class E, int OP, int U, int NT, int MODE = 0, int NS = 0, int ORD = 0>
 __global__ __launch_bounds__(kBlock) void k_reduceN(typename E::S* out, SrcPack srcs, int nsrc, uint64_t nvec,
                                                       Edges edges)
 {
-    ReduceNBody<E, OP, U, NT, MODE, NS>(out, srcs, nsrc, nvec, edges, blockIdx.x, gridDim.x);
+    ReduceNBody<E, OP, U, NT, MODE, NS, ORD>(out, srcs, nsrc, nvec, edges, blockIdx.x, gridDim.x);
 }
 
 // A batch of independent folds (one schedule step's), in one of two layouts chosen by segment size (RunBatch):
@@ -436,13 +441,13 @@ hipError_t Run2Variant(void* out, const void* src, const void* dst, uint64_t nve
     return hipGetLastError();
 }
 
-template <class E, int OP, int U, int NT, int MODE = 0, int NS = 0>
+template <class E, int OP, int U, int NT, int MODE = 0, int NS = 0, int ORD = 0>
 hipError_t RunNVariant(void* out, const SrcPack& pk, int n, uint64_t nvec, Edges edges, uint32_t grid,
                        hipStream_t stream)
 {
     using S = typename E::S;
-    hipLaunchKernelGGL((k_reduceN<E, OP, U, NT, MODE, NS>), dim3(grid), dim3(kBlock), 0, stream, static_cast<S*>(out),
-                       pk, n, nvec, edges);
+    hipLaunchKernelGGL((k_reduceN<E, OP, U, NT, MODE, NS, ORD>), dim3(grid), dim3(kBlock), 0, stream,
+                       static_cast<S*>(out), pk, n, nvec, edges);
     return hipGetLastError();
 }
 
@@ -544,6 +549,14 @@ hipError_t RunN(void* out, const void* const* srcs, uint32_t n, uint64_t count, 
                 case 8 + 3: return RunNMode<E, OP, 2, 3>(out, pk, int(n), nvec, edges, grid, stream);
                 case 16 + 2: return RunNMode<E, OP, 4, 2>(out, pk, int(n), nvec, edges, grid, stream);
                 case 16 + 3: return RunNMode<E, OP, 4, 3>(out, pk, int(n), nvec, edges, grid, stream);
+                default: return hipErrorInvalidValue;
+            }
+        }
+        if (cfg.order == 1 && cfg.nt == 3) {  // SetReduceLaunch cache policy 5: contiguous tile runs (A/B)
+            switch (cfg.unroll) {
+                case 1: return RunNVariant<E, OP, 1, 3, 0, 0, 1>(out, pk, int(n), nvec, edges, grid, stream);
+                case 2: return RunNVariant<E, OP, 2, 3, 0, 0, 1>(out, pk, int(n), nvec, edges, grid, stream);
+                case 4: return RunNVariant<E, OP, 4, 3, 0, 0, 1>(out, pk, int(n), nvec, edges, grid, stream);
                 default: return hipErrorInvalidValue;
             }
         }
@@ -805,17 +818,30 @@ HcclResult LaunchReduceNBatch(const FoldSeg* segs, uint32_t nseg, uint32_t nsrc,
 
 namespace {
 
-// dst[0, bytes) = src[0, bytes): 16-B vectors over the aligned body (plain loads and stores, grid-stride), bytes at
+// dst[0, bytes) = src[0, bytes): 16-B vectors over the aligned body, kCopyU per lane in flight (loads first, then
+// stores; non-temporal both ways like the reduce kernels), over a persistent grid of tiles dealt round-robin; bytes at
 // the ragged ends. A kernel of this library, so the copy's stores are ordered before the next kernel of the stream by
-// the ordinary end-of-kernel release like every other kernel here (device copies).
+// the ordinary end-of-kernel release like every other kernel here (root cause of the stale operands).
+constexpr int kCopyU = 4;
+
 __global__ __launch_bounds__(256) void k_copy_bytes(unsigned char* dst, const unsigned char* src, uint64_t head,
                                                     uint64_t nvec, uint64_t bytes)
 {
-    const uint64_t tid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
     const u32x4* s = reinterpret_cast<const u32x4*>(src + head);
     u32x4* d = reinterpret_cast<u32x4*>(dst + head);
-    for (uint64_t i = tid; i < nvec; i += stride) d[i] = s[i];
+    constexpr uint64_t kTile = uint64_t(256) * kCopyU;
+    const uint64_t fullTiles = nvec / kTile;
+    for (uint64_t t = blockIdx.x; t < fullTiles; t += gridDim.x) {
+        const uint64_t base = t * kTile + threadIdx.x;
+        u32x4 x[kCopyU];
+#pragma unroll
+        for (int u = 0; u < kCopyU; ++u) x[u] = ld<3>(s + base + u * 256);
+#pragma unroll
+        for (int u = 0; u < kCopyU; ++u) st<3>(d + base + u * 256, x[u]);
+    }
+    const uint64_t tid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = fullTiles * kTile + tid; i < nvec; i += stride) d[i] = s[i];
     for (uint64_t i = tid; i < head; i += stride) dst[i] = src[i];
     for (uint64_t i = head + nvec * 16 + tid; i < bytes; i += stride) dst[i] = src[i];
 }
@@ -843,8 +869,13 @@ HcclResult LaunchCopyBytes(void* dst, const void* src, uint64_t bytes, hipStream
     } else {
         head = bytes;  // no common 16-B phase: bytewise
     }
+    // One tile per workgroup up to 16 tiles per CU (latency-bound sizes: 16 MiB ran 8.96 us on a 2-per-CU persistent
+    // grid against hipMemcpyAsync's 7.88, profiles/r04_copy_kernel.jsonl); beyond that a persistent grid of two
+    // workgroups per CU, the reduce kernels' measured best (1 GiB: 410 us = 5.23 TB/s against hipMemcpyAsync's 455).
     const uint64_t work = nvec != 0 ? nvec : bytes;
-    const uint64_t blocks = std::min<uint64_t>(2048, std::max<uint64_t>(1, (work + 4 * 256 - 1) / (4 * 256)));
+    const uint64_t tiles = std::max<uint64_t>(1, (work + 256 * kCopyU - 1) / (256 * kCopyU));
+    const uint64_t cus = uint64_t(CuCount());
+    const uint64_t blocks = tiles <= cus * 16 ? tiles : cus * 2;
     hipLaunchKernelGGL(k_copy_bytes, dim3(uint32_t(blocks)), dim3(256), 0, stream, static_cast<unsigned char*>(dst),
                        static_cast<const unsigned char*>(src), head, nvec, bytes);
     HIP_CHK(hipGetLastError());

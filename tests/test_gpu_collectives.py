@@ -342,11 +342,9 @@ def _stale_line_bait(mib=9):
 
 
 def test_ipc_staging_survives_recycled_cached_pages():
-    """Fresh uncached IPC staging right after a destroyed world released its cached staging. Context: in the suite
-    order (bootstrap, IPC, executor-loop and auto-family tests) an 8-rank two-shot IPC AllReduce returned a few hundred
-    to a few thousand elements with one stale operand in the owner's fold, on every rank alike, in 4 of 5 runs without
-    the L2 scrub of IpcSetup and in none of 4 with it. This test repeats the destroy-then-create pattern; it did not
-    reproduce the failure by itself, so it is a guard, not the proof."""
+    """Fresh uncached IPC staging right after a destroyed world released its cached staging. Context: r01's suite
+    order made an 8-rank two-shot IPC AllReduce return a few stale operand lines in the owner's fold (fixed in r02: the
+    barrier's dropped write-back wait). This test repeats the destroy-then-create pattern as a guard."""
     n, count = 8, (9 << 20) // 4 + 3
     xs = [O.random_operands(O.FP32, count, seed=530 + r, edge=False) for r in range(n)]
     want = R.expected(AR, R.ALGO_TWOSHOT, O.FP32, O.SUM, xs, count)

@@ -468,7 +468,7 @@ def _p2p_channels_worker(per_peer, log_dir, q):
         if per_peer is not None:
             os.environ["HCCL_AMD_P2P_CHANNELS_PER_PEER"] = str(per_peer)
         os.environ["NCCL_DEBUG"] = "INFO"
-        os.environ["NCCL_DEBUG_SUBSYS"] = "INIT"
+        os.environ["NCCL_DEBUG_SUBSYS"] = "INIT"  # bench.py's setting
         os.environ["NCCL_DEBUG_FILE"] = os.path.join(log_dir, f"rccl_init_{per_peer}.%p.log")
         import torch
         import hccl_amd as H
@@ -495,7 +495,7 @@ def _p2p_channels_worker(per_peer, log_dir, q):
         reported = None
         for name in os.listdir(log_dir):
             if name.startswith(f"rccl_init_{per_peer}."):
-                m = re.search(r"p2p channels:(\d+), p2p channels per peer:(\d+)", open(os.path.join(log_dir, name)).read())
+                m = re.search(r"(\d+) p2p channels, (\d+) p2p channels per peer", open(os.path.join(log_dir, name)).read())
                 if m:
                     reported = (int(m.group(1)), int(m.group(2)))
         q.put(("ok", {"per_peer_env": per_peer, "configured": configured, "rccl_reported": reported,
@@ -529,6 +529,7 @@ def test_rccl_p2p_channels_configured(tmp_path):
     default, eight = rows
     assert default["exact"] and eight["exact"]
     assert tuple(default["configured"]) == (4, 4) and tuple(eight["configured"]) == (8, 8), rows
-    if default["rccl_reported"] is not None and eight["rccl_reported"] is not None:
-        assert default["rccl_reported"][1] == 4 and eight["rccl_reported"][1] == 8, rows
+    # RCCL's own summary ("%d p2p channels, %d p2p channels per peer") reports twice the per-peer setting
+    assert default["rccl_reported"] is not None and eight["rccl_reported"] is not None, rows
+    assert eight["rccl_reported"][1] == 2 * default["rccl_reported"][1], rows
     assert eight["self_loop_GBps"] > 1.5 * default["self_loop_GBps"], rows
