@@ -381,25 +381,23 @@ uint32_t Pow2Up(uint32_t x)
 // (profiles/r02_rccl_p2p_channels_selfloop.jsonl: 176 / 345 / 650 GB/s at 4 / 8 / 16 channels per peer), below one
 // 76.8 GB/s xGMI link per direction (cost_model.cc:78-79 prices the reference's links the same way). Left to RCCL's
 // topology defaults a peer may get fewer channels than its link needs; the reference sizes its channels per link
-// explicitly (alg_param.h:434-448). So before the process's first RCCL communicator: NCCL_NCHANNELS_PER_PEER =
-// HCCL_AMD_P2P_CHANNELS_PER_PEER (default 4, about twice a link) and NCCL_MIN_P2P_NCHANNELS = per peer x (n - 1)
-// rounded up to a power of two (at most 64), so every peer's channels are distinct. A value the user already set wins.
-// RCCL reads these once per process, so the first communicator's size decides; HcclAmdRcclP2pChannels reports them.
-void ConfigureRcclP2pChannels(uint32_t nRanks)
+// explicitly (alg_param.h:434-448). So NCCL_NCHANNELS_PER_PEER = HCCL_AMD_P2P_CHANNELS_PER_PEER (default 4, about twice
+// a link) and NCCL_MIN_P2P_NCHANNELS = per peer x 7 (the peers of an 8-GPU node) rounded up to a power of two, at most
+// 64, so every peer's channels are distinct. A value the caller already set wins. RCCL reads them once per process, at
+// its first communicator, so they are set when this library is loaded, while the process has no thread of ours that
+// could read the environment concurrently (setenv is not thread-safe); they then apply to every RCCL communicator of
+// the process, this library's or not. HcclAmdRcclP2pChannels reports them.
+__attribute__((constructor)) void ConfigureRcclP2pChannels()
 {
-    static std::once_flag once;
-    std::call_once(once, [nRanks] {
-        const uint32_t per = Pow2Up(EnvU32("HCCL_AMD_P2P_CHANNELS_PER_PEER", 4));
-        if (std::getenv("NCCL_NCHANNELS_PER_PEER") == nullptr) {
-            setenv("NCCL_NCHANNELS_PER_PEER", std::to_string(per).c_str(), 0);
-        }
-        if (std::getenv("NCCL_MIN_P2P_NCHANNELS") == nullptr) {
-            const uint32_t mn = std::min<uint32_t>(64, Pow2Up(per * std::max<uint32_t>(1, nRanks - 1)));
-            setenv("NCCL_MIN_P2P_NCHANNELS", std::to_string(mn).c_str(), 0);
-        }
-        g_p2pPerPeer = EnvU32("NCCL_NCHANNELS_PER_PEER", 0);
-        g_p2pMin = EnvU32("NCCL_MIN_P2P_NCHANNELS", 0);
-    });
+    const uint32_t per = Pow2Up(EnvU32("HCCL_AMD_P2P_CHANNELS_PER_PEER", 4));
+    if (std::getenv("NCCL_NCHANNELS_PER_PEER") == nullptr) {
+        setenv("NCCL_NCHANNELS_PER_PEER", std::to_string(per).c_str(), 0);
+    }
+    if (std::getenv("NCCL_MIN_P2P_NCHANNELS") == nullptr) {
+        setenv("NCCL_MIN_P2P_NCHANNELS", std::to_string(std::min<uint32_t>(64, Pow2Up(per * 7))).c_str(), 0);
+    }
+    g_p2pPerPeer = EnvU32("NCCL_NCHANNELS_PER_PEER", 0);
+    g_p2pMin = EnvU32("NCCL_MIN_P2P_NCHANNELS", 0);
 }
 
 void RcclP2pChannels(uint32_t* perPeer, uint32_t* minP2p)
@@ -410,7 +408,6 @@ void RcclP2pChannels(uint32_t* perPeer, uint32_t* minP2p)
 
 std::unique_ptr<Transport> MakeRcclTransport(void* uniqueId, uint32_t nRanks, uint32_t rank, HcclResult* err)
 {
-    ConfigureRcclP2pChannels(nRanks);
     ncclUniqueId id;
     std::memcpy(&id, uniqueId, sizeof id);
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
@@ -437,7 +434,6 @@ HcclResult MakeRcclTransportsAll(uint32_t ndev, const int32_t* devices, std::vec
 {
     // ncclCommInitAll's steps, with the communicators' config: one unique id, ncclCommInitRankConfig per device in a
     // group.
-    ConfigureRcclP2pChannels(ndev);
     ncclUniqueId id;
     HCCL_CHK(FromNccl(ncclGetUniqueId(&id), "ncclGetUniqueId"));
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;

@@ -65,8 +65,7 @@ std::unique_ptr<Transport> MakeRcclTransport(void* uniqueId, uint32_t nRanks, ui
 // One RCCL communicator per listed device, all in this process (ncclCommInitAll); (*out)[r] is rank r.
 HcclResult MakeRcclTransportsAll(uint32_t ndev, const int32_t* devices, std::vector<std::unique_ptr<Transport>>* out);
 HcclResult RcclGetUniqueId(void* id128);
-// RCCL's per-peer p2p channels, set in the environment before the process's first RCCL communicator (comm.cc).
-void ConfigureRcclP2pChannels(uint32_t nRanks);
+// RCCL's per-peer p2p channels, set in the environment when the library is loaded (comm.cc).
 void RcclP2pChannels(uint32_t* perPeer, uint32_t* minP2p);
 
 class LoopbackWorld;

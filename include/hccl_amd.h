@@ -277,11 +277,11 @@ extern HcclResult HcclAmdHostProfile(uint64_t* ns, uint64_t* calls, uint32_t n, 
 /* Communicators whose HcclCommDestroy is waiting for the graphs captured on them to be destroyed. */
 extern uint32_t HcclAmdCommPendingDestroys(void);
 
-/* RCCL's p2p channel settings this process's RCCL communicators were created with: *perPeer =
- * NCCL_NCHANNELS_PER_PEER, *minP2pChannels = NCCL_MIN_P2P_NCHANNELS (0 before the first RCCL communicator). Unless the
- * environment already sets them, the library sets them before that communicator: HCCL_AMD_P2P_CHANNELS_PER_PEER
- * (default 4: RCCL's p2p kernel streams about 43 GB/s per channel, an xGMI link 76.8 GB/s per direction) and per peer
- * x (nRanks - 1) rounded up to a power of two, at most 64. RCCL reads them once per process. */
+/* RCCL's p2p channel settings of this process: *perPeer = NCCL_NCHANNELS_PER_PEER, *minP2pChannels =
+ * NCCL_MIN_P2P_NCHANNELS. Unless the environment already sets them, the library sets them when it is loaded (RCCL reads
+ * them once, at the process's first communicator, whoever creates it): HCCL_AMD_P2P_CHANNELS_PER_PEER (default 4: RCCL's
+ * p2p kernel streams about 43 GB/s per channel, an xGMI link 76.8 GB/s per direction) and per peer x 7 (an 8-GPU
+ * node's peers) rounded up to a power of two, at most 64. Child processes inherit them. */
 extern HcclResult HcclAmdRcclP2pChannels(uint32_t* perPeer, uint32_t* minP2pChannels);
 
 /* The executor staging of comm (diagnostics): *ptr = its device address (NULL until allocated), *bytes = its size. */

@@ -465,6 +465,9 @@ def _p2p_channels_worker(per_peer, log_dir, q):
         import sys
         import time
         sys.path.insert(0, ROOT)
+        # the parent's library load already set these in its C environment, which a spawned child inherits
+        os.environ.pop("NCCL_NCHANNELS_PER_PEER", None)
+        os.environ.pop("NCCL_MIN_P2P_NCHANNELS", None)
         if per_peer is not None:
             os.environ["HCCL_AMD_P2P_CHANNELS_PER_PEER"] = str(per_peer)
         os.environ["NCCL_DEBUG"] = "INFO"
@@ -505,9 +508,10 @@ def _p2p_channels_worker(per_peer, log_dir, q):
 
 
 def test_rccl_p2p_channels_configured(tmp_path):
-    """the library sets RCCL's per-peer p2p channels before the process's first communicator
-    (default 4 per peer, NCCL_MIN_P2P_NCHANNELS per peer x (n-1) rounded up), and RCCL honours them: its INIT log
-    reports the per-peer count, and the self-loop message rate scales with it (about 43 GB/s per channel, r02)."""
+    """the library sets RCCL's per-peer p2p channels when it is loaded, before any RCCL
+    communicator (default 4 per peer, NCCL_MIN_P2P_NCHANNELS = per peer x 7 rounded up), and RCCL honours them: its
+    INIT log reports the per-peer count (twice the setting), and the self-loop message rate scales with it (about
+    43 GB/s per channel, r02)."""
     rows = []
     for per_peer in (None, 8):
         ctx = mp.get_context("spawn")
@@ -528,7 +532,7 @@ def test_rccl_p2p_channels_configured(tmp_path):
             f.write(__import__("json").dumps(row) + "\n")
     default, eight = rows
     assert default["exact"] and eight["exact"]
-    assert tuple(default["configured"]) == (4, 4) and tuple(eight["configured"]) == (8, 8), rows
+    assert tuple(default["configured"]) == (4, 32) and tuple(eight["configured"]) == (8, 64), rows
     # RCCL's own summary ("%d p2p channels, %d p2p channels per peer") reports twice the per-peer setting
     assert default["rccl_reported"] is not None and eight["rccl_reported"] is not None, rows
     assert eight["rccl_reported"][1] == 2 * default["rccl_reported"][1], rows
