@@ -818,32 +818,95 @@ HcclResult LaunchReduceNBatch(const FoldSeg* segs, uint32_t nseg, uint32_t nsrc,
 
 namespace {
 
-// dst[0, bytes) = src[0, bytes): 16-B vectors over the aligned body, kCopyU per lane in flight (loads first, then
-// stores; non-temporal both ways like the reduce kernels), over a persistent grid of tiles dealt round-robin; bytes at
-// the ragged ends. A kernel of this library, so the copy's stores are ordered before the next kernel of the stream by
-// the ordinary end-of-kernel release like every other kernel here (root cause of the stale operands).
+// dst[0, bytes) = src[0, bytes) in units of W bytes (W = the widest of 16, 8, 4, 2, 1 in which dst and src share their
+// alignment phase: every schedule's copy is at least element-aligned, and 16 B whenever its offsets are): kCopyU units
+// per lane in flight (loads first, then stores; non-temporal both ways, like the reduce kernels) over a grid of tiles
+// dealt round-robin; the ragged head (before dst reaches a W boundary) and tail bytes one by one. A kernel of this
+// library, so the copy's stores are ordered before the next kernel of the stream by the ordinary end-of-kernel release
+// like every other kernel here (root cause of the stale operands).
 constexpr int kCopyU = 4;
 
-__global__ __launch_bounds__(256) void k_copy_bytes(unsigned char* dst, const unsigned char* src, uint64_t head,
-                                                    uint64_t nvec, uint64_t bytes)
+template <int W>
+struct CopyUnit;
+template <>
+struct CopyUnit<16> {
+    using T = u32x4;
+};
+template <>
+struct CopyUnit<8> {
+    using T = uint64_t;
+};
+template <>
+struct CopyUnit<4> {
+    using T = uint32_t;
+};
+template <>
+struct CopyUnit<2> {
+    using T = uint16_t;
+};
+template <>
+struct CopyUnit<1> {
+    using T = unsigned char;
+};
+
+template <int W>
+__device__ __forceinline__ typename CopyUnit<W>::T CopyLd(const typename CopyUnit<W>::T* p)
 {
-    const u32x4* s = reinterpret_cast<const u32x4*>(src + head);
-    u32x4* d = reinterpret_cast<u32x4*>(dst + head);
+    if constexpr (W == 16) {
+        return ld<3>(p);
+    } else {
+        return __builtin_nontemporal_load(p);
+    }
+}
+
+template <int W>
+__device__ __forceinline__ void CopySt(typename CopyUnit<W>::T* p, typename CopyUnit<W>::T v)
+{
+    if constexpr (W == 16) {
+        st<3>(p, v);
+    } else {
+        __builtin_nontemporal_store(v, p);
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void k_copy_units(unsigned char* dst, const unsigned char* src, uint64_t head,
+                                                    uint64_t nunits, uint64_t bytes)
+{
+    using T = typename CopyUnit<W>::T;
+    const T* s = reinterpret_cast<const T*>(src + head);
+    T* d = reinterpret_cast<T*>(dst + head);
     constexpr uint64_t kTile = uint64_t(256) * kCopyU;
-    const uint64_t fullTiles = nvec / kTile;
+    const uint64_t fullTiles = nunits / kTile;
     for (uint64_t t = blockIdx.x; t < fullTiles; t += gridDim.x) {
         const uint64_t base = t * kTile + threadIdx.x;
-        u32x4 x[kCopyU];
+        T x[kCopyU];
 #pragma unroll
-        for (int u = 0; u < kCopyU; ++u) x[u] = ld<3>(s + base + u * 256);
+        for (int u = 0; u < kCopyU; ++u) x[u] = CopyLd<W>(s + base + u * 256);
 #pragma unroll
-        for (int u = 0; u < kCopyU; ++u) st<3>(d + base + u * 256, x[u]);
+        for (int u = 0; u < kCopyU; ++u) CopySt<W>(d + base + u * 256, x[u]);
     }
     const uint64_t tid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-    for (uint64_t i = fullTiles * kTile + tid; i < nvec; i += stride) d[i] = s[i];
+    for (uint64_t i = fullTiles * kTile + tid; i < nunits; i += stride) d[i] = s[i];
     for (uint64_t i = tid; i < head; i += stride) dst[i] = src[i];
-    for (uint64_t i = head + nvec * 16 + tid; i < bytes; i += stride) dst[i] = src[i];
+    for (uint64_t i = head + nunits * W + tid; i < bytes; i += stride) dst[i] = src[i];
+}
+
+template <int W>
+hipError_t RunCopy(unsigned char* dst, const unsigned char* src, uint64_t bytes, hipStream_t stream)
+{
+    const uint64_t mis = (W - (reinterpret_cast<uintptr_t>(dst) & (W - 1))) & (W - 1);
+    const uint64_t head = std::min<uint64_t>(bytes, mis);
+    const uint64_t nunits = (bytes - head) / W;
+    // One tile per workgroup up to 16 tiles per CU (latency-bound sizes: 16 MiB ran 8.96 us on a 2-per-CU persistent
+    // grid against hipMemcpyAsync's 7.88, profiles/r04_copy_kernel.jsonl); beyond that a persistent grid of two
+    // workgroups per CU, the reduce kernels' measured best (1 GiB: 356-410 us against hipMemcpyAsync's 417-455).
+    const uint64_t tiles = std::max<uint64_t>(1, (std::max<uint64_t>(nunits, 1) + 256 * kCopyU - 1) / (256 * kCopyU));
+    const uint64_t cus = uint64_t(CuCount());
+    const uint64_t blocks = tiles <= cus * 16 ? tiles : cus * 2;
+    hipLaunchKernelGGL((k_copy_units<W>), dim3(uint32_t(blocks)), dim3(256), 0, stream, dst, src, head, nunits, bytes);
+    return hipGetLastError();
 }
 
 }  // namespace
@@ -861,24 +924,25 @@ HcclResult LaunchCopyBytes(void* dst, const void* src, uint64_t bytes, hipStream
         HIP_CHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream));
         return HCCL_SUCCESS;
     }
-    const uintptr_t a = reinterpret_cast<uintptr_t>(dst), b = reinterpret_cast<uintptr_t>(src);
-    uint64_t head = 0, nvec = 0;
-    if ((a & 15u) == (b & 15u)) {
-        head = std::min<uint64_t>(bytes, (16 - (a & 15u)) & 15u);
-        nvec = (bytes - head) / 16;
+    auto* d = static_cast<unsigned char*>(dst);
+    const auto* sp = static_cast<const unsigned char*>(src);
+    const uintptr_t x = reinterpret_cast<uintptr_t>(dst) ^ reinterpret_cast<uintptr_t>(src);  // phase difference
+    hipError_t e;
+    if ((x & 15u) == 0) {
+        e = RunCopy<16>(d, sp, bytes, stream);
+    } else if ((x & 7u) == 0) {
+        e = RunCopy<8>(d, sp, bytes, stream);
+    } else if ((x & 3u) == 0) {
+        e = RunCopy<4>(d, sp, bytes, stream);
+    } else if ((x & 1u) == 0) {
+        e = RunCopy<2>(d, sp, bytes, stream);
     } else {
-        head = bytes;  // no common 16-B phase: bytewise
+        e = RunCopy<1>(d, sp, bytes, stream);
     }
-    // One tile per workgroup up to 16 tiles per CU (latency-bound sizes: 16 MiB ran 8.96 us on a 2-per-CU persistent
-    // grid against hipMemcpyAsync's 7.88, profiles/r04_copy_kernel.jsonl); beyond that a persistent grid of two
-    // workgroups per CU, the reduce kernels' measured best (1 GiB: 410 us = 5.23 TB/s against hipMemcpyAsync's 455).
-    const uint64_t work = nvec != 0 ? nvec : bytes;
-    const uint64_t tiles = std::max<uint64_t>(1, (work + 256 * kCopyU - 1) / (256 * kCopyU));
-    const uint64_t cus = uint64_t(CuCount());
-    const uint64_t blocks = tiles <= cus * 16 ? tiles : cus * 2;
-    hipLaunchKernelGGL(k_copy_bytes, dim3(uint32_t(blocks)), dim3(256), 0, stream, static_cast<unsigned char*>(dst),
-                       static_cast<const unsigned char*>(src), head, nvec, bytes);
-    HIP_CHK(hipGetLastError());
+    if (e != hipSuccess) {
+        HCCL_AMD_ERR("copy launch failed: %s", hipGetErrorString(e));
+        return HCCL_E_RUNTIME;
+    }
     return HCCL_SUCCESS;
 }
 

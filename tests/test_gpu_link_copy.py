@@ -40,10 +40,11 @@ def test_r03_failing_order_passes_with_kernel_copies(fence):
 
 
 @pytest.mark.parametrize("nbytes", [1, 15, 16, 17, 4099, (1 << 20) + 5, (64 << 20) + 3])
-@pytest.mark.parametrize("shift", [(0, 0), (3, 3), (1, 6), (0, 8)])
+@pytest.mark.parametrize("shift", [(0, 0), (3, 3), (1, 6), (0, 8), (2, 6), (0, 2), (5, 9)])
 def test_device_copy_kernel_bytes(nbytes, shift):
     """LaunchCopyBytes (reached through HcclAmdLocalReduceN with one source, the single-operand fold): every byte
-    copied, none outside the range, for aligned, equally misaligned and differently phased pointers."""
+    copied, none outside the range, for aligned, equally misaligned and differently phased pointers (phase differences
+    0, 8, 4, 2 and odd: the 16-, 8-, 4-, 2- and 1-byte unit paths)."""
     so, do = shift
     g = torch.Generator(device="cuda").manual_seed(nbytes + 7 * so + do)
     src = torch.randint(0, 256, (nbytes + 32,), dtype=torch.uint8, device="cuda", generator=g)
