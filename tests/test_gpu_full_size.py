@@ -6,7 +6,9 @@ properties that do not need the CPU oracle to run at that size:
   * C3 with the reference's own selection (MeshChunk at this size) on integer-valued fp32: exact sums, so every
     element holds every rank exactly once;
   * C4, 2 GiB bf16 per rank: ReduceScatter then AllGather of integer-valued bf16 equals the exact AllReduce;
-  * C5's largest point, 4 GiB fp16 per rank on the RHD schedule: integer-valued fp16, exact sums.
+  * C5's largest point, 4 GiB fp16 per rank on the RHD schedule: integer-valued fp16, exact sums;
+  * (r04) C4's MeshChunk ReduceScatter (RCCL path and one-sided kernel) and C5's RHD on random data: bit-exact against
+    the same bf16 / fp16 steps (fp32 add, RNE) in the same order done by torch on the GPU.
 The small-size tests pin the association order of every family bit for bit against the oracle; these pin that
 nothing changes at the sizes the benchmark runs.
 """
@@ -171,3 +173,125 @@ def test_c5_largest_point_rhd_exact(world):
         for c in world:
             c.set_algo(H.Algo.AUTO)
     del xs, outs
+
+
+def _o6_peers(n, t, j):
+    """tests/sched_ref.py o6_peers: senders into sub-slice j of owner t, step by step."""
+    out = []
+    for s in range(n - 1):
+        x = s + j + 1
+        if x >= n:
+            x += 1
+        out.append((t + x) % n)
+    return out
+
+
+def _rs_subslices(count, parts, es):
+    """tests/sched_ref.py rs_subslices (…meshchunk.cc:155-180): 4-KiB aligned sub-slices, the rest last."""
+    align = count * es // parts // 4096 * 4096
+    if parts < 2 or align == 0:
+        base, big = divmod(count, parts)
+        out, b = [], 0
+        for i in range(parts):
+            ln = base + (1 if i < big else 0)
+            out.append((b, b + ln))
+            b += ln
+        return out
+    a = align // es
+    return [(i * a, (i + 1) * a) for i in range(parts - 1)] + [((parts - 1) * a, count)]
+
+
+@pytest.mark.parametrize("algo", [H.Algo.AUTO, H.Algo.IPC])
+def test_c4_full_size_reduce_scatter_meshchunk_bf16_random(world, algo):
+    """C4 as named: ReduceScatter of 2 GiB bf16 per rank on 8 ranks, random data, the reference's own selection
+    (MeshChunk: order O6 per 4-KiB sub-slice, per executor loop of min(ccl - 1 MiB, (ccl - 1 MiB) / (n-1)) bytes,
+    ins_temp_reduce_scatter_mesh_1D_meshchunk.cc, ins_v2_reduce_scatter_sole_executor.cc:160-175) on the RCCL-path
+    schedule and on the one-sided kernel (HCCL_AMD_ALGO_IPC, same family): bit-exact against the same bf16 adds
+    (fp32 add, round to nearest even) in the same order done by torch on the GPU (tests/sched_ref.py
+    reduce_scatter_meshchunk restated for torch); then AllGather of the shards is every shard in rank order."""
+    count = (2 << 30) // 2
+    rc = count // N
+    es = 2
+    xs = []
+    for r in range(N):
+        g = torch.Generator(device="cuda").manual_seed(0xC4 + r)
+        xs.append(torch.rand(count, device="cuda", generator=g).mul_(2).sub_(1).to(torch.bfloat16))
+    ccl = 200 << 20
+    tmp = ccl - (1 << 20)
+    per = max(1, min(tmp, tmp // (N - 1) // 128 * 128) // es)
+    want = [torch.empty(rc, dtype=torch.bfloat16, device="cuda") for _ in range(N)]
+    for off in range(0, rc, per):
+        cnt = min(per, rc - off)
+        for t in range(N):
+            for j, (sb, se) in enumerate(_rs_subslices(cnt, N - 1, es)):
+                if se <= sb:
+                    continue
+                lo, hi = t * rc + off + sb, t * rc + off + se
+                acc = xs[t][lo:hi].clone()
+                for q in _o6_peers(N, t, j):
+                    acc = xs[q][lo:hi] + acc  # bf16: fp32 add, RNE
+                want[t][off + sb:off + se] = acc
+    shards = [torch.empty(rc, dtype=torch.bfloat16, device="cuda") for _ in range(N)]
+    for c in world:
+        c.set_algo(algo)
+    try:
+        run_all(world, lambda r, s: world[r].reduce_scatter(xs[r], shards[r], H.HcclReduceOp.SUM, s))
+        used = world[0].last_algo
+        assert used == (H.Algo.MESH_CHUNK if algo == H.Algo.AUTO else H.Algo.IPC), used
+        for r in range(N):
+            bad = torch.count_nonzero(shards[r].view(torch.int16) != want[r].view(torch.int16)).item()
+            assert bad == 0, (r, bad)
+        del xs
+        fulls = [torch.empty(count, dtype=torch.bfloat16, device="cuda") for _ in range(N)]
+        run_all(world, lambda r, s: world[r].all_gather(shards[r], fulls[r], s))
+        cat = torch.cat(shards)
+        for r in range(N):
+            assert torch.equal(fulls[r].view(torch.int16), cat.view(torch.int16)), r
+    finally:
+        for c in world:
+            c.set_algo(H.Algo.AUTO)
+
+
+def test_c5_largest_point_rhd_fp16_random(world):
+    """C5's largest point as named: RHD AllReduce of 4 GiB fp16 per rank on 8 ranks, random data: bit-exact against
+    the RHD closed form done by torch on the GPU. The buffer is split into the schedule's concurrent instances (128-B
+    aligned ceil parts, instance j on virtual ranks table[j]); an element of chunk v of part j is the recursive-halving
+    tree over the operands of virtual ranks v ^ q: at distance M = 4, 2, 1 leaf q takes leaf q + M (op) leaf q (fp16:
+    fp32 add, round to nearest even; tests/sched_ref.py allreduce_rhd / rhd_virtual)."""
+    count = (4 << 30) // 2
+    es = 2
+    xs = []
+    for r in range(N):
+        g = torch.Generator(device="cuda").manual_seed(0xC5 + r)
+        xs.append(torch.rand(count, device="cuda", generator=g).mul_(2).sub_(1).to(torch.float16))
+    table = H.rhd_table(N)
+    nbytes = count * es
+    inst = 1
+    while inst < N - 1 and (inst + 1) ** 2 * (1 << 20) <= 2 * nbytes:
+        inst += 1
+    table = table[:inst]
+    want = torch.empty(count, dtype=torch.float16, device="cuda")
+    for j, (pb, pe) in enumerate(_bounds(count, len(table), es)):
+        for v, (b, e) in enumerate(_bounds(pe - pb, N, es)):
+            if e <= b:
+                continue
+            sl = slice(pb + b, pb + e)
+            leaves = [xs[table[j][v ^ q]][sl] for q in range(N)]
+            m = N // 2
+            while m >= 1:
+                leaves = [leaves[q + m] + leaves[q] for q in range(m)]
+                m //= 2
+            want[sl] = leaves[0]
+    outs = [torch.empty(count, dtype=torch.float16, device="cuda") for _ in range(N)]
+    for c in world:
+        c.set_algo(H.Algo.RHD)
+    try:
+        run_all(world, lambda r, s: world[r].all_reduce(xs[r], outs[r], H.HcclReduceOp.SUM, s))
+        assert world[0].last_algo == H.Algo.RHD
+        for r in range(N):
+            bad = torch.count_nonzero(outs[r].view(torch.int16) != want.view(torch.int16)).item()
+            assert bad == 0, (r, bad)
+    finally:
+        for c in world:
+            c.set_algo(H.Algo.AUTO)
+    del xs, outs, want
