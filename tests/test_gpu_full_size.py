@@ -8,7 +8,11 @@ properties that do not need the CPU oracle to run at that size:
   * C4, 2 GiB bf16 per rank: ReduceScatter then AllGather of integer-valued bf16 equals the exact AllReduce;
   * C5's largest point, 4 GiB fp16 per rank on the RHD schedule: integer-valued fp16, exact sums;
   * (r04) C4's MeshChunk ReduceScatter (RCCL path and one-sided kernel) and C5's RHD on random data: bit-exact against
-    the same bf16 / fp16 steps (fp32 add, RNE) in the same order done by torch on the GPU.
+    the same bf16 / fp16 steps (fp32 add, RNE) in the same order done by torch on the GPU;
+  * (r04) C3's MeshChunk AllReduce (the reference's selection at 4 GiB) on random fp32: bit-exact against the same
+    adds in the same order (executor loops, n-1 sub-slices per chunk, owner then O6 peers).
+Each random-data test first asserts that the plain rank-order fold differs from the closed form on its data, so a pass
+pins the association order and not only the sum.
 The small-size tests pin the association order of every family bit for bit against the oracle; these pin that
 nothing changes at the sizes the benchmark runs.
 """
@@ -231,6 +235,11 @@ def test_c4_full_size_reduce_scatter_meshchunk_bf16_random(world, algo):
                 for q in _o6_peers(N, t, j):
                     acc = xs[q][lo:hi] + acc  # bf16: fp32 add, RNE
                 want[t][off + sb:off + se] = acc
+    o2 = xs[0][:rc].clone()  # the order matters on this data (rank 0's shard, plain rank-order fold)
+    for r in range(1, N):
+        o2 = xs[r][:rc] + o2
+    assert torch.count_nonzero(o2.view(torch.int16) != want[0].view(torch.int16)).item() > 0
+    del o2
     shards = [torch.empty(rc, dtype=torch.bfloat16, device="cuda") for _ in range(N)]
     for c in world:
         c.set_algo(algo)
@@ -282,6 +291,11 @@ def test_c5_largest_point_rhd_fp16_random(world):
                 leaves = [leaves[q + m] + leaves[q] for q in range(m)]
                 m //= 2
             want[sl] = leaves[0]
+    o2 = xs[0].clone()  # the order matters on this data: the plain rank-order fold differs somewhere
+    for r in range(1, N):
+        o2 = xs[r] + o2
+    assert torch.count_nonzero(o2.view(torch.int16) != want.view(torch.int16)).item() > 0
+    del o2
     outs = [torch.empty(count, dtype=torch.float16, device="cuda") for _ in range(N)]
     for c in world:
         c.set_algo(H.Algo.RHD)
@@ -290,6 +304,58 @@ def test_c5_largest_point_rhd_fp16_random(world):
         assert world[0].last_algo == H.Algo.RHD
         for r in range(N):
             bad = torch.count_nonzero(outs[r].view(torch.int16) != want.view(torch.int16)).item()
+            assert bad == 0, (r, bad)
+    finally:
+        for c in world:
+            c.set_algo(H.Algo.AUTO)
+    del xs, outs, want
+
+
+@pytest.mark.parametrize("algo", [H.Algo.AUTO, H.Algo.IPC])
+def test_c3_full_size_meshchunk_random(world, algo):
+    """C3 with the reference's own selection at 4 GiB fp32 per rank (MeshChunk AllReduce, order O6), random data, on
+    the RCCL-path schedule and on the one-sided kernel: bit-exact against torch's fp32 adds in the closed form of
+    tests/sched_ref.py allreduce_meshchunk (executor loops of min(ccl, ccl / 2) rounded down to 128 B, chunks of
+    ceil(cnt / n) elements, n - 1 even sub-slices per chunk, owner first then o6_peers per sub-slice)."""
+    count = (4 << 30) // 4
+    es = 4
+    xs = []
+    for r in range(N):
+        g = torch.Generator(device="cuda").manual_seed(0xC36 + r)
+        xs.append(torch.rand(count, device="cuda", generator=g).mul_(2).sub_(1))
+    ccl = 200 << 20
+    per = max(1, min(ccl, ccl // 2 // 128 * 128) // es)
+    want = torch.empty(count, device="cuda")
+    for off in range(0, count, per):
+        cnt = min(per, count - off)
+        cs = -(-cnt // N)
+        for t in range(N):
+            b, e = min(cnt, t * cs), min(cnt, (t + 1) * cs)
+            base, big = divmod(e - b, N - 1)
+            sb = 0
+            for j in range(N - 1):
+                se = sb + base + (1 if j < big else 0)
+                if se > sb:
+                    sl = slice(off + b + sb, off + b + se)
+                    acc = xs[t][sl].clone()
+                    for q in _o6_peers(N, t, j):
+                        acc = xs[q][sl] + acc
+                    want[sl] = acc
+                sb = se
+    # the order matters on this data: the plain rank-order fold (O2) differs from the closed form somewhere
+    o2 = xs[0].clone()
+    for r in range(1, N):
+        o2.add_(xs[r])
+    assert torch.count_nonzero(o2.view(torch.int32) != want.view(torch.int32)).item() > 0
+    del o2
+    outs = [torch.empty(count, device="cuda") for _ in range(N)]
+    for c in world:
+        c.set_algo(algo)
+    try:
+        run_all(world, lambda r, s: world[r].all_reduce(xs[r], outs[r], H.HcclReduceOp.SUM, s))
+        assert world[0].last_algo == (H.Algo.MESH_CHUNK if algo == H.Algo.AUTO else H.Algo.IPC)
+        for r in range(N):
+            bad = torch.count_nonzero(outs[r].view(torch.int32) != want.view(torch.int32)).item()
             assert bad == 0, (r, bad)
     finally:
         for c in world:
