@@ -569,6 +569,14 @@ def _graph_us(call, calls: int = 50, replays: int = 5) -> float:
     return float(t[0])
 
 
+def _xgmi_frac(busbw_GBps: float, world: int):
+    """busbw as a fraction of the xGMI algorithmic-bus roofline a rank has (one 76.8 GB/s link per peer, at most 7);
+    None in the one-GPU harness mode, whose ranks share one device and have no xGMI in the path."""
+    if os.environ.get("HCCL_AMD_BENCH_HOST_EXCHANGE") == "1" or world < 2:
+        return None
+    return round(busbw_GBps / (min(world - 1, 7) * XGMI_LINK_GBPS), 4)
+
+
 def bench_c4(comm, send, recv, world) -> dict:
     """C4: ZeRO-style gradient bucket, bf16, 2 GiB per rank: HcclReduceScatter (SUM) then HcclAllGather."""
     nbytes = 2 << 30
@@ -584,6 +592,7 @@ def bench_c4(comm, send, recv, world) -> dict:
            "rs_ms": round(t_rs * 1e3, 3), "ag_ms": round(t_ag * 1e3, 3),
            "rs_busbw_GBps": round(nbytes / t_rs / 1e9 * f, 2), "ag_busbw_GBps": round(nbytes / t_ag / 1e9 * f, 2),
            "rs_ag_busbw_GBps": round(2 * nbytes / (t_rs + t_ag) / 1e9 * f, 2)}
+    out["rs_ag_xgmi_frac"] = _xgmi_frac(out["rs_ag_busbw_GBps"], world)
     # the mesh ReduceScatter (order O1) and the one-sided IPC kernel with the same order: same bits; then the IPC
     # kernel in the auto family (MeshChunk O6 here), which must match the auto ReduceScatter
     try:
@@ -595,6 +604,7 @@ def bench_c4(comm, send, recv, world) -> dict:
         t_ipc = _timed(lambda: comm.reduce_scatter(x, shard, H.HcclReduceOp.SUM, s), 5)
         out["rs_ipc_ms"] = round(t_ipc * 1e3, 3)
         out["rs_ipc_busbw_GBps"] = round(nbytes / t_ipc / 1e9 * f, 2)
+        out["rs_ipc_xgmi_frac"] = _xgmi_frac(out["rs_ipc_busbw_GBps"], world)
         out["rs_ipc_ran"] = H.Algo(comm.last_algo).name
         out["rs_ipc_matches_mesh"] = bool(torch.equal(ref, shard.view(torch.int16)[:: 1 << 10]))
         out["rs_ipc_barrier_timeouts"] = comm.ipc_status() & 1
@@ -620,6 +630,7 @@ def bench_c4(comm, send, recv, world) -> dict:
         t_ag_ipc = _timed(lambda: comm.all_gather(shard, full, s), 5)
         out["ag_ipc_ms"] = round(t_ag_ipc * 1e3, 3)
         out["ag_ipc_busbw_GBps"] = round(nbytes / t_ag_ipc / 1e9 * f, 2)
+        out["ag_ipc_xgmi_frac"] = _xgmi_frac(out["ag_ipc_busbw_GBps"], world)
         out["ag_ipc_ran"] = H.Algo(comm.last_algo).name
         out["ag_ipc_matches_auto"] = bool(torch.equal(ref_ag, full.view(torch.int16)[:: 1 << 10]))
         out["ag_ipc_barrier_timeouts"] = comm.ipc_status() & 1
@@ -665,6 +676,8 @@ def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
                     continue
                 row[f"{key[algo]}_us"] = round(t * 1e6, 1)
                 row[f"{key[algo]}_busbw_GBps"] = round(nbytes / t / 1e9 * f, 2)
+                if nbytes >= (256 << 20):  # the bandwidth end of the curve
+                    row[f"{key[algo]}_xgmi_frac"] = _xgmi_frac(row[f"{key[algo]}_busbw_GBps"], world)
                 # RHD's bits from the one-sided kernel: the IPC_RHD output must equal the RHD schedule's, bit for bit
                 sample = b.view(torch.int16)[:: 1 << 10].clone()
                 if algo == H.Algo.RHD:
@@ -777,6 +790,7 @@ def bench_c3_algos(comm, send, recv, world) -> dict:
                 continue
             row = {"ms": round(t * 1e3, 3), "busbw_GBps": round(C3_BYTES / t / 1e9 * 2 * (world - 1) / world, 2),
                    "ran": H.Algo(comm.last_algo).name}  # an IPC row reads MESH_* if the IPC set-up fell back
+            row["xgmi_frac"] = _xgmi_frac(row["busbw_GBps"], world)
             digests.setdefault(algo, recv.view(torch.int32)[:: 1 << 12].clone())
             digest = recv.view(torch.int32)[:: 1 << 12].clone()
             if algo in twin and twin[algo] in digests:

@@ -381,19 +381,25 @@ uint32_t Pow2Up(uint32_t x)
 // (profiles/r02_rccl_p2p_channels_selfloop.jsonl: 176 / 345 / 650 GB/s at 4 / 8 / 16 channels per peer), below one
 // 76.8 GB/s xGMI link per direction (cost_model.cc:78-79 prices the reference's links the same way). Left to RCCL's
 // topology defaults a peer may get fewer channels than its link needs; the reference sizes its channels per link
-// explicitly (alg_param.h:434-448). So NCCL_NCHANNELS_PER_PEER = HCCL_AMD_P2P_CHANNELS_PER_PEER (default 4, about twice
-// a link) and NCCL_MIN_P2P_NCHANNELS = per peer x 7 (the peers of an 8-GPU node) rounded up to a power of two, at most
-// 64, so every peer's channels are distinct. A value the caller already set wins. RCCL reads them once per process, at
+// explicitly (alg_param.h:434-448). So NCCL_NCHANNELS_PER_PEER = HCCL_AMD_P2P_CHANNELS_PER_PEER (default 16) and
+// NCCL_MIN_P2P_NCHANNELS = per peer x 7 (the peers of an 8-GPU node) rounded up to a power of two, at most 64. Why 16:
+// on an 8-GPU node the 64 p2p channels are shared by seven peers, about nine each (three to four links' worth) at any
+// setting from 4 up, while on a one-rank self loop (the one-GPU proxy) the count caps the only "link": 4 made the
+// self-loop MeshChunk program 2.9x and the ring 1.7x slower than RCCL's default, 16 is within 0-20 %
+// (profiles/r04_span_channels.jsonl). A value the caller already set wins. RCCL reads them once per process, at
 // its first communicator, so they are set when this library is loaded, while the process has no thread of ours that
 // could read the environment concurrently (setenv is not thread-safe); they then apply to every RCCL communicator of
-// the process, this library's or not. HcclAmdRcclP2pChannels reports them.
+// the process, this library's or not. HcclAmdRcclP2pChannels reports them. HCCL_AMD_P2P_CHANNELS_PER_PEER=0 sets
+// neither (RCCL's own defaults; they report 0; on a self loop RCCL then reports 64 p2p channels, 128 per peer).
 __attribute__((constructor)) void ConfigureRcclP2pChannels()
 {
-    const uint32_t per = Pow2Up(EnvU32("HCCL_AMD_P2P_CHANNELS_PER_PEER", 4));
-    if (std::getenv("NCCL_NCHANNELS_PER_PEER") == nullptr) {
+    const char* raw = std::getenv("HCCL_AMD_P2P_CHANNELS_PER_PEER");
+    const bool rcclDefaults = raw != nullptr && std::strcmp(raw, "0") == 0;  // 0: leave both to RCCL
+    const uint32_t per = Pow2Up(EnvU32("HCCL_AMD_P2P_CHANNELS_PER_PEER", 16));
+    if (!rcclDefaults && std::getenv("NCCL_NCHANNELS_PER_PEER") == nullptr) {
         setenv("NCCL_NCHANNELS_PER_PEER", std::to_string(per).c_str(), 0);
     }
-    if (std::getenv("NCCL_MIN_P2P_NCHANNELS") == nullptr) {
+    if (!rcclDefaults && std::getenv("NCCL_MIN_P2P_NCHANNELS") == nullptr) {
         setenv("NCCL_MIN_P2P_NCHANNELS", std::to_string(std::min<uint32_t>(64, Pow2Up(per * 7))).c_str(), 0);
     }
     g_p2pPerPeer = EnvU32("NCCL_NCHANNELS_PER_PEER", 0);

@@ -279,9 +279,10 @@ extern uint32_t HcclAmdCommPendingDestroys(void);
 
 /* RCCL's p2p channel settings of this process: *perPeer = NCCL_NCHANNELS_PER_PEER, *minP2pChannels =
  * NCCL_MIN_P2P_NCHANNELS. Unless the environment already sets them, the library sets them when it is loaded (RCCL reads
- * them once, at the process's first communicator, whoever creates it): HCCL_AMD_P2P_CHANNELS_PER_PEER (default 4: RCCL's
+ * them once, at the process's first communicator, whoever creates it): HCCL_AMD_P2P_CHANNELS_PER_PEER (default 16: RCCL's
  * p2p kernel streams about 43 GB/s per channel, an xGMI link 76.8 GB/s per direction) and per peer x 7 (an 8-GPU
- * node's peers) rounded up to a power of two, at most 64. Child processes inherit them. */
+ * node's peers) rounded up to a power of two, at most 64. HCCL_AMD_P2P_CHANNELS_PER_PEER=0 sets neither (both report
+ * 0). Child processes inherit them. */
 extern HcclResult HcclAmdRcclP2pChannels(uint32_t* perPeer, uint32_t* minP2pChannels);
 
 /* The executor staging of comm (diagnostics): *ptr = its device address (NULL until allocated), *bytes = its size. */

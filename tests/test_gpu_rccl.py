@@ -509,11 +509,11 @@ def _p2p_channels_worker(per_peer, log_dir, q):
 
 def test_rccl_p2p_channels_configured(tmp_path):
     """the library sets RCCL's per-peer p2p channels when it is loaded, before any RCCL
-    communicator (default 4 per peer, NCCL_MIN_P2P_NCHANNELS = per peer x 7 rounded up), and RCCL honours them: its
-    INIT log reports the per-peer count (twice the setting), and the self-loop message rate scales with it (about
-    43 GB/s per channel, r02)."""
+    communicator (default 16 per peer, NCCL_MIN_P2P_NCHANNELS = per peer x 7 rounded up, at most 64), and RCCL
+    honours them: its INIT log reports the per-peer count (twice the setting), and the self-loop message rate scales
+    with it (about 43 GB/s per channel, r02). HCCL_AMD_P2P_CHANNELS_PER_PEER=0 leaves both to RCCL."""
     rows = []
-    for per_peer in (None, 8):
+    for per_peer in (None, 4, 0):
         ctx = mp.get_context("spawn")
         q = ctx.Queue()
         p = ctx.Process(target=_p2p_channels_worker, args=(per_peer, str(tmp_path), q))
@@ -530,10 +530,13 @@ def test_rccl_p2p_channels_configured(tmp_path):
     with open(os.path.join(ROOT, "gpurun_out", "rccl_p2p_channels_configured.jsonl"), "w") as f:
         for row in rows:
             f.write(__import__("json").dumps(row) + "\n")
-    default, eight = rows
-    assert default["exact"] and eight["exact"]
-    assert tuple(default["configured"]) == (4, 32) and tuple(eight["configured"]) == (8, 64), rows
+    default, four, rccl_own = rows
+    assert default["exact"] and four["exact"] and rccl_own["exact"]
+    assert tuple(default["configured"]) == (16, 64) and tuple(four["configured"]) == (4, 32), rows
     # RCCL's own summary ("%d p2p channels, %d p2p channels per peer") reports twice the per-peer setting
-    assert default["rccl_reported"] is not None and eight["rccl_reported"] is not None, rows
-    assert eight["rccl_reported"][1] == 2 * default["rccl_reported"][1], rows
-    assert eight["self_loop_GBps"] > 1.5 * default["self_loop_GBps"], rows
+    assert default["rccl_reported"] is not None and four["rccl_reported"] is not None, rows
+    assert default["rccl_reported"][1] == 4 * four["rccl_reported"][1], rows
+    assert default["self_loop_GBps"] > 2 * four["self_loop_GBps"], rows
+    # 0 leaves both to RCCL (reported as 0); what RCCL then picks is recorded only
+    assert tuple(rccl_own["configured"]) == (0, 0), rows
+    assert rccl_own["rccl_reported"] is not None, rows

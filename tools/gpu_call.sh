@@ -12,6 +12,7 @@
 #   host_cost      host enqueue cost of the RCCL path by category (default, watchdog off, blocking RCCL)
 #   ipc_pmc        rocprofv3 kernel trace + FETCH_SIZE + WRITE_SIZE of the one-sided kernel, rank mode, n = 2
 #   span_pmc       the same over a self-loop MeshChunk program (RCCL copies + folds)
+#   span_channels  self-loop MeshChunk and ring program spans at 0 (RCCL defaults) / 4 / 8 / 16 p2p channels per peer
 #   bench          bench.py default line
 #   profile        tools/profile_round.sh: rocprofv3 trace + FETCH/WRITE of the N=1 bench line, per-kernel summaries
 #   ipc_ab         one-sided kernel: block shares (contiguous / tiles) x cache policy A/B, loopback world
@@ -119,6 +120,20 @@ step_span_pmc() {
     -- python3 -u tools/rccl_selfloop_trace.py "${args[@]}"
   run span_mesh_chunk_write 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/span_write" -o run \
     -- python3 -u tools/rccl_selfloop_trace.py "${args[@]}"
+}
+
+# r04: the self-loop program span under each per-peer channel setting (0 = RCCL's defaults). On a one-rank self loop
+# the per-peer count caps the only "link", so this shows what the xGMI-sized default costs the one-GPU proxy.
+step_span_channels() {
+  : > "$OUT/span_channels.jsonl"
+  local algo v
+  for algo in mesh_chunk ring; do
+    for v in 0 4 8 16; do
+      HCCL_AMD_P2P_CHANNELS_PER_PEER=$v run "span_channels_${algo}_$v" 150 python3 -u tools/rccl_selfloop_trace.py \
+        --algo "$algo" --units 64 --iters 5 || return $?
+      grep '^{' "$OUT/span_channels_${algo}_$v.log" | python3 -c "import json,sys; [print(json.dumps(dict(json.loads(l), p2p_channels_per_peer_env=$v))) for l in sys.stdin]" >> "$OUT/span_channels.jsonl"
+    done
+  done
 }
 
 step_bench() {
