@@ -17,6 +17,7 @@
 #   profile        tools/profile_round.sh: rocprofv3 trace + FETCH/WRITE of the N=1 bench line, per-kernel summaries
 #   ipc_ab         one-sided kernel: block shares (contiguous / tiles) x cache policy A/B, loopback world
 #   harness        bench.py's N > 1 code path with two ranks sharing the GPU (IPC-only; a crash check, not a result)
+#   harness_wide   the same with 4 and 8 ranks
 #   counters       the TCC counters this rocprofv3 offers
 #   ipc_staging    one-sided kernel: uncached vs cached staging memory (A/B on one device)
 #   ipc_fence      one-sided kernel: system-scope vs light barrier fences x workgroups per rank (A/B)
@@ -147,6 +148,12 @@ step_profile() {
 
 step_harness() {
   run harness_n2 420 bash tools/gpu_harness_n2.sh
+}
+
+# the same with 4 and 8 ranks on the one GPU (every rank's buffers in one HBM: 8 x 8 GiB at N = 8)
+step_harness_wide() {
+  HARNESS_N=4 HARNESS_LIMIT=600 run harness_n4 620 bash tools/gpu_harness_n2.sh || return $?
+  HARNESS_N=8 HARNESS_LIMIT=900 run harness_n8 920 bash tools/gpu_harness_n2.sh
 }
 
 step_ipc_ab() {
