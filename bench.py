@@ -272,7 +272,7 @@ def fold_roofline(dev, stream, n: int = 8, reps: int = 10) -> dict:
             "kernel_avg_us": round(kavg * 1e6, 1), "kernel_median_us": round(float(np.median(per)) * 1e6, 1),
             "achieved_GBps": round(nbytes / kavg / 1e9, 1), "peak_GBps": HBM_PEAK_GBPS,
             "frac": round(nbytes / kavg / 1e9 / HBM_PEAK_GBPS, 4),
-            "traffic": load_pmc_traffic("r04_pmc_fold_n8.json") or load_pmc_traffic("r03d_pmc_fold_n8.json"),
+            "traffic": load_pmc_traffic("r04f_pmc_fold_n8.json") or load_pmc_traffic("r04_pmc_fold_n8.json") or load_pmc_traffic("r03d_pmc_fold_n8.json"),
             "result_ok": ok}
 
 
@@ -342,7 +342,7 @@ def ipc_two_shot_roofline(dev, n: int = 2, mib: int = 512, reps: int = 10) -> di
             "call_to_call_avg_us": round(float(np.mean(per_call)) * 1e6, 1),
             "achieved_GBps": round(nbytes / kavg / 1e9, 1), "peak_GBps": HBM_PEAK_GBPS,
             "frac": round(nbytes / kavg / 1e9 / HBM_PEAK_GBPS, 4),
-            "traffic": load_pmc_traffic("r04_pmc_ipc_two_shot.json") or load_pmc_traffic("r03d_pmc_ipc_two_shot.json"),
+            "traffic": load_pmc_traffic("r04f_pmc_ipc_two_shot.json") or load_pmc_traffic("r04_pmc_ipc_two_shot.json") or load_pmc_traffic("r03d_pmc_ipc_two_shot.json"),
             "barrier_timeouts": timeouts,
             "result_ok": ok}
 
@@ -406,7 +406,7 @@ def bench_local(args) -> dict:
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": load_pmc_traffic("r04_pmc_local_reduce.json") or load_pmc_traffic("r03d_pmc_local_reduce.json"),
+            "traffic": load_pmc_traffic("r04f_pmc_local_reduce.json") or load_pmc_traffic("r04_pmc_local_reduce.json") or load_pmc_traffic("r03d_pmc_local_reduce.json"),
             "kernel": "k_reduce2<EFp<float>, SUM>",
             "algorithmic_bytes_per_launch": bytes_step,
             "kernel_avg_us": round(kavg * 1e6, 2),
