@@ -605,6 +605,11 @@ HcclResult RunCompiled(Comm& c, const CompiledSchedule& cs, void* const bufs[3],
         // capture must not have to do.
         if (cs.eagerRuns++ == 0) return Execute(c, cs.sched.ops, bufs, dt, op, user, false, &cs.plan);
         if (c.graphs.size() >= cap) {
+            // The evicted executable may still run: the host is ahead of the device. Every earlier call precedes the
+            // previous call's end on the device (EntryScope orders each call after the last one's tail), so once that
+            // tail has completed no launch of it is in flight. Eviction is rare (more distinct calls than the cache
+            // holds) and already pays a capture, so the wait costs little.
+            if (c.tail != nullptr) HIP_CHK(hipEventSynchronize(c.tail));
             auto lru = std::min_element(c.graphs.begin(), c.graphs.end(),
                                         [](const GraphEntry& x, const GraphEntry& y) { return x.lastUse < y.lastUse; });
             if (lru->exec != nullptr) (void)hipGraphExecDestroy(lru->exec);

@@ -457,6 +457,75 @@ def test_executor_graph_cache_replays_bit_exact():
     assert launches and all(x >= 3 for x in launches), results
 
 
+def _graph_eviction_worker(q):
+    """HCCL_AMD_GRAPH_CACHE=2 with more programs than that, called round-robin without a host synchronisation between
+    calls: every capture evicts an executable whose last launch may still be in flight (RunCompiled waits for the
+    previous call's end before destroying it). Each call's output is copied aside on the same stream and checked
+    against the oracle once the whole sequence has been issued."""
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        os.environ["HCCL_AMD_GRAPH_CACHE"] = "2"  # read per call
+        import torch
+        import hccl_amd as H
+        from oracle import oracle as O
+        from tests._util import to_device, to_host
+        torch.cuda.set_device(0)
+        comm = H.comm_init_root_info(1, H.get_root_info(), 0)
+        s = torch.cuda.Stream()
+        dtype, op = O.FP32, O.SUM
+        st = O.NP_STORAGE[dtype]
+        progs = []
+        for k, (op_type, algo, n, rank, count) in enumerate(CAPTURE_CASES):
+            prog = self_looped(op_type, algo, n, rank, count, dtype)
+            if prog is None:
+                continue
+            in_len = count * n if op_type == 1 else count
+            out_len = count * n if op_type == 3 else count
+            progs.append((k, prog, in_len, out_len, to_device(dtype, np.zeros(in_len, st)),
+                          to_device(dtype, np.zeros(out_len, st))))
+        assert len(progs) >= 4, len(progs)
+        issued = []
+        captures0 = comm.graph_stats()[1]
+        with torch.cuda.stream(s):
+            for rnd in range(4):
+                for k, (arr, nops, scratch), in_len, out_len, xd, od in progs:
+                    x = O.random_operands(dtype, in_len, seed=9000 + 100 * k + rnd, edge=False)
+                    xd.copy_(to_device(dtype, x))
+                    comm.execute(arr, nops, xd, od, op, False, s, dtype=dtype)
+                    issued.append((k, rnd, arr, nops, scratch, x, out_len, od.clone()))
+        torch.cuda.synchronize()
+        captures = comm.graph_stats()[1] - captures0
+        results = []
+        for k, rnd, arr, nops, scratch, x, out_len, got in issued:
+            bufs = [[x.copy(), np.zeros(out_len, st), np.zeros(max(scratch, 1), st)]]
+            assert O.replay(1, dtype, op, [(arr, nops)], bufs) == 0
+            results.append((k, rnd, "ok" if O.equal_bits(dtype, to_host(dtype, got), bufs[0][1]) else "mismatch"))
+        comm.destroy()
+        q.put(("ok", {"results": results, "captures": captures, "programs": len(progs)}))
+    except Exception as e:  # noqa: BLE001
+        q.put(("err", f"{type(e).__name__}: {e}\n{traceback.format_exc()}"))
+
+
+def test_executor_graph_cache_eviction_while_in_flight():
+    """More programs than the executor graph cache holds, issued back to back without host synchronisation: every
+    output bit-exact, and the cache really evicted (more captures than slots)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_graph_eviction_worker, args=(q,))
+    p.start()
+    try:
+        status, res = q.get(timeout=300)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert status == "ok", res
+    assert not [r for r in res["results"] if r[-1] != "ok"], res
+    assert len(res["results"]) == 4 * res["programs"], res
+    assert res["captures"] > 2, res
+
+
 def _p2p_channels_worker(per_peer, log_dir, q):
     """One 1-rank RCCL communicator (this process's first): the channel settings the library gave RCCL, what RCCL's
     INIT log reports, and the self-loop send/recv rate of one 256 MiB message."""
