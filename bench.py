@@ -1154,10 +1154,12 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
 
 _PRINTED = threading.Event()
 _PRINT_LOCK = threading.Lock()
-# Exit codes besides 0: the headline loop failed on some rank (the line carries "error"), or the extras watchdog
-# stopped the run (the line carries "watchdog"). The JSON line is printed first either way.
+# Exit codes besides 0: the headline loop failed on some rank (the line carries "error"), the extras watchdog
+# stopped the run (the line carries "watchdog"), or the timed path's output was wrong (`result_ok` false). The JSON
+# line is printed first in every case.
 EXIT_FAILED = 3
 EXIT_WATCHDOG = 4
+EXIT_WRONG_RESULT = 5
 _EXIT_CODE = 0
 
 
@@ -1228,8 +1230,11 @@ def main():
         res = bench_allreduce(args, rank, world, int(os.environ.get("LOCAL_RANK", rank)))
     else:
         res = bench_local(args)
+    global _EXIT_CODE
     if res is not None:
         emit(res)
+        if res.get("result_ok") is False and _EXIT_CODE == 0:
+            _EXIT_CODE = EXIT_WRONG_RESULT
     sys.stdout.flush()
     sys.exit(_EXIT_CODE)
 
