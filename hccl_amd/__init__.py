@@ -15,6 +15,7 @@ import torch
 from ._lib import (  # noqa: F401
     Algo,
     AivVariant,
+    Config,
     HcclAmdIrOp,
     HcclAmdUnitPlan,
     HcclDataType,
@@ -96,6 +97,12 @@ def local_reduce_n(out: torch.Tensor, srcs: Sequence[torch.Tensor], op: int = Hc
 def set_reduce_launch(blocks_per_cu: int = 0, unroll: int = 0, cache_policy: int = 0) -> None:
     """0 restores each default; see HcclAmdSetReduceLaunch in include/hccl_amd.h."""
     check("HcclAmdSetReduceLaunch", lib.HcclAmdSetReduceLaunch(blocks_per_cu, unroll, cache_policy))
+
+
+def set_device_copy_kernel(on: bool = True) -> None:
+    """Process-wide: device copies by the library's copy kernel (True, the default) or hipMemcpyAsync (False;
+    diagnostics). HcclAmdSetDeviceCopyKernel."""
+    check("HcclAmdSetDeviceCopyKernel", lib.HcclAmdSetDeviceCopyKernel(1 if on else 0))
 
 
 def set_fold_mode(mode: int = 0) -> None:
@@ -243,6 +250,16 @@ class Comm:
     @property
     def last_algo(self) -> int:
         return lib.HcclAmdCommLastAlgo(self.handle)
+
+    def set_config(self, key: int, value: int) -> None:
+        """HcclAmdCommSetConfig: one entry of the communicator's configuration (Config; read from the environment when
+        the communicator was created)."""
+        check("HcclAmdCommSetConfig", lib.HcclAmdCommSetConfig(self.handle, int(key), int(value)))
+
+    def get_config(self, key: int) -> int:
+        v = ctypes.c_int64(0)
+        check("HcclAmdCommGetConfig", lib.HcclAmdCommGetConfig(self.handle, int(key), ctypes.byref(v)))
+        return v.value
 
     def execute(self, ops, nops: int, send: torch.Tensor, recv: torch.Tensor, op: int = HcclReduceOp.SUM,
                 single_stream: bool = False, stream=None, dtype=None) -> None:

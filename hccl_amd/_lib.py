@@ -87,6 +87,26 @@ class Algo(enum.IntEnum):
     IPC_RHD = 12
 
 
+class Config(enum.IntEnum):
+    """HcclAmdConfigKey (include/hccl_amd.h): a communicator's configuration, read from the environment at creation."""
+    DETERMINISTIC_STRICT = 0
+    EXPANSION_MODE_AIV = 1
+    AIV_CORE_LIMIT = 2
+    SINGLE_STREAM_BYTES = 3
+    SMALL_IPC_BYTES = 4
+    PLAN_CACHE = 5
+    GRAPH_CACHE = 6
+    IPC_LIGHT_FENCE = 7
+    IPC_NT = 8
+    IPC_THREADS = 9
+    IPC_TILE_KIB = 10
+    IPC_TIMEOUT_MS = 11
+    IPC_STAGING_MIB = 12
+    IPC_STAGING_CACHED = 13
+    IPC_TRACE = 14
+    IPC_L2_SCRUB = 15
+
+
 class AivVariant(enum.IntEnum):
     NOT_MATCHED = 0
     AR_ONESHOT = 1
@@ -190,6 +210,9 @@ SIGNATURES = {
     "HcclAmdCommSetPieceBytes": (_res, [_vp, _u64]),
     "HcclAmdCommSetIpcBlocks": (_res, [_vp, _u32]),
     "HcclAmdCommLastAlgo": (_i32, [_vp]),
+    "HcclAmdCommSetConfig": (_res, [_vp, _i32, ctypes.c_int64]),
+    "HcclAmdCommGetConfig": (_res, [_vp, _i32, ctypes.POINTER(ctypes.c_int64)]),
+    "HcclAmdSetDeviceCopyKernel": (_res, [_i32]),
     "HcclAmdCommCompileStats": (_res, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     "HcclAmdCommGraphStats": (_res, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     "HcclAmdCommExecute": (_res, [_vp, ctypes.POINTER(HcclAmdIrOp), _u64, _vp, _vp, _i32, _i32, _i32, _vp]),

@@ -38,20 +38,10 @@ uint64_t CclBytesDefault()
 // Every communicator holds 2 x HCCL_BUFFSIZE (HCCL_BUFFSIZE.md: "2*HCCL_BUFFSIZE", send and receive halves).
 uint64_t ScratchBytesDefault() { return 2 * CclBytesDefault(); }
 
-uint64_t SingleStreamBytes()
-{
-    const char* e = std::getenv("HCCL_AMD_SINGLE_STREAM_BYTES");  // read per call: tests switch it
-    if (e != nullptr && e[0] != '\0') {
-        char* end = nullptr;
-        unsigned long long x = std::strtoull(e, &end, 10);
-        if (end != e) return static_cast<uint64_t>(x);
-    }
-    return static_cast<uint64_t>(1) << 20;
-}
-
 HcclResult Comm::Init(int dev)
 {
     device = dev;
+    cfg = ReadCommConfig();
     HIP_CHK(hipSetDevice(dev));
     int lo = 0, hi = 0;
     HIP_CHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -247,10 +237,10 @@ public:
     }
     const char* Name() const override { return "rccl"; }
     bool Abortable() const override { return true; }
-    void SetLocalTeardown() override
+    void SetLocalTeardown(bool on) override
     {
         std::lock_guard<std::mutex> lk(mu_);
-        localTeardown_ = true;
+        localTeardown_ = on;
     }
     // From the watchdog thread. The communicator is taken out under the lock and aborted outside it: RCCL's abort
     // raises the kernels' abort flag at once but then waits for the graphs holding its plans (the executor graph cache,
@@ -376,31 +366,32 @@ uint32_t Pow2Up(uint32_t x)
 
 }  // namespace
 
-// Per-peer p2p channels of RCCL. The schedules move their data with grouped ncclSend/ncclRecv,
-// one message per peer per step, and RCCL's p2p kernel streams about 43 GB/s per channel
+// Per-peer p2p channels of RCCL, opt-in. The schedules move their data with grouped ncclSend/ncclRecv, one
+// message per peer per step, and RCCL's p2p kernel streams about 43 GB/s per channel
 // (profiles/r02_rccl_p2p_channels_selfloop.jsonl: 176 / 345 / 650 GB/s at 4 / 8 / 16 channels per peer), below one
-// 76.8 GB/s xGMI link per direction (cost_model.cc:78-79 prices the reference's links the same way). Left to RCCL's
-// topology defaults a peer may get fewer channels than its link needs; the reference sizes its channels per link
-// explicitly (alg_param.h:434-448). So NCCL_NCHANNELS_PER_PEER = HCCL_AMD_P2P_CHANNELS_PER_PEER (default 16) and
-// NCCL_MIN_P2P_NCHANNELS = per peer x 7 (the peers of an 8-GPU node) rounded up to a power of two, at most 64. Why 16:
-// on an 8-GPU node the 64 p2p channels are shared by seven peers, about nine each (three to four links' worth) at any
-// setting from 4 up, while on a one-rank self loop (the one-GPU proxy) the count caps the only "link": 4 made the
-// self-loop MeshChunk program 2.9x and the ring 1.7x slower than RCCL's default, 16 is within 0-20 %
-// (profiles/r04_span_channels.jsonl). A value the caller already set wins. RCCL reads them once per process, at
-// its first communicator, so they are set when this library is loaded, while the process has no thread of ours that
-// could read the environment concurrently (setenv is not thread-safe); they then apply to every RCCL communicator of
-// the process, this library's or not. HcclAmdRcclP2pChannels reports them. HCCL_AMD_P2P_CHANNELS_PER_PEER=0 sets
-// neither (RCCL's own defaults; they report 0; on a self loop RCCL then reports 64 p2p channels, 128 per peer).
+// 76.8 GB/s xGMI link per direction (cost_model.cc:78-79 prices the reference's links the same way); the reference
+// sizes its channels per link explicitly (alg_param.h:434-448). RCCL reads NCCL_NCHANNELS_PER_PEER and
+// NCCL_MIN_P2P_NCHANNELS once per process, at its first communicator, whoever creates it, and they then apply to every
+// RCCL communicator of the process (torch.distributed's too), with a device-memory cost per channel that no run on this
+// pool has measured at seven peers. So the library changes them only when asked: HCCL_AMD_P2P_CHANNELS_PER_PEER=k sets
+// NCCL_NCHANNELS_PER_PEER=k unless the caller set it, and NCCL_MIN_P2P_NCHANNELS = (the per-peer value in effect) x 7
+// (the peers of an 8-GPU node) rounded up to a power of two, at most 64, unless the caller set it. They are set when the
+// library is loaded, before any thread of the library exists; a caller that loads it after starting threads of its own
+// that read the environment should set the NCCL_* variables itself instead. bench.py opts in with 16 (r04: 4 made the
+// one-GPU self-loop proxy of the RCCL path 1.7-2.9x slower, profiles/r04_span_channels.jsonl). HcclAmdRcclP2pChannels
+// reports the values in the environment after this step (requested, not necessarily what RCCL used: RCCL's INIT log
+// line "%d p2p channels, %d p2p channels per peer" says that, and bench.py's transport.p2p_channels carries it).
 __attribute__((constructor)) void ConfigureRcclP2pChannels()
 {
-    const char* raw = std::getenv("HCCL_AMD_P2P_CHANNELS_PER_PEER");
-    const bool rcclDefaults = raw != nullptr && std::strcmp(raw, "0") == 0;  // 0: leave both to RCCL
-    const uint32_t per = Pow2Up(EnvU32("HCCL_AMD_P2P_CHANNELS_PER_PEER", 16));
-    if (!rcclDefaults && std::getenv("NCCL_NCHANNELS_PER_PEER") == nullptr) {
-        setenv("NCCL_NCHANNELS_PER_PEER", std::to_string(per).c_str(), 0);
-    }
-    if (!rcclDefaults && std::getenv("NCCL_MIN_P2P_NCHANNELS") == nullptr) {
-        setenv("NCCL_MIN_P2P_NCHANNELS", std::to_string(std::min<uint32_t>(64, Pow2Up(per * 7))).c_str(), 0);
+    const uint32_t per = EnvU32("HCCL_AMD_P2P_CHANNELS_PER_PEER", 0);
+    if (per != 0) {
+        if (std::getenv("NCCL_NCHANNELS_PER_PEER") == nullptr) {
+            setenv("NCCL_NCHANNELS_PER_PEER", std::to_string(Pow2Up(per)).c_str(), 0);
+        }
+        const uint32_t inEffect = EnvU32("NCCL_NCHANNELS_PER_PEER", Pow2Up(per));
+        if (std::getenv("NCCL_MIN_P2P_NCHANNELS") == nullptr) {
+            setenv("NCCL_MIN_P2P_NCHANNELS", std::to_string(std::min<uint32_t>(64, Pow2Up(inEffect * 7))).c_str(), 0);
+        }
     }
     g_p2pPerPeer = EnvU32("NCCL_NCHANNELS_PER_PEER", 0);
     g_p2pMin = EnvU32("NCCL_MIN_P2P_NCHANNELS", 0);
@@ -489,9 +480,15 @@ public:
         bool consumed = false;
         bool failed = false;
     };
-    explicit LoopbackWorld(uint32_t n) : n_(n), boxes_(size_t(n) * n), slots_(n) {}
+    explicit LoopbackWorld(uint32_t n) : n_(n), boxes_(size_t(n) * n), slots_(n)
+    {
+        const char* e = std::getenv("HCCL_AMD_LOOPBACK_EVENT_DESTROY");  // diagnostics, read once per world
+        immediateDestroy_ = e != nullptr && std::strcmp(e, "immediate") == 0;
+    }
     ~LoopbackWorld()
     {
+        // every rank's communicator has drained its streams before it released the world (~Comm)
+        for (hipEvent_t e : retired_) (void)hipEventDestroy(e);
         if (failHost_ != nullptr) (void)hipHostFree(failHost_);
     }
     LoopbackWorld(const LoopbackWorld&) = delete;
@@ -511,6 +508,30 @@ public:
     // the failure word of the world's IPC launches (Transport::SharedFailWord), allocated by the first rank to ask
     uint32_t* failHost_ = nullptr;
     uint32_t* failDev_ = nullptr;
+
+    // Events of the links, retired once both sides have enqueued their waits on them. They were destroyed at once
+    // before r05, right after another thread's stream had been told to wait on them: HIP may hand a
+    // destroyed event's completion signal to a new event while a wait on it is still queued. They now live until the
+    // world is torn down; past kRetiredMax the oldest completed ones go, far behind any wait still queued.
+    // HCCL_AMD_LOOPBACK_EVENT_DESTROY=immediate restores the old lifetime (the r05 experiment).
+    static constexpr size_t kRetiredMax = 16384;
+    bool immediateDestroy_ = false;
+    std::deque<hipEvent_t> retired_;
+
+    void Retire(hipEvent_t e)  // mu_ not held
+    {
+        if (e == nullptr) return;
+        if (immediateDestroy_) {
+            (void)hipEventDestroy(e);
+            return;
+        }
+        std::lock_guard<std::mutex> lk(mu_);
+        retired_.push_back(e);
+        while (retired_.size() > kRetiredMax && hipEventQuery(retired_.front()) == hipSuccess) {
+            (void)hipEventDestroy(retired_.front());
+            retired_.pop_front();
+        }
+    }
 
     uint32_t* FailWord(uint32_t** dev)
     {
@@ -639,11 +660,9 @@ public:
                 }
             }
             if (e->failed) result = HCCL_E_INTERNAL;
-            if (e->done != nullptr) {
-                if (hipStreamWaitEvent(stream, e->done, 0) != hipSuccess) result = HCCL_E_RUNTIME;
-                (void)hipEventDestroy(e->done);
-            }
-            (void)hipEventDestroy(e->ready);
+            if (e->done != nullptr && hipStreamWaitEvent(stream, e->done, 0) != hipSuccess) result = HCCL_E_RUNTIME;
+            w.Retire(e->done);
+            w.Retire(e->ready);
         }
         return result;
     }

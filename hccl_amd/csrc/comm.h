@@ -15,6 +15,7 @@
 #include <thread>
 #include <vector>
 
+#include "config.h"
 #include "internal.h"
 #include "ipc.h"
 #include "schedule.h"
@@ -49,9 +50,9 @@ public:
     virtual bool Abortable() const { return false; }
     // ncclCommAbort: in-flight device work returns, later groups fail. Callable from any thread.
     virtual void Abort() {}
-    // The teardown will run later, on one rank alone (a destroy deferred behind live graphs): it must not wait on
-    // peers (RCCL: abort instead of finalize).
-    virtual void SetLocalTeardown() {}
+    // on: the teardown will run later, on one rank alone (a destroy deferred behind live graphs), and must not wait on
+    // peers (RCCL: abort instead of finalize); off: it runs now, with its peers (the deferral fell through).
+    virtual void SetLocalTeardown(bool on) {}
     // Loopback world: the pinned failure word all its ranks share (the world's single IPC launch writes it), owned by
     // the world so that it outlives every rank's communicator; *dev receives its device address. nullptr elsewhere.
     virtual uint32_t* SharedFailWord(uint32_t** dev)
@@ -97,7 +98,6 @@ struct CompiledSchedule {
     bool hasPlan = false;
     std::vector<UnitPlan> plan;
     uint64_t lastUse = 0;
-    mutable uint64_t eagerRuns = 0;  // RunCompiled: runs issued eagerly (a graph is captured only after one)
 };
 
 // One rank's executor program captured into a HIP graph for exact buffers, stream, dtype and op (RunCompiled).
@@ -107,8 +107,16 @@ struct GraphEntry {
     hipStream_t stream = nullptr;
     HcclDataType dt = HCCL_DATA_TYPE_RESERVED;
     HcclReduceOp op = HCCL_REDUCE_RESERVED;
-    hipGraphExec_t exec = nullptr;  // nullptr: capture failed for this key, run eagerly
+    bool single = false;            // a single-stream program (Execute's singleStream)
+    bool tried = false;             // the capture was attempted (the key's second call)
+    hipGraphExec_t exec = nullptr;  // nullptr: not captured (first call) or the capture failed: run eagerly
     uint64_t lastUse = 0;
+};
+
+// An evicted executor graph, destroyed once `done` (recorded after its last possible launch) has completed.
+struct RetiredGraph {
+    hipGraphExec_t exec;
+    hipEvent_t done;
 };
 
 struct Comm;
@@ -191,6 +199,7 @@ struct Comm {
     uint32_t rank = 0;
     uint32_t nRanks = 1;
     int device = 0;
+    CommConfig cfg;  // the environment at creation (config.h); HcclAmdCommSetConfig changes it under mu
     std::unique_ptr<Transport> transport;
     hipStream_t commStream = nullptr;
     hipStream_t reduceStream = nullptr;
@@ -245,6 +254,7 @@ struct Comm {
     // Executor graphs (RunCompiled): the two-stream programs of the RCCL path, captured once on a private stream and
     // replayed with one hipGraphLaunch per call. graphLaunches / graphCaptures count them (HcclAmdCommGraphStats).
     std::vector<GraphEntry> graphs;
+    std::vector<RetiredGraph> retiredGraphs;
     hipStream_t captureStream = nullptr;
     uint64_t graphLaunches = 0;
     uint64_t graphCaptures = 0;
@@ -286,10 +296,6 @@ HcclResult IpcPlanForFamily(int32_t opType, int32_t family, uint32_t n, uint64_t
 // engine; *plan receives the one-sided kernel's plan for a matched variant.
 int32_t SelectAivPlan(int32_t opType, uint32_t n, uint64_t count, HcclDataType dt, HcclReduceOp op, bool strict,
                       bool aivOnly, uint64_t cclBytes, uint32_t coreLimit, IpcPlan* plan, uint32_t* group);
-// HCCL_AMD_AIV_CORE_LIMIT (default 48, MAX_NUM_BLOCKS of aiv_defines.h:35).
-uint32_t AivCoreLimit();
-// HCCL_OP_EXPANSION_MODE selects the AIV engine ("AIV").
-bool ExpansionModeAiv();
 // Collective: every rank's IPC kernels have finished before any rank unmaps or frees (called by ~Comm).
 void IpcQuiesce(Comm& c);
 void IpcRelease(Comm& c);
@@ -322,11 +328,12 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
 
 std::vector<UnitPlan> PlanUnits(const std::vector<HcclAmdIrOp>& ops, void* const bufs[3], uint64_t es);
 
-// Runs a compiled two-stream collective: from the communicator's graph cache when the transport allows capture (RCCL)
-// and HCCL_AMD_GRAPH_CACHE is not 0 (the first run of a compiled collective is eager, later ones with the same
-// buffers, stream, dtype and op replay one captured graph), else through Execute.
+// Runs a compiled collective (the two-stream program, or with `single` the single-stream one): from the communicator's
+// graph cache when the transport allows capture (RCCL) and HCCL_AMD_GRAPH_CACHE is not 0 (the first run of a compiled
+// collective is eager, later ones with the same buffers, stream, dtype, op and mode replay one captured graph), else
+// through Execute.
 HcclResult RunCompiled(Comm& c, const CompiledSchedule& cs, void* const bufs[3], HcclDataType dt, HcclReduceOp op,
-                       hipStream_t user);
+                       hipStream_t user, bool single = false);
 void ReleaseGraphs(Comm& c);
 
 // Entry/exit of every collective: under the caller's capture, NoteCapture; otherwise wait for the previous call's end
@@ -355,9 +362,5 @@ HcclResult CompileCollective(Comm& c, const ScheduleParams& p, void* const bufs[
 constexpr int32_t kProgramOpType = -1;
 HcclResult CompileProgram(Comm& c, const HcclAmdIrOp* ops, uint64_t numOps, uint32_t elemSize, void* const bufs[3],
                           const CompiledSchedule** out);
-
-// Collectives whose per-rank payload is at most this many bytes run single-stream (HCCL_AMD_SINGLE_STREAM_BYTES,
-// default 1 MiB).
-uint64_t SingleStreamBytes();
 
 }  // namespace hccl_amd

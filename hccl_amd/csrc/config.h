@@ -1,0 +1,45 @@
+// config.h — a communicator's configuration, read from the environment once, when the communicator is created.
+//
+// The reference reads its environment once per process (InitEnvConfig, src/common/alg_env_config.cc:176) and its
+// collectives consult the parsed values. Here every collective consults Comm::cfg; no collective calls getenv (a
+// getenv racing a setenv on another thread is undefined behaviour). HcclAmdCommSetConfig changes one entry afterwards
+// (tests, the bench's A/B rows).
+#pragma once
+
+#include <cstdint>
+
+#include "internal.h"
+
+namespace hccl_amd {
+
+struct CommConfig {
+    bool strict = false;                          // HCCL_DETERMINISTIC=strict (alg_env_config.cc:1036-1076)
+    bool expansionAiv = false;                    // HCCL_OP_EXPANSION_MODE=AIV
+    uint32_t aivCoreLimit = 48;                   // HCCL_AMD_AIV_CORE_LIMIT (MAX_NUM_BLOCKS, aiv_defines.h:35)
+    uint64_t singleStreamBytes = 1ull << 20;      // HCCL_AMD_SINGLE_STREAM_BYTES: single-stream programs up to this
+    uint64_t smallIpcBytes = 1ull << 20;          // HCCL_AMD_SMALL_IPC_BYTES: AllReduce up to this on the one-sided kernel
+    bool planCache = true;                        // HCCL_AMD_PLAN_CACHE
+    uint32_t graphCache = 16;                     // HCCL_AMD_GRAPH_CACHE: executor graphs kept (0 = every call eager)
+    int32_t ipcLightFence = -1;                   // HCCL_AMD_IPC_LIGHT_FENCE: -1 = per mode (ipc.cc), 0, 1
+    bool ipcNt = true;                            // HCCL_AMD_IPC_NT
+    uint32_t ipcThreads = 256;                    // HCCL_AMD_IPC_THREADS (256 or 512)
+    uint64_t ipcTileBytes = 0;                    // HCCL_AMD_IPC_TILE_KIB (0 = one window per block)
+    uint64_t ipcTimeoutMs = 1091000;              // HCCL_AMD_IPC_TIMEOUT_MS, else HCCL_EXEC_TIMEOUT (AIV rule)
+    // HCCL_AMD_IPC_STAGING_MIB (read at the IPC set-up): the slot area per rank; the result area is as large, and so is
+    // each alternate slot area, so 2 GiB of uncached HBM per rank once a communicator makes its first IPC call. 512 MiB
+    // areas run the C3-sized calls in one staging round where 128 MiB areas took 2-4, 5-12 % faster at n = 2 and 4
+    // (profiles/r03_ipc_variant_ab_shapes.jsonl): each round costs two barriers and three phase fills and drains.
+    uint64_t ipcStagingBytes = 512ull << 20;
+    bool ipcStagingCached = false;                // HCCL_AMD_IPC_STAGING_CACHED (diagnostics)
+    bool ipcTrace = false;                        // HCCL_AMD_IPC_TRACE (diagnostics)
+    bool ipcL2Scrub = true;                       // HCCL_AMD_IPC_L2_SCRUB
+};
+
+// The configuration a communicator created now takes.
+CommConfig ReadCommConfig();
+// HcclAmdCommSetConfig / HcclAmdCommGetConfig by HcclAmdConfigKey; HCCL_E_PARA for an unknown key or a value outside
+// the key's range.
+HcclResult SetConfigEntry(CommConfig& cfg, int32_t key, int64_t value);
+HcclResult GetConfigEntry(const CommConfig& cfg, int32_t key, int64_t* value);
+
+}  // namespace hccl_amd

@@ -4,7 +4,7 @@
 // hcomm tasks on a main "thread" and slave threads joined by notifies: alg_data_trans_wrapper.cc:1005-1073,
 // SURVEY.md §8a rows R5, R8). Here:
 //   * SEND/RECV records with one group id become one transport group on the link stream (RCCL over xGMI);
-//   * REDUCE and COPY records go to the reduce stream (HIP kernels of reduce_kernels.hip / a DMA copy);
+//   * REDUCE and COPY records go to the reduce stream (the fold kernels and the copy kernel of reduce_kernels.hip);
 //   * dependencies are not written by hand: every record's byte ranges (absolute device addresses, so in-place
 //     buffers alias correctly) are checked against the earlier units of the OTHER stream, and the latest
 //     conflicting unit (RAW, WAR or WAW) becomes a hipStreamWaitEvent. Same-stream order is program order.
@@ -293,12 +293,6 @@ void Relation(const uint64_t ext[3], void* const bufs[3], int64_t rel[3])
     }
 }
 
-bool PlanCacheEnabled()
-{
-    const char* e = std::getenv("HCCL_AMD_PLAN_CACHE");  // read per call: tests switch it
-    return e == nullptr || std::strcmp(e, "0") != 0;
-}
-
 }  // namespace
 
 namespace {
@@ -309,8 +303,7 @@ template <class Make>
 HcclResult FindOrCompile(Comm& c, const ScheduleParams& p, void* const bufs[3], bool withPlan, Make make,
                          const CompiledSchedule** out)
 {
-    const bool cache = PlanCacheEnabled();
-    if (!cache) c.compiled.clear();
+    if (!c.cfg.planCache) c.compiled.clear();  // HCCL_AMD_PLAN_CACHE=0: compile every call
     CompiledSchedule* hit = nullptr;
     for (auto& e : c.compiled) {
         if (SameParams(e->params, p)) {
@@ -544,25 +537,16 @@ EntryScope::~EntryScope()
 
 namespace {
 
-// HCCL_AMD_GRAPH_CACHE: the number of executor graphs a communicator keeps (default 16; 0 = every call eager). Read
-// per call: tests switch it.
-size_t GraphCacheSize()
-{
-    const char* e = std::getenv("HCCL_AMD_GRAPH_CACHE");
-    if (e == nullptr || *e == '\0') return 16;
-    return static_cast<size_t>(std::strtoull(e, nullptr, 10));
-}
-
 // Captures the program on the communicator's private stream (thread-local capture mode: other threads' HIP calls do
 // not disturb it, and it disturbs no capture of theirs). Under capture Execute posts the transport groups on the
 // capturing stream and forks only the folds (executor.cc Execute), the RCCL capture pattern that instantiates.
 HcclResult CaptureProgram(Comm& c, const CompiledSchedule& cs, void* const bufs[3], HcclDataType dt, HcclReduceOp op,
-                          hipGraphExec_t* exec)
+                          bool single, hipGraphExec_t* exec)
 {
     *exec = nullptr;
     if (c.captureStream == nullptr) HIP_CHK(hipStreamCreateWithFlags(&c.captureStream, hipStreamNonBlocking));
     HIP_CHK(hipStreamBeginCapture(c.captureStream, hipStreamCaptureModeThreadLocal));
-    const HcclResult r = Execute(c, cs.sched.ops, bufs, dt, op, c.captureStream, false, &cs.plan);
+    const HcclResult r = Execute(c, cs.sched.ops, bufs, dt, op, c.captureStream, single, single ? nullptr : &cs.plan);
     hipGraph_t g = nullptr;
     const hipError_t e = hipStreamEndCapture(c.captureStream, &g);
     if (r != HCCL_SUCCESS || e != hipSuccess || g == nullptr) {
@@ -583,36 +567,59 @@ HcclResult CaptureProgram(Comm& c, const CompiledSchedule& cs, void* const bufs[
 
 }  // namespace
 
-HcclResult RunCompiled(Comm& c, const CompiledSchedule& cs, void* const bufs[3], HcclDataType dt, HcclReduceOp op,
-                       hipStream_t user)
+// Destroys the retired executables whose last launch has completed (all of them, waiting, when wait is set).
+void ReapRetiredGraphs(Comm& c, bool wait)
 {
-    const size_t cap = GraphCacheSize();
+    for (size_t i = 0; i < c.retiredGraphs.size();) {
+        RetiredGraph& g = c.retiredGraphs[i];
+        if (wait) (void)hipEventSynchronize(g.done);
+        if (hipEventQuery(g.done) == hipErrorNotReady) {
+            ++i;
+            continue;
+        }
+        (void)hipGraphExecDestroy(g.exec);
+        (void)hipEventDestroy(g.done);
+        c.retiredGraphs.erase(c.retiredGraphs.begin() + static_cast<std::ptrdiff_t>(i));
+    }
+}
+
+HcclResult RunCompiled(Comm& c, const CompiledSchedule& cs, void* const bufs[3], HcclDataType dt, HcclReduceOp op,
+                       hipStream_t user, bool single)
+{
+    const size_t cap = c.cfg.graphCache;
+    const std::vector<UnitPlan>* plan = single ? nullptr : &cs.plan;
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     HIP_CHK(hipStreamIsCapturing(user, &st));
     if (cap == 0 || st != hipStreamCaptureStatusNone || !c.transport->Abortable()) {
-        return Execute(c, cs.sched.ops, bufs, dt, op, user, false, &cs.plan);
+        return Execute(c, cs.sched.ops, bufs, dt, op, user, single, plan);
     }
+    if (!c.retiredGraphs.empty()) ReapRetiredGraphs(c, false);
     GraphEntry* hit = nullptr;
     for (GraphEntry& g : c.graphs) {
-        if (g.stream == user && g.dt == dt && g.op == op && std::memcmp(g.bufs, bufs, sizeof g.bufs) == 0 &&
-            SameParams(g.params, cs.params)) {
+        if (g.stream == user && g.dt == dt && g.op == op && g.single == single &&
+            std::memcmp(g.bufs, bufs, sizeof g.bufs) == 0 && SameParams(g.params, cs.params)) {
             hit = &g;
             break;
         }
     }
     if (hit == nullptr) {
-        // The first run of a compiled collective is eager: it makes RCCL connect to the program's peers, which a
-        // capture must not have to do.
-        if (cs.eagerRuns++ == 0) return Execute(c, cs.sched.ops, bufs, dt, op, user, false, &cs.plan);
+        // A key's first call runs eagerly (it makes RCCL connect to the program's peers, which a capture must not have
+        // to do) and leaves a placeholder; its second call captures. A workload whose buffers change from call to call
+        // therefore never pays a capture it cannot replay.
         if (c.graphs.size() >= cap) {
-            // The evicted executable may still run: the host is ahead of the device. Every earlier call precedes the
-            // previous call's end on the device (EntryScope orders each call after the last one's tail), so once that
-            // tail has completed no launch of it is in flight. Eviction is rare (more distinct calls than the cache
-            // holds) and already pays a capture, so the wait costs little.
-            if (c.tail != nullptr) HIP_CHK(hipEventSynchronize(c.tail));
+            // The evicted executable may still run: the host is ahead of the device. It is retired with an
+            // event recorded on this call's stream before this call's work: EntryScope has already ordered this stream
+            // after the previous call's end, which every earlier launch precedes, so once the event has completed no
+            // launch of the executable is in flight. It is destroyed then (ReapRetiredGraphs at a later call or at
+            // teardown); the host never waits here.
             auto lru = std::min_element(c.graphs.begin(), c.graphs.end(),
                                         [](const GraphEntry& x, const GraphEntry& y) { return x.lastUse < y.lastUse; });
-            if (lru->exec != nullptr) (void)hipGraphExecDestroy(lru->exec);
+            if (lru->exec != nullptr) {
+                RetiredGraph r{lru->exec, nullptr};
+                HIP_CHK(hipEventCreateWithFlags(&r.done, hipEventDisableTiming));
+                HIP_CHK(hipEventRecord(r.done, user));
+                c.retiredGraphs.push_back(r);
+            }
             c.graphs.erase(lru);
         }
         GraphEntry e;
@@ -621,14 +628,20 @@ HcclResult RunCompiled(Comm& c, const CompiledSchedule& cs, void* const bufs[3],
         e.stream = user;
         e.dt = dt;
         e.op = op;
-        (void)CaptureProgram(c, cs, bufs, dt, op, &e.exec);
-        if (e.exec != nullptr) ++c.graphCaptures;
+        e.single = single;
+        e.lastUse = ++c.compileTick;
         c.graphs.push_back(e);
-        hit = &c.graphs.back();
+        return Execute(c, cs.sched.ops, bufs, dt, op, user, single, plan);
+    }
+    if (!hit->tried) {
+        hit->tried = true;
+        (void)CaptureProgram(c, cs, bufs, dt, op, single, &hit->exec);
+        if (hit->exec != nullptr) ++c.graphCaptures;
     }
     hit->lastUse = ++c.compileTick;
-    if (hit->exec == nullptr) return Execute(c, cs.sched.ops, bufs, dt, op, user, false, &cs.plan);
-    WatchScope watch(c.watchdog.get(), user);
+    if (hit->exec == nullptr) return Execute(c, cs.sched.ops, bufs, dt, op, user, single, plan);
+    // a single-stream program is not start-stamped eagerly either (the watchdog infers its start, watchdog.cc)
+    WatchScope watch(c.watchdog.get(), user, !single);
     HIP_CHK(hipGraphLaunch(hit->exec, user));
     ++c.graphLaunches;
     return HCCL_SUCCESS;
@@ -640,6 +653,7 @@ void ReleaseGraphs(Comm& c)
         if (g.exec != nullptr) (void)hipGraphExecDestroy(g.exec);
     }
     c.graphs.clear();
+    ReapRetiredGraphs(c, true);
     if (c.captureStream != nullptr) (void)hipStreamDestroy(c.captureStream);
     c.captureStream = nullptr;
 }

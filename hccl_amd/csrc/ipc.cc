@@ -29,22 +29,6 @@ struct RawPtrs {
     uint8_t ok;
 };
 
-// HCCL_AMD_IPC_L2_SCRUB=0 skips the scrub of fresh staging (diagnostics only: tests/test_gpu_collectives.py shows the
-// stale-line failure it prevents).
-bool ScrubEnabled()
-{
-    const char* e = std::getenv("HCCL_AMD_IPC_L2_SCRUB");
-    return e == nullptr || std::strcmp(e, "0") != 0;
-}
-
-// HCCL_AMD_IPC_TRACE=1 (read at set-up): the kernel stamps its phases per block (IpcTraceSlot), read back with
-// HcclAmdCommIpcTrace. Diagnostics for the phase timeline (tools/ipc_phase_trace.py); off by default.
-bool IpcTraceEnabled()
-{
-    const char* e = std::getenv("HCCL_AMD_IPC_TRACE");
-    return e != nullptr && std::strcmp(e, "1") == 0;
-}
-
 // The four areas inside one staging allocation at base (every rank has the same layout).
 void AreasOf(const IpcState& s, void* base, void* areas[kIpcAreas])
 {
@@ -62,7 +46,7 @@ HcclResult IpcSetup(Comm& c)
     if (s.unavailable) return HCCL_E_NOT_SUPPORT;
     const uint32_t n = c.nRanks, me = c.rank;
     s.blocks = kIpcBlocks;
-    const uint64_t area = IpcStagingBytes();
+    const uint64_t area = c.cfg.ipcStagingBytes;
     s.stgInBytes = area;
     s.stgResBytes = area;  // results of a whole round, in round coordinates
     // slots of the single-barrier kinds, two areas used alternately: as large as the others, within the one
@@ -74,8 +58,7 @@ HcclResult IpcSetup(Comm& c)
     // HCCL_AMD_IPC_STAGING_CACHED=1 (diagnostics, one device only: the r03 A/B of what uncached staging costs) puts
     // the slot and result areas in ordinary cached memory; the barriers' system-scope release and acquire then carry
     // the hand-off through the L2s of that one device.
-    const char* cachedEnv = std::getenv("HCCL_AMD_IPC_STAGING_CACHED");
-    const bool cached = cachedEnv != nullptr && std::strcmp(cachedEnv, "1") == 0;
+    const bool cached = c.cfg.ipcStagingCached;
     s.cachedStaging = cached;
     // One allocation [in][results][alternate 0][alternate 1], below 2 GiB: hipIpcOpenMemHandle never returned for a
     // 2 GiB allocation on this stack (the r03 512 MiB areas in one 2 GiB block hung the rank-mode set-up;
@@ -94,11 +77,11 @@ HcclResult IpcSetup(Comm& c)
               hipHostMalloc(reinterpret_cast<void**>(&s.failHost), 64, hipHostMallocCoherent | hipHostMallocMapped) ==
                   hipSuccess &&
               hipHostGetDevicePointer(reinterpret_cast<void**>(&s.failDev), s.failHost, 0) == hipSuccess &&
-              hipDeviceSynchronize() == hipSuccess && (!ScrubEnabled() || ScrubL2(c.reduceStream) == HCCL_SUCCESS) &&
+              hipDeviceSynchronize() == hipSuccess && (!c.cfg.ipcL2Scrub || ScrubL2(c.reduceStream) == HCCL_SUCCESS) &&
               hipMemset(s.flags, 0, flagBytes) == hipSuccess && hipMemset(s.status, 0, kIpcStatusBytes) == hipSuccess &&
               hipDeviceSynchronize() == hipSuccess;
-    if (ok && IpcTraceEnabled()) {
-        // phase stamps (diagnostics): every rank's and block's row, so a loopback world's one launch fits too
+    if (ok && c.cfg.ipcTrace) {
+        // phase stamps (diagnostics, HCCL_AMD_IPC_TRACE; HcclAmdCommIpcTrace reads them back): every rank's and block's row, so a loopback world's one launch fits too
         const size_t tb = size_t(kIpcMaxRanks) * kIpcMaxBlocks * kIpcTraceSlots * sizeof(uint64_t);
         ok = hipMalloc(reinterpret_cast<void**>(&s.trace), tb) == hipSuccess && hipMemset(s.trace, 0, tb) == hipSuccess &&
              hipDeviceSynchronize() == hipSuccess;
@@ -206,16 +189,6 @@ bool Aligned16(const void* p, const void* q)
     return ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(q)) & 15u) == 0;
 }
 
-// Block shares and cache policy of the copy and fold loops (r03 A/B, tools/ipc_variant_ab.py): HCCL_AMD_IPC_TILE_KIB
-// (0 = one contiguous window per block) and HCCL_AMD_IPC_NT (1 = non-temporal loads and stores). Read per call, and
-// equal on every rank (block b pairs with block b of each peer over the same coordinates).
-uint64_t IpcTileBytes()
-{
-    const char* e = std::getenv("HCCL_AMD_IPC_TILE_KIB");
-    if (e == nullptr || *e == '\0') return 0;
-    return std::strtoull(e, nullptr, 10) << 10;
-}
-
 // Barrier fences (IpcArgs::fence). Every byte a barrier hands over lives in uncached staging, which no L2 holds: the
 // storing waves' vmcnt drains order the data before the flag (a store completes at memory), and an agent-scope acquire
 // (the CU's L1) suffices for the reader, whose loads go to memory. The user buffers are never handed over inside the
@@ -223,55 +196,16 @@ uint64_t IpcTileBytes()
 // kernel boundaries, which make plain and non-temporal stores visible to the next kernel on every XCD
 // (tools/coherence_probe.hip, profiles/r04_coherence_probe.jsonl). The light fences skip the system-scope release and
 // acquire, which write back and invalidate the whole XCD L2 for every block: 3-13 % per call in loopback worlds
-// (profiles/r03_ipc_variant_ab_fence.jsonl). Default: light in a loopback world (one device, the argument above and
-// tests/test_gpu_collectives.py cover it), system scope in rank mode, whose stores cross to other devices' staging
-// through imported mappings that no test on this pool has exercised over xGMI. HCCL_AMD_IPC_LIGHT_FENCE=1
-// or 0 forces either. The r03 stale-operand failure blamed on the light fences was the loopback link's
-// hipMemcpyAsync, with either setting. Read per call, equal on every rank.
-bool IpcLightFence(bool sharedDevice)
+// (profiles/r03_ipc_variant_ab_fence.jsonl). Default (CommConfig::ipcLightFence = -1): light in a loopback world, where
+// every store goes through the owner's own uncached pointer; system scope in rank mode, whose stores reach the peers'
+// staging through hipIpcOpenMemHandle mappings, and an imported mapping need not keep the exporter's uncached memory
+// type (imported mappings). HCCL_AMD_IPC_LIGHT_FENCE=1 or 0 forces either. Equal on every rank.
+bool IpcLightFence(const Comm& c)
 {
-    const char* e = std::getenv("HCCL_AMD_IPC_LIGHT_FENCE");
-    if (e == nullptr || *e == '\0') return sharedDevice;
-    return std::strcmp(e, "0") != 0;
-}
-
-// HCCL_AMD_IPC_THREADS: threads per workgroup, 256 (default) or 512 (r03 A/B). Read per call, equal on every rank.
-uint32_t IpcThreads()
-{
-    const char* e = std::getenv("HCCL_AMD_IPC_THREADS");
-    return (e != nullptr && std::strcmp(e, "512") == 0) ? 512u : static_cast<uint32_t>(kIpcBlock);
-}
-
-bool IpcNonTemporal()
-{
-    const char* e = std::getenv("HCCL_AMD_IPC_NT");
-    return e == nullptr || std::strcmp(e, "0") != 0;  // default on: 2-3 % at n = 2, 4, 8 (profiles/r03_ipc_variant_ab_{policy,shapes}.jsonl)
+    return c.cfg.ipcLightFence < 0 ? c.transport->SharedDevice() : c.cfg.ipcLightFence != 0;
 }
 
 }  // namespace
-
-// Wall-time bound of one barrier wait, in 100 MHz s_memrealtime ticks. The IPC kernel is the reference's AIV engine,
-// so HCCL_EXEC_TIMEOUT follows its AIV-mode rule (docs/zh/user_guide/hccl_env/HCCL_EXEC_TIMEOUT.md): seconds with
-// at most two decimals, default 1091, and 0 or anything above 1091 taken as 1091. A malformed value is ignored with
-// the default, as ParseExecTimeout does (src/common/alg_env_config.cc:75-110). HCCL_AMD_IPC_TIMEOUT_MS (1 ms ..
-// 1 h), when set, takes precedence: it is the tests' and the benchmark's short bound.
-uint64_t IpcTimeoutTicks()
-{
-    constexpr uint64_t kTicksPerMs = 100000;
-    const char* e = std::getenv("HCCL_AMD_IPC_TIMEOUT_MS");
-    if (e != nullptr && *e != '\0') {
-        const unsigned long long v = std::strtoull(e, nullptr, 0);
-        if (v >= 1 && v <= 3600000ull) return v * kTicksPerMs;
-    }
-    constexpr uint64_t kAivMaxMs = 1091000;
-    uint64_t ms = kAivMaxMs;
-    double sec = 0;
-    if (ParseExecTimeoutSeconds(std::getenv("HCCL_EXEC_TIMEOUT"), &sec) && sec > 0) {
-        const double m = sec * 1000.0;
-        ms = m >= double(kAivMaxMs) ? kAivMaxMs : std::max<uint64_t>(1, static_cast<uint64_t>(m + 0.5));
-    }
-    return ms * kTicksPerMs;
-}
 
 void IpcQuiesce(Comm& c)
 {
@@ -324,17 +258,6 @@ uint32_t DefaultIpcBlocks(uint64_t bytes)
     if (bytes <= (32ull << 20)) return 64;
     if (bytes <= (64ull << 20)) return 128;
     return 256;
-}
-
-uint64_t IpcStagingBytes()
-{
-    const char* e = std::getenv("HCCL_AMD_IPC_STAGING_MIB");
-    if (e != nullptr && *e != '\0') {
-        const unsigned long long v = std::strtoull(e, nullptr, 10);
-        // the staging allocation stays below 2 GiB (IpcSetup): areas of at most 1000 MiB
-        if (v >= 16 && v <= 1000) return static_cast<uint64_t>(v) << 20;
-    }
-    return kIpcStagingBytes;
 }
 
 // ------------------------------------------------------------------------------------------------ plans
@@ -422,26 +345,6 @@ HcclResult IpcPlanRhd(uint32_t n, IpcPlan* pl)
     p.geom = kIpcGeomWhole;
     *pl = p;
     return HCCL_SUCCESS;
-}
-
-uint32_t AivCoreLimit()
-{
-    // The reference takes the vector-core count from the comm config (aivCoreLimit) or the device
-    // (aclrtGetResInCurrentThread(ACL_RT_DEV_RES_VECTOR_CORE), op_common.cc:1063-1078). It only decides the AIV
-    // kernels' variant and slice boundaries here, so it is a parameter: HCCL_AMD_AIV_CORE_LIMIT, default 48
-    // (MAX_NUM_BLOCKS, aiv_defines.h:35).
-    const char* e = std::getenv("HCCL_AMD_AIV_CORE_LIMIT");
-    if (e != nullptr && *e != '\0') {
-        const unsigned long long v = std::strtoull(e, nullptr, 10);
-        if (v >= 1 && v <= 4096) return static_cast<uint32_t>(v);
-    }
-    return 48;
-}
-
-bool ExpansionModeAiv()
-{
-    const char* e = std::getenv("HCCL_OP_EXPANSION_MODE");  // read per call, like HCCL_DETERMINISTIC
-    return e != nullptr && std::strcmp(e, "AIV") == 0;
 }
 
 int32_t SelectAivPlan(int32_t opType, uint32_t n, uint64_t count, HcclDataType dt, HcclReduceOp op, bool strict,
@@ -591,7 +494,7 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
     // so ranks of a node agree on it.
     {
         const uint32_t here = c.transport->SharedDevice() ? n : std::max<uint32_t>(1, s.ranksOnDevice);
-        const uint32_t resident = IpcResidentBlocks(dt, op, plan.order == kIpcRhd, IpcThreads());
+        const uint32_t resident = IpcResidentBlocks(dt, op, plan.order == kIpcRhd, c.cfg.ipcThreads);
         if (resident != 0) s.blocks = std::max<uint32_t>(1, std::min(s.blocks, resident / here));
     }
     const uint64_t V = 16 / es;
@@ -609,7 +512,7 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
     a.order = plan.order;
     a.subMode = plan.subMode;
     a.root = root;
-    a.timeoutTicks = IpcTimeoutTicks();  // a lost peer ends the kernel with status bit 0, never a hang
+    a.timeoutTicks = c.cfg.ipcTimeoutMs * 100000;  // a lost peer ends the kernel with status bit 0, never a hang
     a.status = s.status;
     a.failHost = s.failDev;
     a.callSeq = ++s.callSeq;  // equal on every rank of a loopback world (each runs this once per call)
@@ -699,10 +602,10 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
         const uint64_t widest = g.balanced ? g.group * g.chunkLen + std::min<uint64_t>(g.group, g.rem) : g.chunkLen;
         g.piece = std::max<uint64_t>(V, std::min(slotCap, (widest + V - 1) / V * V));
         g.blockElems = ((g.piece + s.blocks - 1) / s.blocks + V - 1) / V * V;
-        g.tileElems = IpcTileBytes() / es / V * V;  // 0: contiguous windows
-        g.nt = IpcNonTemporal() ? 1u : 0u;
-        g.fence = (IpcLightFence(c.transport->SharedDevice()) && !s.cachedStaging) ? 1u : 0u;
-        g.threads = IpcThreads();
+        g.tileElems = c.cfg.ipcTileBytes / es / V * V;  // 0: contiguous windows (HCCL_AMD_IPC_TILE_KIB)
+        g.nt = c.cfg.ipcNt ? 1u : 0u;                     // non-temporal loads and stores (HCCL_AMD_IPC_NT)
+        g.fence = (IpcLightFence(c) && !s.cachedStaging) ? 1u : 0u;
+        g.threads = c.cfg.ipcThreads;                    // HCCL_AMD_IPC_THREADS
         g.rounds = static_cast<uint32_t>((widest + g.piece - 1) / g.piece);
         g.epochSpan = (single ? 1 : 2) * g.rounds;
     };

@@ -217,13 +217,8 @@ uint32_t DefaultIpcBlocks(uint64_t bytes);  // workgroups per launch when the co
 constexpr size_t kIpcStatusBytes = 32;  // status words (IpcArgs::status)
 constexpr int kIpcEpochWord = 4;
 constexpr int kIpcDoneWord = 5;
-// Slot area per rank (default); the result area is as large, and so is each alternate slot area: 2 GiB of uncached
-// HBM per rank once a communicator makes its first IPC call. r03: 512 MiB areas run the C3-sized calls in one staging
-// round where 128 MiB areas took 2-4, 5-12 % faster at n = 2 and 4 (tools/ipc_variant_ab.py,
-// profiles/r03_ipc_variant_ab_{policy,shapes}.jsonl); each round costs two cross-rank barriers and three phase fills and drains.
-constexpr uint64_t kIpcStagingBytes = 512ull << 20;
-uint64_t IpcStagingBytes();  // HCCL_AMD_IPC_STAGING_MIB (16 .. 1000) or kIpcStagingBytes; equal on every rank
-// Bound of the one staging allocation of a rank (IpcSetup): a 2 GiB allocation's IPC handle never opened.
+// The staging allocation of a rank (slot, result and two alternate areas) stays below 2 GiB: hipIpcOpenMemHandle never
+// returned for a 2 GiB allocation on this stack (IpcSetup). The area size is CommConfig::ipcStagingBytes.
 constexpr uint64_t kIpcStagingMaxBytes = 2047ull << 20;
 
 }  // namespace hccl_amd

@@ -45,12 +45,14 @@ HcclResult CheckReduceOp(HcclDataType dt, HcclReduceOp op)
     return HCCL_SUCCESS;
 }
 
-// HCCL_DETERMINISTIC=strict (alg_env_config.cc:1036-1076) with fp16/fp32/bf16/fp64, SUM/PROD and more than two
-// ranks selects the order-preserved tree (IsNeedStrictModeForOrderPreserved, order_preserved_common.h:63-73).
-bool NeedStrictOrder(int32_t opType, HcclDataType dt, HcclReduceOp op, uint32_t nRanks)
+// HCCL_DETERMINISTIC=strict (alg_env_config.cc:1036-1076; CommConfig::strict) with fp16/fp32/bf16/fp64, SUM/PROD and
+// more than two ranks selects the order-preserved tree (IsNeedStrictModeForOrderPreserved, order_preserved_common.h:
+// 63-73). At n <= 8 the reference runs it as InsTempReduceScatterOrderPreservedLevel1 (reduce_scatter_auto_selector.cc:
+// 406-413), whose tree is the same O4 (schedule.cc ReduceScatterTree).
+bool NeedStrictOrder(const Comm& c, int32_t opType, HcclDataType dt, HcclReduceOp op)
 {
-    const char* e = std::getenv("HCCL_DETERMINISTIC");
-    if (e == nullptr || strcasecmp(e, "strict") != 0) return false;
+    const uint32_t nRanks = c.nRanks;
+    if (!c.cfg.strict) return false;
     if (opType != HCCL_AMD_OP_ALLREDUCE && opType != HCCL_AMD_OP_REDUCE_SCATTER) return false;
     const bool fp = dt == HCCL_DATA_TYPE_FP16 || dt == HCCL_DATA_TYPE_FP32 || dt == HCCL_DATA_TYPE_BFP16 ||
                     dt == HCCL_DATA_TYPE_FP64;
@@ -76,6 +78,28 @@ uint64_t PieceBytesFor(const Comm& c, bool singleStream, uint64_t payload)
     return singleStream ? std::max<uint64_t>(payload, 128) : 0;  // no slice is larger than the payload
 }
 
+// A pointer a kernel of this device may dereference: device memory, or host memory registered and mapped for it.
+bool DeviceAccessible(const void* p)
+{
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // an unregistered host pointer reports an error: clear it
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged ||
+           (a.type == hipMemoryTypeHost && a.devicePointer != nullptr);
+}
+
+// The one-rank collective's copy (SingleRankProc). The library's copy kernel when both buffers are device-accessible;
+// hipMemcpyAsync otherwise, which resolves pageable host memory where a kernel would fault the GPU.
+HcclResult CopyUserBuffer(void* dst, const void* src, uint64_t bytes, hipStream_t stream)
+{
+    if (bytes == 0 || dst == src) return HCCL_SUCCESS;
+    if (DeviceAccessible(dst) && DeviceAccessible(src)) return LaunchCopyBytes(dst, src, bytes, stream);
+    HIP_CHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, stream));
+    return HCCL_SUCCESS;
+}
+
 HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, uint64_t count, HcclDataType dt,
                          HcclReduceOp op, uint32_t root, hipStream_t stream)
 {
@@ -88,7 +112,7 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     if (c.nRanks == 1) {
         // SingleRankProc (op_common.cc:3042-3098): copy in -> out unless they are the same buffer.
         c.lastAlgo = HCCL_AMD_ALGO_AUTO;
-        return LaunchCopyBytes(recvBuf, sendBuf, count * es, stream);
+        return CopyUserBuffer(recvBuf, sendBuf, count * es, stream);
     }
     ScheduleParams p;
     p.opType = opType;
@@ -100,10 +124,10 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     // AIV_ONLY (the reference's OpExecuteConfig::AIV_ONLY, a communicator's configured expansion mode) takes no
     // fallback: an operation the AIV engine does not match returns HCCL_E_NOT_SUPPORT (op_common.cc:115-122).
     const bool aivOnly = p.algo == HCCL_AMD_ALGO_AIV_ONLY;
-    if (aivOnly || p.algo == HCCL_AMD_ALGO_AIV || (p.algo == HCCL_AMD_ALGO_AUTO && ExpansionModeAiv())) {
+    if (aivOnly || p.algo == HCCL_AMD_ALGO_AIV || (p.algo == HCCL_AMD_ALGO_AUTO && c.cfg.expansionAiv)) {
         IpcPlan plan{};
-        const int32_t v = SelectAivPlan(opType, c.nRanks, count, dt, op, NeedStrictOrder(opType, dt, op, c.nRanks),
-                                        aivOnly, c.cclBytes, AivCoreLimit(), &plan, nullptr);
+        const int32_t v = SelectAivPlan(opType, c.nRanks, count, dt, op, NeedStrictOrder(c, opType, dt, op), aivOnly,
+                                        c.cclBytes, c.cfg.aivCoreLimit, &plan, nullptr);
         if (v != HCCL_AMD_AIV_NOT_MATCHED) {
             const HcclResult r = RunIpcPlan(c, opType, plan, sendBuf, recvBuf, count, dt, op, root, stream);
             if (r != HCCL_E_NOT_SUPPORT) {
@@ -131,8 +155,35 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     // an IPC-only communicator (bootstrap transport without send/recv) runs every reducing op on the IPC kernel in
     // the auto family, whatever schedule family was asked for
     if (!c.transport->HasSendRecv() && p.algo != HCCL_AMD_ALGO_IPC_TWOSHOT) p.algo = HCCL_AMD_ALGO_IPC;
-    if (p.algo == HCCL_AMD_ALGO_AUTO && NeedStrictOrder(opType, dt, op, c.nRanks)) {
+    if (p.algo == HCCL_AMD_ALGO_AUTO && NeedStrictOrder(c, opType, dt, op)) {
         p.algo = HCCL_AMD_ALGO_ORDER_PRESERVED;
+    }
+    // Small AllReduces take the one-sided kernel (HCCL_AMD_SMALL_IPC_BYTES, default 1 MiB per rank): one launch with
+    // one or two cross-rank barriers instead of the transport groups of a schedule, each of which costs a group launch
+    // (1 KiB one-shot over RCCL: 29-32 us, an 8-rank RHD: 81.5 us; profiles/r03_host_cost_rccl_selfloop.jsonl,
+    // r02_rccl_selfloop_latency.jsonl). The reference runs small data on its vector cores the same way
+    // (all_reduce_auto_selector.cc:591-683; a task costs it 1-2 us, cost_model.cc:240-245). The bits do not change: the
+    // auto family runs in the auto family's order (HCCL_AMD_ALGO_IPC), RHD in RHD's (HCCL_AMD_ALGO_IPC_RHD). Every rank
+    // decides alike (count, dtype and the (=) config are equal on every rank); a call the kernel cannot take (no peer
+    // mappings, a capture before the set-up) runs the schedule.
+    if (opType == HCCL_AMD_OP_ALLREDUCE && c.transport->HasSendRecv() && !c.ipc.unavailable &&
+        count * es <= c.cfg.smallIpcBytes && (p.algo == HCCL_AMD_ALGO_AUTO || p.algo == HCCL_AMD_ALGO_RHD)) {
+        IpcPlan plan{};
+        HcclResult r = HCCL_E_NOT_SUPPORT;
+        int32_t ran = HCCL_AMD_ALGO_IPC;
+        if (p.algo == HCCL_AMD_ALGO_RHD) {
+            ran = HCCL_AMD_ALGO_IPC_RHD;
+            if (IpcPlanRhd(c.nRanks, &plan) == HCCL_SUCCESS) {
+                r = RunIpcPlan(c, opType, plan, sendBuf, recvBuf, count, dt, op, root, stream);
+            }
+        } else {
+            const int32_t family = SelectAlgo(opType, c.nRanks, count * es, IsSpecialForSelector(dt, op));
+            r = RunIpcCollective(c, opType, family, sendBuf, recvBuf, count, dt, op, root, stream);
+        }
+        if (r != HCCL_E_NOT_SUPPORT) {
+            c.lastAlgo = ran;
+            return r;
+        }
     }
     if (p.algo == HCCL_AMD_ALGO_IPC_TWOSHOT || p.algo == HCCL_AMD_ALGO_IPC) {
         // the order family of the one-sided kernel: IPC_TWOSHOT fixes AllReduce two-shot (O2), mesh ReduceScatter
@@ -162,7 +213,7 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     p.special = IsSpecialForSelector(dt, op);
     void* bufs[3] = {sendBuf, recvBuf, c.scratch};
     const uint64_t payload = count * es * (opType == HCCL_AMD_OP_REDUCE_SCATTER ? c.nRanks : 1);
-    const bool single = payload <= SingleStreamBytes();
+    const bool single = payload <= c.cfg.singleStreamBytes;
     p.pieceBytes = PieceBytesFor(c, single, payload);
     const CompiledSchedule* cs = nullptr;
     HCCL_CHK(CompileCollective(c, p, bufs, !single, &cs));
@@ -175,8 +226,8 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     c.lastAlgo = s.algo;
     HCCL_AMD_LOG("rank %u op %d algo %d count %llu ops %zu", c.rank, opType, s.algo, (unsigned long long)count,
                  s.ops.size());
-    if (single) return Execute(c, s.ops, bufs, dt, op, stream, true);
-    return RunCompiled(c, *cs, bufs, dt, op, stream);
+    // single-stream programs replay from the executor graph cache too (RCCL path, the key's second call on)
+    return RunCompiled(c, *cs, bufs, dt, op, stream, single);
 }
 
 // ReduceScatterV (reduce_scatter_v_op.cc:24-83, ReduceScatterVOutPlaceCommon :285-330): the mesh template's order
@@ -224,15 +275,14 @@ HcclResult RunReduceScatterV(Comm& c, void* sendBuf, const uint64_t* counts, con
     void* bufs[3] = {sendBuf, recvBuf, c.scratch};
     uint64_t payload = 0;
     for (uint32_t q = 0; q < c.nRanks; ++q) payload += counts[q] * es;
-    const bool single = c.nRanks == 1 || payload <= SingleStreamBytes();
+    const bool single = c.nRanks == 1 || payload <= c.cfg.singleStreamBytes;
     p.pieceBytes = PieceBytesFor(c, single, payload);
     const CompiledSchedule* cs = nullptr;
     HCCL_CHK(CompileCollective(c, p, bufs, !single, &cs));
     const Schedule& s = cs->sched;
     if (s.scratchElems * es > c.scratchBytes) return HCCL_E_INTERNAL;
     c.lastAlgo = s.algo;
-    if (single) return Execute(c, s.ops, bufs, dt, op, stream, true);
-    return RunCompiled(c, *cs, bufs, dt, op, stream);
+    return RunCompiled(c, *cs, bufs, dt, op, stream, single);
 }
 
 }  // namespace
@@ -477,6 +527,22 @@ int32_t HcclAmdCommLastAlgo(HcclComm comm)
     return c == nullptr ? -1 : c->lastAlgo;
 }
 
+HcclResult HcclAmdCommSetConfig(HcclComm comm, int32_t key, int64_t value)
+{
+    Comm* c = AsComm(comm);
+    if (c == nullptr) return HCCL_E_PTR;
+    std::lock_guard<std::mutex> lk(c->mu);
+    return SetConfigEntry(c->cfg, key, value);
+}
+
+HcclResult HcclAmdCommGetConfig(HcclComm comm, int32_t key, int64_t* value)
+{
+    Comm* c = AsComm(comm);
+    if (c == nullptr || value == nullptr) return HCCL_E_PTR;
+    std::lock_guard<std::mutex> lk(c->mu);
+    return GetConfigEntry(c->cfg, key, value);
+}
+
 HcclResult HcclAmdCommScratch(HcclComm comm, void** ptr, uint64_t* bytes)
 {
     Comm* c = AsComm(comm);
@@ -613,7 +679,7 @@ int32_t HcclAmdSelectAivAlgo(int32_t opType, uint32_t nRanks, uint64_t count, Hc
                              uint32_t coreLimit, int32_t flags, uint32_t* groupSize)
 {
     return SelectAivPlan(opType, nRanks, count, dataType, op, (flags & 1) != 0, (flags & 2) != 0, CclBytesDefault(),
-                         coreLimit != 0 ? coreLimit : AivCoreLimit(), nullptr, groupSize);
+                         coreLimit != 0 ? coreLimit : ReadCommConfig().aivCoreLimit, nullptr, groupSize);
 }
 
 HcclResult HcclAmdBuildScheduleV(uint32_t nRanks, uint32_t rank, const uint64_t* sendCounts,

@@ -911,11 +911,16 @@ hipError_t RunCopy(unsigned char* dst, const unsigned char* src, uint64_t bytes,
 
 }  // namespace
 
-bool DeviceCopyByKernel()
-{
-    const char* e = std::getenv("HCCL_AMD_DEVICE_COPY");  // read per call: tests switch it
+// HCCL_AMD_DEVICE_COPY=memcpy (read once, at library load) or HcclAmdSetDeviceCopyKernel(0): hipMemcpyAsync instead of
+// the copy kernel (diagnostics of the r03 stale-operand failure).
+std::atomic<bool> g_copyByKernel{[] {
+    const char* e = std::getenv("HCCL_AMD_DEVICE_COPY");
     return e == nullptr || std::strcmp(e, "memcpy") != 0;
-}
+}()};
+
+bool DeviceCopyByKernel() { return g_copyByKernel.load(std::memory_order_relaxed); }
+
+void SetDeviceCopyByKernel(bool on) { g_copyByKernel.store(on, std::memory_order_relaxed); }
 
 HcclResult LaunchCopyBytes(void* dst, const void* src, uint64_t bytes, hipStream_t stream)
 {

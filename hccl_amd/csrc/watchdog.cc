@@ -345,10 +345,15 @@ bool DeferDestroy(Comm* c)
     // depend on are deferred. (A graph replayed after its communicator's destroy is the caller's error.)
     TeardownTrace(c->rank, "IPC quiesce (destroy time)", true);
     IpcQuiesce(*c);
-    if (c->transport != nullptr) c->transport->SetLocalTeardown();
+    if (c->transport != nullptr) c->transport->SetLocalTeardown(true);
     Reaper& r = TheReaper();
     std::lock_guard<std::mutex> lk(r.mu);
-    if (c->graphRefs.load(std::memory_order_acquire) == 0) return false;  // the last graph went meanwhile
+    if (c->graphRefs.load(std::memory_order_acquire) == 0) {
+        // the last graph went meanwhile: the teardown runs now, on the caller's thread, and may still flush this
+        // rank's outstanding work with its peers (bounded finalize), so the local-only flag is withdrawn
+        if (c->transport != nullptr) c->transport->SetLocalTeardown(false);
+        return false;
+    }
     TeardownTrace(c->rank, "destroy deferred (graphs)", true);
     r.pending.push_back(c);
     if (!r.started) {

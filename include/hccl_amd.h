@@ -203,8 +203,44 @@ extern HcclResult HcclAmdCommSetIpcBlocks(HcclComm comm, uint32_t blocks);
 /* Pipelining granule (bytes per piece) for subsequent collectives on comm; 0 restores the default. */
 extern HcclResult HcclAmdCommSetPieceBytes(HcclComm comm, uint64_t pieceBytes);
 
-/* Algorithm the last collective on comm executed (HcclAmdAlgo), or -1. */
+/* Algorithm the last collective on comm executed (HcclAmdAlgo), or -1. An AllReduce that the small-call rule
+ * (HCCL_AMD_CFG_SMALL_IPC_BYTES) put on the one-sided kernel reports HCCL_AMD_ALGO_IPC (the auto family's order) or
+ * HCCL_AMD_ALGO_IPC_RHD (RHD's order). */
 extern int32_t HcclAmdCommLastAlgo(HcclComm comm);
+
+/* Configuration. A communicator reads the environment once, when it is created (the reference parses its environment
+ * once, InitEnvConfig, src/common/alg_env_config.cc:176); no collective reads it. HcclAmdCommSetConfig changes one
+ * entry of comm afterwards: keys marked (=) must be equal on every rank of the communicator, as the environment
+ * variables they stand for must be. HCCL_E_PARA for an unknown key or a value out of range. */
+typedef enum {
+    HCCL_AMD_CFG_DETERMINISTIC_STRICT = 0, /* (=) HCCL_DETERMINISTIC=strict: 1, else 0 */
+    HCCL_AMD_CFG_EXPANSION_MODE_AIV = 1,   /* (=) HCCL_OP_EXPANSION_MODE=AIV: 1, else 0 */
+    HCCL_AMD_CFG_AIV_CORE_LIMIT = 2,       /* (=) HCCL_AMD_AIV_CORE_LIMIT, 1..4096 (default 48) */
+    HCCL_AMD_CFG_SINGLE_STREAM_BYTES = 3,  /* HCCL_AMD_SINGLE_STREAM_BYTES: programs up to this per-rank payload run
+                                              on the caller's stream alone (default 1 MiB) */
+    HCCL_AMD_CFG_SMALL_IPC_BYTES = 4,      /* (=) HCCL_AMD_SMALL_IPC_BYTES: an AllReduce of auto or RHD family up to this
+                                              many bytes per rank runs on the one-sided kernel, same bits (default
+                                              1 MiB; 0 = never) */
+    HCCL_AMD_CFG_PLAN_CACHE = 5,           /* HCCL_AMD_PLAN_CACHE: compiled-collective cache on (1, default) / off (0) */
+    HCCL_AMD_CFG_GRAPH_CACHE = 6,          /* HCCL_AMD_GRAPH_CACHE: executor graphs kept, 0..1024 (default 16) */
+    HCCL_AMD_CFG_IPC_LIGHT_FENCE = 7,      /* (=) HCCL_AMD_IPC_LIGHT_FENCE: -1 per mode (default), 0 system, 1 light */
+    HCCL_AMD_CFG_IPC_NT = 8,               /* (=) HCCL_AMD_IPC_NT: non-temporal loads and stores (default 1) */
+    HCCL_AMD_CFG_IPC_THREADS = 9,          /* (=) HCCL_AMD_IPC_THREADS: 256 (default) or 512 */
+    HCCL_AMD_CFG_IPC_TILE_KIB = 10,        /* (=) HCCL_AMD_IPC_TILE_KIB: 0 = one window per block (default) */
+    HCCL_AMD_CFG_IPC_TIMEOUT_MS = 11,      /* HCCL_AMD_IPC_TIMEOUT_MS, else HCCL_EXEC_TIMEOUT's AIV rule (HcclAmdIpcTimeoutMs) */
+    HCCL_AMD_CFG_IPC_STAGING_MIB = 12,     /* (=) HCCL_AMD_IPC_STAGING_MIB, 16..1000 (default 512); at the IPC set-up */
+    HCCL_AMD_CFG_IPC_STAGING_CACHED = 13,  /* (=) HCCL_AMD_IPC_STAGING_CACHED (diagnostics); at the IPC set-up */
+    HCCL_AMD_CFG_IPC_TRACE = 14,           /* HCCL_AMD_IPC_TRACE: phase stamps (diagnostics); at the IPC set-up */
+    HCCL_AMD_CFG_IPC_L2_SCRUB = 15,        /* HCCL_AMD_IPC_L2_SCRUB: L2 maintenance at the IPC set-up (default 1) */
+    HCCL_AMD_CFG_COUNT = 16
+} HcclAmdConfigKey;
+extern HcclResult HcclAmdCommSetConfig(HcclComm comm, int32_t key, int64_t value);
+extern HcclResult HcclAmdCommGetConfig(HcclComm comm, int32_t key, int64_t* value);
+
+/* Process-wide: the device-to-device copies the library makes (loopback links, COPY records, one-operand folds, a
+ * one-rank collective) run as its copy kernel (on != 0, the default) or as hipMemcpyAsync (0; diagnostics).
+ * Initialised at library load from HCCL_AMD_DEVICE_COPY (=memcpy: 0). */
+extern HcclResult HcclAmdSetDeviceCopyKernel(int32_t on);
 
 /* Runs one rank's IR program on comm's executor: what every collective runs after it has built its schedule (SEND/RECV
  * groups on the transport, folds and copies on the reduce stream, the cross-stream waits derived from the records'

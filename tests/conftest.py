@@ -29,6 +29,10 @@ _ensure_built()
 # for 128 MiB areas (a chunk wider than one area runs several staging rounds), so the suite keeps that size unless a
 # test sets its own (test_gpu_collectives.py::test_ipc_default_staging covers the default). Child processes inherit it.
 os.environ.setdefault("HCCL_AMD_IPC_STAGING_MIB", "128")
+# AllReduces of up to 1 MiB per rank run on the one-sided kernel by default (HCCL_AMD_SMALL_IPC_BYTES, same bits as the
+# schedule they stand for). The suite checks the schedules themselves at those sizes, so it turns the rule off unless a
+# test sets it (tests/test_gpu_small_ipc.py covers the rule, its bits and its fallbacks).
+os.environ.setdefault("HCCL_AMD_SMALL_IPC_BYTES", "0")
 
 
 def pytest_configure(config):

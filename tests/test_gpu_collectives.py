@@ -176,9 +176,9 @@ def test_ipc_phase_trace(monkeypatch, n, count):
         assert (a > 0).all(), "a block or rank left a stamp unwritten"
         assert (np.diff(a, axis=2) >= 0).all(), "phase stamps out of order"
         assert not st[n:].any() and not st[:n, blocks:].any()
-        # a world without the variable has no trace
-        plain = H.loopback_world(2)
+        # a world created without the variable has no trace
         monkeypatch.delenv("HCCL_AMD_IPC_TRACE")
+        plain = H.loopback_world(2)
         try:
             collective(plain, AR, 7, O.FP32, O.SUM, xs[:2], count)
             with pytest.raises(H.HcclError):

@@ -322,9 +322,42 @@ def test_ipc_lost_peer_fails_the_communicator():
     assert r0["after_s"] < 1.0, r0  # the gate enqueues nothing
 
 
+# Calls of the default-staging test (no HCCL_AMD_IPC_STAGING_MIB: 512 MiB slot and result areas, 511.5 MiB alternate
+# areas): (collective, elements per rank's input, in place). At n = 2 a two-shot owner's slot holds 64 Mi int32 per
+# staging round, so the 600 MiB AllReduces (chunks of 75 Mi elements) cross one round boundary, in place and out of
+# place; the 640 MiB ReduceScatter input (blocks of 80 Mi elements) crosses the alternate areas' boundary.
+DEFAULT_STAGING_CALLS = [
+    (AR, 1025, False),
+    (AR, (300 << 20) // 4 + 3, False),  # the r03 call that once returned a wrong result on rank 0
+    (AR, (600 << 20) // 4 + 5, False),
+    (AR, (600 << 20) // 4 + 5, True),
+    (RS, 2 * ((320 << 20) // 4 + 7), False),
+    (AR, 4097, True),
+]
+
+
+def _mismatch_detail(torch, y, want, xs_fn, prev, count, n, k):
+    """Everything a wrong result can say about its cause: how many elements, where (owner chunk and
+    staging round of the first, owners of all), the values at the first, and what the wrong value equals: the fold
+    with one rank's operand missing, the previous call's result, zero, or none of these."""
+    bad = (y != want).nonzero().flatten()
+    i = int(bad[0])
+    es, align = 4, 32  # int32; chunks rounded up to 128 B (HCCL_MIN_SLICE_ALIGN)
+    chunk = ((count + n - 1) // n + align - 1) // align * align
+    slot = (512 << 20) // es // n // 4 * 4  # elements of one owner's slot per staging round
+    owners = torch.bincount(torch.div(bad, chunk, rounding_mode="floor"), minlength=n).tolist()
+    got_i, want_i = int(y[i]), int(want[i])
+    missing = [q for q in range(n) if got_i == want_i - int(xs_fn(q, i))]
+    return {"call": k, "count": count, "bad": int(bad.numel()), "first": i, "last": int(bad[-1]),
+            "first_owner": i // chunk, "first_round": (i % chunk) // slot, "bad_per_owner": owners,
+            "got": got_i, "want": want_i, "missing_operand_of_rank": missing,
+            "equals_previous_call": prev is not None and i < prev.numel() and got_i == int(prev[i]),
+            "is_zero": got_i == 0}
+
+
 def _default_staging_main(rank, n, port, q):
-    # the default staging (four 512 MiB areas per rank, each its own allocation and handle): in r03 the areas were
-    # one 2 GiB allocation, whose handle hipIpcOpenMemHandle never opened, so the rank-mode set-up hung
+    # the default staging: one allocation of 2047 MiB per rank (a 2 GiB one, r03's first layout, never opened with
+    # hipIpcOpenMemHandle, so the rank-mode set-up hung)
     os.environ.pop("HCCL_AMD_IPC_STAGING_MIB", None)
     os.environ["HCCL_AMD_IPC_TIMEOUT_MS"] = "20000"
     try:
@@ -344,17 +377,31 @@ def _default_staging_main(rank, n, port, q):
         comm.set_algo(H.Algo.IPC_TWOSHOT)
         s = torch.cuda.Stream()
         res = []
-        for count in (1025, (300 << 20) // 4 + 3):  # one staging round, and one 300 MiB call
-            x = torch.arange(count, device="cuda", dtype=torch.int32) % 1000 + rank
-            y = torch.empty_like(x)
+        prev = None
+        for k, (kind, count, inplace) in enumerate(DEFAULT_STAGING_CALLS):
+            # values distinct per call (1000 k), so a result left over from an earlier call is recognisable
+            base = torch.arange(count, device="cuda", dtype=torch.int32) % 1000 + 1000 * k
+            x = base + rank
+            y = x if inplace else torch.full_like(x, -7)
+            out_len = count // n if kind == RS else count
+            if kind == RS:
+                y = torch.full((out_len,), -7, dtype=torch.int32, device="cuda")
             torch.cuda.synchronize()  # x was made on the current stream; the collective runs on s
-            comm.all_reduce(x, y, H.HcclReduceOp.SUM, s)
+            if kind == RS:
+                comm.reduce_scatter(x, y, H.HcclReduceOp.SUM, s)
+                want = base[rank * out_len:(rank + 1) * out_len] * n + n * (n - 1) // 2
+                xs_fn = (lambda qq, i, b0=base, o=rank * out_len: int(b0[o + i]) + qq)
+            else:
+                comm.all_reduce(x, y, H.HcclReduceOp.SUM, s)
+                want = base * n + n * (n - 1) // 2
+                xs_fn = (lambda qq, i, b0=base: int(b0[i]) + qq)
             s.synchronize()
-            want = (torch.arange(count, device="cuda", dtype=torch.int32) % 1000) * n + n * (n - 1) // 2
-            bad = (y != want).nonzero()
-            res.append((H.Algo(comm.last_algo).name, bad.numel() == 0, comm.ipc_status() & 1))
-            if bad.numel():
-                res.append(("mismatches", int(bad.numel()), int(bad[0]), int(bad[-1]), count))
+            ok = bool(torch.equal(y, want))
+            res.append((H.Algo(comm.last_algo).name, ok, comm.ipc_status() & 1))
+            if not ok:
+                res.append(("mismatch", _mismatch_detail(torch, y, want, xs_fn, prev, out_len, n, k)))
+            prev = y.clone() if kind == AR else None
+            del x, y, want, base
         dist.barrier()
         comm.destroy()
         dist.destroy_process_group()
@@ -364,10 +411,12 @@ def _default_staging_main(rank, n, port, q):
         time.sleep(10)
 
 
-@pytest.mark.timeout(200)
+@pytest.mark.timeout(240)
 def test_ipc_rank_mode_default_staging():
-    """Rank mode with the default staging areas (no HCCL_AMD_IPC_STAGING_MIB): the set-up opens every peer's four
-    area handles and the two-shot AllReduce is exact, without a barrier timeout."""
+    """Rank mode with the default staging (no HCCL_AMD_IPC_STAGING_MIB; one allocation below 2 GiB per rank, opened by
+    every peer): two-shot AllReduces and a ReduceScatter exact without a barrier timeout, including calls that cross
+    the default areas' round boundary in place and out of place. A wrong result reports everything it can say about its
+    cause (_mismatch_detail) in the assertion message, in full."""
     n = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -378,13 +427,20 @@ def test_ipc_rank_mode_default_staging():
     try:
         got = {}
         for _ in procs:
-            rank, msg, res = q.get(timeout=150)
+            rank, msg, res = q.get(timeout=200)
             got[rank] = (msg, res)
     finally:
         for p in procs:
             p.join(timeout=60)
             if p.is_alive():
                 p.kill()
+    import json
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/ipc_default_staging.json", "w") as f:
+        json.dump({str(r): got[r] for r in got}, f, indent=1)
     for r in range(n):
         assert got[r][0] == "ok", f"rank {r}:\n{got[r][0]}"
-        assert got[r][1] == [("IPC_TWOSHOT", True, 0)] * 2, got[r][1]
+    # every rank's record in full, whichever rank is wrong (pytest would truncate a list diff)
+    detail = json.dumps({r: got[r][1] for r in range(n)})
+    for r in range(n):
+        assert got[r][1] == [("IPC_TWOSHOT", True, 0)] * len(DEFAULT_STAGING_CALLS), detail

@@ -39,6 +39,22 @@ def test_r03_failing_order_passes_with_kernel_copies(fence):
     assert f"{len(ids)} passed" in r.stdout, r.stdout[-2000:]
 
 
+def test_user_copy_at_the_end_of_the_r03_failing_order():
+    """a caller's own device-to-device copy (torch copy_, a hipMemcpyAsync) into sendBuf on the
+    collective's stream immediately before HcclAllReduce, run at the end of the r03 failing order (the allocation
+    history that reproduced the link-copy failure, 64 MiB staging). The library's copies are its kernel; the caller's
+    is not, and the fold reads what it wrote."""
+    ids = open(os.path.join(ROOT, "tests", "r03_failing_selection.txt")).read().split()
+    ids.append("tests/test_gpu_user_copy.py::test_user_copy_then_allreduce")
+    env = dict(os.environ, HCCL_AMD_IPC_STAGING_MIB="64")
+    env.pop("HCCL_AMD_DEVICE_COPY", None)
+    r = subprocess.run([sys.executable, "-u", "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", "--timeout", "120",
+                        "--timeout-method", "thread", *ids], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=400)
+    assert r.returncode == 0, r.stdout[-6000:] + r.stderr[-2000:]
+    assert f"{len(ids) - 1 + 4} passed" in r.stdout, r.stdout[-2000:]
+
+
 @pytest.mark.parametrize("nbytes", [1, 15, 16, 17, 4099, (1 << 20) + 5, (64 << 20) + 3])
 @pytest.mark.parametrize("shift", [(0, 0), (3, 3), (1, 6), (0, 8), (2, 6), (0, 2), (5, 9)])
 def test_device_copy_kernel_bytes(nbytes, shift):
@@ -60,12 +76,16 @@ def test_device_copy_kernel_bytes(nbytes, shift):
     assert (host[:do] == 0xA5).all() and (host[do + nbytes:] == 0xA5).all()
 
 
-def test_device_copy_env_selects_memcpy(monkeypatch):
-    """HCCL_AMD_DEVICE_COPY=memcpy (diagnostics) still copies, through hipMemcpyAsync."""
-    monkeypatch.setenv("HCCL_AMD_DEVICE_COPY", "memcpy")
-    x = torch.arange(1000, dtype=torch.float32, device="cuda")
-    y = torch.zeros_like(x)
-    H.local_reduce_n(y, [x])
-    torch.cuda.synchronize()
-    assert torch.equal(x, y)
-    assert np.array_equal(y.cpu().numpy(), np.arange(1000, dtype=np.float32))
+def test_device_copy_memcpy_mode():
+    """HcclAmdSetDeviceCopyKernel(0) (HCCL_AMD_DEVICE_COPY=memcpy at load; diagnostics) still copies, through
+    hipMemcpyAsync."""
+    H.set_device_copy_kernel(False)
+    try:
+        x = torch.arange(1000, dtype=torch.float32, device="cuda")
+        y = torch.zeros_like(x)
+        H.local_reduce_n(y, [x])
+        torch.cuda.synchronize()
+        assert torch.equal(x, y)
+        assert np.array_equal(y.cpu().numpy(), np.arange(1000, dtype=np.float32))
+    finally:
+        H.set_device_copy_kernel(True)

@@ -465,7 +465,7 @@ def _graph_eviction_worker(q):
     try:
         import sys
         sys.path.insert(0, ROOT)
-        os.environ["HCCL_AMD_GRAPH_CACHE"] = "2"  # read per call
+        os.environ["HCCL_AMD_GRAPH_CACHE"] = "2"  # read when the communicator is created
         import torch
         import hccl_amd as H
         from oracle import oracle as O
@@ -490,10 +490,13 @@ def _graph_eviction_worker(q):
         with torch.cuda.stream(s):
             for rnd in range(4):
                 for k, (arr, nops, scratch), in_len, out_len, xd, od in progs:
-                    x = O.random_operands(dtype, in_len, seed=9000 + 100 * k + rnd, edge=False)
-                    xd.copy_(to_device(dtype, x))
-                    comm.execute(arr, nops, xd, od, op, False, s, dtype=dtype)
-                    issued.append((k, rnd, arr, nops, scratch, x, out_len, od.clone()))
+                    # twice in a row: a key's first call runs eagerly, its second captures and replays; the next
+                    # program's first call then evicts an executable whose replay may still run
+                    for rep in range(2):
+                        x = O.random_operands(dtype, in_len, seed=9000 + 100 * k + 10 * rnd + rep, edge=False)
+                        xd.copy_(to_device(dtype, x))
+                        comm.execute(arr, nops, xd, od, op, False, s, dtype=dtype)
+                        issued.append((k, rnd, arr, nops, scratch, x, out_len, od.clone()))
         torch.cuda.synchronize()
         captures = comm.graph_stats()[1] - captures0
         results = []
@@ -522,7 +525,7 @@ def test_executor_graph_cache_eviction_while_in_flight():
             p.kill()
     assert status == "ok", res
     assert not [r for r in res["results"] if r[-1] != "ok"], res
-    assert len(res["results"]) == 4 * res["programs"], res
+    assert len(res["results"]) == 8 * res["programs"], res
     assert res["captures"] > 2, res
 
 
@@ -534,11 +537,13 @@ def _p2p_channels_worker(per_peer, log_dir, q):
         import sys
         import time
         sys.path.insert(0, ROOT)
-        # the parent's library load already set these in its C environment, which a spawned child inherits
+        # the child decides for itself (a parent that opted in would have set these in the environment it inherits)
         os.environ.pop("NCCL_NCHANNELS_PER_PEER", None)
         os.environ.pop("NCCL_MIN_P2P_NCHANNELS", None)
         if per_peer is not None:
             os.environ["HCCL_AMD_P2P_CHANNELS_PER_PEER"] = str(per_peer)
+        else:
+            os.environ.pop("HCCL_AMD_P2P_CHANNELS_PER_PEER", None)
         os.environ["NCCL_DEBUG"] = "INFO"
         os.environ["NCCL_DEBUG_SUBSYS"] = "INIT"  # bench.py's setting
         os.environ["NCCL_DEBUG_FILE"] = os.path.join(log_dir, f"rccl_init_{per_peer}.%p.log")
@@ -577,12 +582,12 @@ def _p2p_channels_worker(per_peer, log_dir, q):
 
 
 def test_rccl_p2p_channels_configured(tmp_path):
-    """the library sets RCCL's per-peer p2p channels when it is loaded, before any RCCL
-    communicator (default 16 per peer, NCCL_MIN_P2P_NCHANNELS = per peer x 7 rounded up, at most 64), and RCCL
-    honours them: its INIT log reports the per-peer count (twice the setting), and the self-loop message rate scales
-    with it (about 43 GB/s per channel, r02). HCCL_AMD_P2P_CHANNELS_PER_PEER=0 leaves both to RCCL."""
+    """HCCL_AMD_P2P_CHANNELS_PER_PEER=k (opt-in since r05) makes the library set RCCL's per-peer p2p
+    channels when it is loaded, before any RCCL communicator (NCCL_MIN_P2P_NCHANNELS = the per-peer value x 7 rounded
+    up, at most 64), and RCCL honours them: its INIT log reports the per-peer count (twice the setting), and the
+    self-loop message rate scales with it (about 43 GB/s per channel, r02). Unset, both are RCCL's."""
     rows = []
-    for per_peer in (None, 4, 0):
+    for per_peer in (16, 4, None):
         ctx = mp.get_context("spawn")
         q = ctx.Queue()
         p = ctx.Process(target=_p2p_channels_worker, args=(per_peer, str(tmp_path), q))
@@ -599,13 +604,13 @@ def test_rccl_p2p_channels_configured(tmp_path):
     with open(os.path.join(ROOT, "gpurun_out", "rccl_p2p_channels_configured.jsonl"), "w") as f:
         for row in rows:
             f.write(__import__("json").dumps(row) + "\n")
-    default, four, rccl_own = rows
+    default, four, rccl_own = rows  # opted in at 16 (bench.py's setting), at 4, and not at all
     assert default["exact"] and four["exact"] and rccl_own["exact"]
     assert tuple(default["configured"]) == (16, 64) and tuple(four["configured"]) == (4, 32), rows
     # RCCL's own summary ("%d p2p channels, %d p2p channels per peer") reports twice the per-peer setting
     assert default["rccl_reported"] is not None and four["rccl_reported"] is not None, rows
     assert default["rccl_reported"][1] == 4 * four["rccl_reported"][1], rows
     assert default["self_loop_GBps"] > 2 * four["self_loop_GBps"], rows
-    # 0 leaves both to RCCL (reported as 0); what RCCL then picks is recorded only
+    # unset leaves both to RCCL (reported as 0); what RCCL then picks is recorded only
     assert tuple(rccl_own["configured"]) == (0, 0), rows
     assert rccl_own["rccl_reported"] is not None, rows

@@ -1,0 +1,134 @@
+"""Small AllReduces on the one-sided kernel (HCCL_AMD_SMALL_IPC_BYTES, default 1 MiB per rank; ops.cc RunCollective;
+VERDICT r04 next #2).
+
+An AllReduce of the auto family or RHD up to the threshold runs as one launch of the one-sided kernel in the same
+order family: the auto family's order (one-shot O1 at these sizes, ins_temp_all_reduce_mesh_1D_one_shot.cc:211-226)
+or RHD's (the HCCL_AMD_ALGO_IPC_RHD closed form), so the bits are the schedule's. The suite's other
+files run with the rule off (conftest) so that they keep checking the schedules themselves at these sizes; here it is
+on, as it is by default outside the suite.
+"""
+import numpy as np
+import pytest
+import torch
+
+import hccl_amd as H
+from oracle import oracle as O
+from tests import sched_ref as R
+from tests.test_gpu_collectives import AR, collective, ipc_status, oracle_replay
+
+pytestmark = pytest.mark.gpu
+
+DEFAULT = 1 << 20
+
+
+def world(n, small=DEFAULT):
+    comms = H.loopback_world(n)
+    for c in comms:
+        c.set_config(H.Config.SMALL_IPC_BYTES, small)
+    return comms
+
+
+def destroy(comms):
+    torch.cuda.synchronize()
+    for c in comms:
+        c.destroy()
+
+
+@pytest.mark.parametrize("dtype,op,count", [
+    (O.FP16, O.SUM, 512),            # C5's smallest point, 1 KiB
+    (O.FP16, O.SUM, (1 << 19)),      # C5 at 1 MiB, the threshold itself
+    (O.FP32, O.SUM, 4099),
+    (O.BFP16, O.MAX, 65537),
+    (O.INT32, O.PROD, 9999),
+    (O.FP64, O.SUM, 3001),           # 64-bit: the selector's special case (still one-shot at this size)
+    (O.INT8, O.MIN, 1),
+], ids=lambda v: str(v))
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
+def test_small_auto_allreduce_runs_one_sided_with_the_schedule_bits(n, dtype, op, count):
+    comms = world(n)
+    try:
+        xs = [O.random_operands(dtype, count, seed=4400 + 7 * n + r) for r in range(n)]
+        used, outs = collective(comms, AR, H.Algo.AUTO, dtype, op, xs, count)
+        assert used == H.Algo.IPC, H.Algo(used).name
+        assert ipc_status(comms[0]) & 1 == 0
+        want = oracle_replay(AR, H.Algo.AUTO, n, count, dtype, op, xs, 0, 0)  # the auto schedule's IR, replayed
+        for r in range(n):
+            assert O.equal_bits(dtype, outs[r], want[r]), r
+    finally:
+        destroy(comms)
+
+
+@pytest.mark.parametrize("count", [512, 4096 + 3, (1 << 19)])
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_small_rhd_allreduce_runs_ipc_rhd_with_rhd_bits(n, count):
+    """C5's algorithm at its latency end: RHD's bits from one launch (random fp16, where the order decides them)."""
+    comms = world(n)
+    try:
+        xs = [O.random_operands(O.FP16, count, seed=4500 + 7 * n + r, edge=False) for r in range(n)]
+        used, outs = collective(comms, AR, H.Algo.RHD, O.FP16, O.SUM, xs, count)
+        assert used == H.Algo.IPC_RHD, H.Algo(used).name
+        want = oracle_replay(AR, H.Algo.RHD, n, count, O.FP16, O.SUM, xs, 0, 0)
+        rank_order = R.allreduce_o2(O.FP16, O.SUM, xs)[0]
+        for r in range(n):
+            assert O.equal_bits(O.FP16, outs[r], want[r]), r
+        if n > 2 and count > 512:  # the check has teeth: the plain rank-order fold differs somewhere
+            assert not O.equal_bits(O.FP16, want[0], rank_order)
+    finally:
+        destroy(comms)
+
+
+def test_threshold_and_switch():
+    """Above the threshold, with the rule off, and for other operations the schedules run as before."""
+    n = 4
+    comms = world(n, small=64 << 10)
+    try:
+        xs = [O.random_operands(O.FP32, 20000, seed=4600 + r) for r in range(n)]  # 80 KB > 64 KiB
+        used, outs = collective(comms, AR, H.Algo.AUTO, O.FP32, O.SUM, xs, 20000)
+        assert used == R.ALGO_ONESHOT, H.Algo(used).name
+        used, _ = collective(comms, AR, H.Algo.AUTO, O.FP32, O.SUM, [x[:1000] for x in xs], 1000)
+        assert used == H.Algo.IPC
+        # ReduceScatter is not covered by the rule
+        used, _ = collective(comms, 1, H.Algo.AUTO, O.FP32, O.SUM, [x[:4000] for x in xs], 1000)
+        assert used == R.ALGO_ONESHOT, H.Algo(used).name
+        # an explicit family is never rerouted
+        used, _ = collective(comms, AR, H.Algo.MESH_TWOSHOT, O.FP32, O.SUM, [x[:1000] for x in xs], 1000)
+        assert used == R.ALGO_TWOSHOT
+        for c in comms:
+            c.set_config(H.Config.SMALL_IPC_BYTES, 0)
+            assert c.get_config(H.Config.SMALL_IPC_BYTES) == 0
+        used, _ = collective(comms, AR, H.Algo.AUTO, O.FP32, O.SUM, [x[:1000] for x in xs], 1000)
+        assert used == R.ALGO_ONESHOT
+    finally:
+        destroy(comms)
+
+
+def test_in_place_small_allreduce():
+    n, count = 4, 3333
+    comms = world(n)
+    try:
+        xs = [O.random_operands(O.FP32, count, seed=4700 + r) for r in range(n)]
+        used, outs = collective(comms, AR, H.Algo.AUTO, O.FP32, O.SUM, xs, count, inplace=True)
+        assert used == H.Algo.IPC
+        want = R.allreduce_o1(O.FP32, O.SUM, xs)
+        for r in range(n):
+            assert O.equal_bits(O.FP32, outs[r], want[r]), r
+    finally:
+        destroy(comms)
+
+
+def test_config_round_trip_and_ranges():
+    comms = H.loopback_world(2)
+    try:
+        c = comms[0]
+        assert c.get_config(H.Config.SMALL_IPC_BYTES) == 0  # the suite's environment (conftest)
+        assert c.get_config(H.Config.GRAPH_CACHE) == 16
+        assert c.get_config(H.Config.IPC_THREADS) == 256
+        c.set_config(H.Config.IPC_THREADS, 512)
+        assert c.get_config(H.Config.IPC_THREADS) == 512
+        for key, bad in ((H.Config.IPC_THREADS, 300), (H.Config.IPC_LIGHT_FENCE, 2), (H.Config.IPC_STAGING_MIB, 8),
+                         (H.Config.AIV_CORE_LIMIT, 0), (99, 1)):
+            with pytest.raises(H.HcclError) as e:
+                c.set_config(key, bad)
+            assert e.value.code == H.HcclResult.HCCL_E_PARA
+    finally:
+        destroy(comms)
