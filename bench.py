@@ -32,6 +32,13 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+# RCCL's per-peer p2p channels for the N > 1 run: the library sets them only when asked (HCCL_AMD_P2P_CHANNELS_PER_PEER,
+# read when it is loaded, i.e. now; comm.cc ConfigureRcclP2pChannels). The bench asks for 16 per peer, the setting r04
+# chose on the one-GPU proxy (4 made the self-loop RCCL programs 1.7-2.9x slower, profiles/r04_span_channels.jsonl);
+# they apply to torch.distributed's RCCL communicators of this process too. transport.p2p_channels reports what RCCL's
+# INIT log says it set up. A caller's own setting wins.
+os.environ.setdefault("HCCL_AMD_P2P_CHANNELS_PER_PEER", "16")
+
 import hccl_amd as H  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters"
@@ -233,15 +240,39 @@ def end_to_end_host(steps: int = 5, chunk: int = 64 << 20) -> dict:
             "note": "pinned host buffers; 2 GiB H2D + reduce + 1 GiB D2H per step (PCIe-bound)"}
 
 
-def load_pmc_traffic(name: str):
-    """Per-launch HBM bytes from the committed rocprofv3 PMC summary (profiles/), if one exists for this kernel."""
-    path = os.path.join(ROOT, "profiles", name)
+def pmc_traffic(name: str):
+    """(HBM bytes per launch, provenance) from the newest committed rocprofv3 PMC summary of this kernel
+    (profiles/<round>_pmc_<name>.json, tools/profile_round.sh). The counters are never measured inside this run (a
+    counter pass is a run of its own under rocprofv3, MI355X_MICROARCH.md), so the line says where they came from and
+    whether they were taken on the library it has loaded (VERDICT r04 next #5)."""
+    import glob
+    import hashlib
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{name}.json")),
+                   key=lambda p: os.path.basename(p).split("_pmc_")[0])
+    if not files:
+        return None, {"file": None, "measured_in_run": False}
+    path = files[-1]
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        return None
+    except (OSError, ValueError) as e:
+        return None, {"file": os.path.relpath(path, ROOT), "error": str(e), "measured_in_run": False}
+    try:
+        with open(H.LIB_PATH, "rb") as f:
+            loaded = hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        loaded = None
+    profiled = d.get("library_sha256")
+    return d.get("hbm_bytes_per_launch"), {
+        "file": os.path.relpath(path, ROOT),
+        "source_commit": d.get("source_commit"),
+        "library_sha256": profiled,
+        # False: the counters were taken on another build of the library than the one this line measured
+        "library_matches": (profiled == loaded) if profiled and loaded else None,
+        "traffic_over_algorithmic": d.get("traffic_over_algorithmic"),
+        "measured_in_run": False,
+    }
 
 
 def fold_roofline(dev, stream, n: int = 8, reps: int = 10) -> dict:
@@ -268,11 +299,12 @@ def fold_roofline(dev, stream, n: int = 8, reps: int = 10) -> dict:
     nbytes = (n + 1) * count * 4
     kavg = float(np.mean(per))
     del ins, out, acc
+    traffic, source = pmc_traffic("fold_n8")
     return {"kernel": "k_reduceN<EFp<float>, SUM> (8 inputs)", "algorithmic_bytes_per_launch": nbytes,
             "kernel_avg_us": round(kavg * 1e6, 1), "kernel_median_us": round(float(np.median(per)) * 1e6, 1),
             "achieved_GBps": round(nbytes / kavg / 1e9, 1), "peak_GBps": HBM_PEAK_GBPS,
             "frac": round(nbytes / kavg / 1e9 / HBM_PEAK_GBPS, 4),
-            "traffic": load_pmc_traffic("r04f_pmc_fold_n8.json") or load_pmc_traffic("r04_pmc_fold_n8.json") or load_pmc_traffic("r03d_pmc_fold_n8.json"),
+            "traffic": traffic, "traffic_source": source,
             "result_ok": ok}
 
 
@@ -334,6 +366,7 @@ def ipc_two_shot_roofline(dev, n: int = 2, mib: int = 512, reps: int = 10) -> di
             c.destroy()
     nbytes = n * 2 * (3 * n - 2) * count * 4 // n
     kavg = float(np.mean(per))
+    traffic, source = pmc_traffic("ipc_two_shot")
     return {"kernel": "k_ipc_collective<EFp<float>, SUM> (two-shot AllReduce, loopback world)", "ranks": n,
             "bytes_per_rank": count * 4, "ran": ran, "algorithmic_bytes_per_launch": nbytes,
             "kernel_avg_us": round(kavg * 1e6, 1), "kernel_median_us": round(float(np.median(per)) * 1e6, 1),
@@ -342,7 +375,7 @@ def ipc_two_shot_roofline(dev, n: int = 2, mib: int = 512, reps: int = 10) -> di
             "call_to_call_avg_us": round(float(np.mean(per_call)) * 1e6, 1),
             "achieved_GBps": round(nbytes / kavg / 1e9, 1), "peak_GBps": HBM_PEAK_GBPS,
             "frac": round(nbytes / kavg / 1e9 / HBM_PEAK_GBPS, 4),
-            "traffic": load_pmc_traffic("r04f_pmc_ipc_two_shot.json") or load_pmc_traffic("r04_pmc_ipc_two_shot.json") or load_pmc_traffic("r03d_pmc_ipc_two_shot.json"),
+            "traffic": traffic, "traffic_source": source,
             "barrier_timeouts": timeouts,
             "result_ok": ok}
 
@@ -378,6 +411,7 @@ def bench_local(args) -> dict:
     value = bytes_step * args.steps / total / GIB
     kavg = float(np.mean(per))
     achieved = bytes_step / kavg / 1e9
+    traffic, traffic_source = pmc_traffic("local_reduce")
     log(f"[bench] C2 local reduce: {value:.1f} GiB/s  kernel avg {kavg*1e6:.1f} us  min {min(per)*1e6:.1f} us  "
         f"max {max(per)*1e6:.1f} us  host wall {wall:.3f} s")
     res = {
@@ -406,7 +440,8 @@ def bench_local(args) -> dict:
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": load_pmc_traffic("r04f_pmc_local_reduce.json") or load_pmc_traffic("r04_pmc_local_reduce.json") or load_pmc_traffic("r03d_pmc_local_reduce.json"),
+            "traffic": traffic,
+            "traffic_source": traffic_source,
             "kernel": "k_reduce2<EFp<float>, SUM>",
             "algorithmic_bytes_per_launch": bytes_step,
             "kernel_avg_us": round(kavg * 1e6, 2),
@@ -646,11 +681,15 @@ def bench_c4(comm, send, recv, world) -> dict:
 
 
 def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
-    """C5: AllReduce fp16 SUM, 1 KiB .. 4 GiB: latency at small sizes, busbw at large. Each size runs the RHD schedule
-    (the config's algorithm), the auto selection (what the reference would run: one-shot / two-shot / MeshChunk),
-    up to 256 MiB the one-sided IPC kernel in the same order family (one launch per call: the latency end), and up to
-    64 MiB IPC_RHD (the RHD schedule's bits from one one-sided launch, compared with them). The RCCL rows of every size
-    run before the IPC rows: an IPC barrier timeout fails the communicator."""
+    """C5: AllReduce fp16 SUM, 1 KiB .. 4 GiB: latency at small sizes, busbw at large. Rows per size (`<row>_ran` names
+    the path that ran, `<row>_us` and `<row>_busbw_GBps` its time):
+      rhd / auto        the RHD schedule (the config's algorithm) and the auto selection (what the reference would
+                        run), every size, over the transport with the small-call rule off (Config.SMALL_IPC_BYTES 0);
+      rhd_default / auto_default   the same calls as a caller gets them by default up to the rule's threshold
+                        (1 MiB): one launch of the one-sided kernel in the same order (IPC_RHD / IPC), compared bit for
+                        bit with the rhd / auto rows, and from a HIP graph (`*_graph_us`);
+      ipc / ipc_rhd     the one-sided kernel forced, up to 256 / 64 MiB.
+    The transport rows of every size run before the one-sided ones: an IPC barrier timeout fails the communicator."""
     s = torch.cuda.current_stream()
     sizes = []
     nbytes = 1 << 10
@@ -659,15 +698,19 @@ def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
         nbytes *= 2
     rows = {b: {"bytes": b} for b in sizes}
     f = 2 * (world - 1) / world
-    key = {H.Algo.RHD: "rhd", H.Algo.AUTO: "auto", H.Algo.IPC: "ipc", H.Algo.IPC_RHD: "ipc_rhd"}
-    rhd_digest = {}
+    small = comm.get_config(H.Config.SMALL_IPC_BYTES)  # the default threshold (HCCL_AMD_SMALL_IPC_BYTES)
+    plan = (("rhd", H.Algo.RHD, 0, max_bytes), ("auto", H.Algo.AUTO, 0, max_bytes),
+            ("rhd_default", H.Algo.RHD, small, small), ("auto_default", H.Algo.AUTO, small, small),
+            ("ipc", H.Algo.IPC, 0, 256 << 20), ("ipc_rhd", H.Algo.IPC_RHD, 0, 64 << 20))
+    twin = {"rhd_default": "rhd", "auto_default": "auto", "ipc_rhd": "rhd", "ipc": "auto"}
+    own = {"rhd": "RHD"}  # the path a transport row must have run for a comparison with it to mean anything
+    digests = {}
     try:
-        for algo in (H.Algo.RHD, H.Algo.AUTO, H.Algo.IPC, H.Algo.IPC_RHD):
+        for key, algo, rule, limit in plan:
             comm.set_algo(algo)
+            comm.set_config(H.Config.SMALL_IPC_BYTES, rule)
             for nbytes in sizes:
-                if algo == H.Algo.IPC and nbytes > (256 << 20):
-                    break
-                if algo == H.Algo.IPC_RHD and nbytes > (64 << 20):  # one-shot: (n-1) x S arrive at every rank
+                if nbytes > limit:
                     break
                 row = rows[nbytes]
                 a = send.view(torch.float16)[: nbytes // 2]
@@ -676,41 +719,90 @@ def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
                 try:
                     t = _timed(lambda: comm.all_reduce(a, b, H.HcclReduceOp.SUM, s), iters)
                 except H.HcclError as e:
-                    row[f"{key[algo]}_error"] = str(e)
+                    row[f"{key}_error"] = str(e)
                     continue
-                row[f"{key[algo]}_us"] = round(t * 1e6, 1)
-                row[f"{key[algo]}_busbw_GBps"] = round(nbytes / t / 1e9 * f, 2)
+                row[f"{key}_us"] = round(t * 1e6, 1)
+                row[f"{key}_busbw_GBps"] = round(nbytes / t / 1e9 * f, 2)
+                ran = H.Algo(comm.last_algo).name
+                row[f"{key}_ran"] = ran
                 if nbytes >= (256 << 20):  # the bandwidth end of the curve
-                    row[f"{key[algo]}_xgmi_frac"] = _xgmi_frac(row[f"{key[algo]}_busbw_GBps"], world)
-                # RHD's bits from the one-sided kernel: the IPC_RHD output must equal the RHD schedule's, bit for bit
+                    row[f"{key}_xgmi_frac"] = _xgmi_frac(row[f"{key}_busbw_GBps"], world)
                 sample = b.view(torch.int16)[:: 1 << 10].clone()
-                if algo == H.Algo.RHD:
-                    rhd_digest[nbytes] = sample
-                elif algo == H.Algo.IPC_RHD and nbytes in rhd_digest:
-                    row["ipc_rhd_ran"] = H.Algo(comm.last_algo).name
-                    row["ipc_rhd_matches_rhd"] = bool(torch.equal(sample, rhd_digest[nbytes]))
-                if algo == H.Algo.AUTO:
-                    row["auto_algo"] = H.Algo(comm.last_algo).name
-                if algo == H.Algo.IPC:
-                    row["ipc_ran"] = H.Algo(comm.last_algo).name
-                    row["ipc_barrier_timeouts"] = comm.ipc_status() & 1
+                digests[(key, nbytes)] = sample
+                tw = twin.get(key)
+                if tw is not None and (tw, nbytes) in digests:
+                    tw_ran = row.get(f"{tw}_ran")
+                    # compared only when the twin ran its own schedule (the one-GPU harness runs every row on the
+                    # one-sided kernel; the auto twin's family is whatever the selector picked, so any transport path)
+                    meaningful = tw_ran == own[tw] if tw in own else (tw_ran is not None and not tw_ran.startswith("IPC"))
+                    row[f"{key}_matches_{tw}"] = bool(torch.equal(sample, digests[(tw, nbytes)])) if meaningful else None
+                if ran.startswith("IPC"):
+                    row[f"{key}_barrier_timeouts"] = comm.ipc_status() & 1
         for nbytes in sizes:
             row = rows[nbytes]
-            if nbytes > (1 << 20) or row.get("ipc_ran") != "IPC":
-                continue
-            # the latency end replayed from a HIP graph (50 captured calls per replay; device-side epochs)
-            a = send.view(torch.float16)[: nbytes // 2]
-            b = recv.view(torch.float16)[: nbytes // 2]
-            try:
-                comm.set_algo(H.Algo.IPC)
-                row["ipc_graph_us"] = round(_graph_us(lambda st: comm.all_reduce(a, b, H.HcclReduceOp.SUM, st)), 1)
-                row["ipc_graph_barrier_timeouts"] = comm.ipc_status() & 1
-            except Exception as e:  # noqa: BLE001  (capture problems never end the sweep)
-                row["ipc_graph_error"] = f"{type(e).__name__}: {e}"
+            for key, algo, rule in (("ipc", H.Algo.IPC, 0), ("rhd_default", H.Algo.RHD, small)):
+                if nbytes > (1 << 20) or not str(row.get(f"{key}_ran", "")).startswith("IPC"):
+                    continue
+                # the latency end replayed from a HIP graph (50 captured calls per replay; device-side epochs)
+                a = send.view(torch.float16)[: nbytes // 2]
+                b = recv.view(torch.float16)[: nbytes // 2]
+                try:
+                    comm.set_algo(algo)
+                    comm.set_config(H.Config.SMALL_IPC_BYTES, rule)
+                    row[f"{key}_graph_us"] = round(_graph_us(lambda st: comm.all_reduce(a, b, H.HcclReduceOp.SUM, st)),
+                                                   1)
+                    row[f"{key}_graph_barrier_timeouts"] = comm.ipc_status() & 1
+                except Exception as e:  # noqa: BLE001  (capture problems never end the sweep)
+                    row[f"{key}_graph_error"] = f"{type(e).__name__}: {e}"
     finally:
         comm.set_algo(H.Algo.AUTO)
+        comm.set_config(H.Config.SMALL_IPC_BYTES, small)
     return {"workload": "C5: AllReduce fp16 SUM, size sweep (RHD schedule and auto selection)",
-            "points": [rows[b] for b in sizes]}
+            "small_call_rule_bytes": small, "points": [rows[b] for b in sizes]}
+
+
+def bench_fold_piece(comm, send, recv, world) -> dict:
+    """The fold kernel at its real operating point: inside the C3 program with the reference's own
+    selection (MeshChunk, 4 GiB fp32: batched 8-input folds of the MeshChunk sub-slices over staging a transport group
+    has just written) and inside the C4 ReduceScatter (MeshChunk, 2 GiB bf16), every fold launch timed with HIP events
+    on the reduce stream (Config.FOLD_TIMING: the calls run eagerly) against the program's span on the caller's stream.
+    fold_GBps = the folds' algorithmic bytes ((operands + 1) x elements x size) over their summed durations; whether the
+    folds are on the critical path shows in fold_busy_over_span. Max over ranks."""
+    import torch.distributed as dist
+
+    s = torch.cuda.current_stream()
+    x = send.view(torch.bfloat16)[: (2 << 30) // 2]
+    shard = torch.empty(x.numel() // world, dtype=torch.bfloat16, device=x.device)
+    out = {"note": "per rank: the second of two calls, eager; fold durations are HIP-event brackets of each fold launch"}
+    comm.set_config(H.Config.FOLD_TIMING, 1)
+    try:
+        for name, call in (("c3_mesh_chunk", lambda: comm.all_reduce(send, recv, H.HcclReduceOp.SUM, s)),
+                           ("c4_rs_mesh_chunk", lambda: comm.reduce_scatter(x, shard, H.HcclReduceOp.SUM, s))):
+            comm.set_algo(H.Algo.MESH_CHUNK)
+            try:
+                call()
+                torch.cuda.synchronize()
+                dist.barrier()
+                call()
+                t = comm.fold_timing()
+            except H.HcclError as e:
+                out[name] = {"error": str(e), "ran": H.Algo(comm.last_algo).name}
+                continue
+            v = torch.tensor([t["fold_us"], t["span_us"]], dtype=torch.float64)
+            dist.all_reduce(v, op=dist.ReduceOp.MAX)
+            fold_us, span_us = float(v[0]), float(v[1])
+            out[name] = {"ran": H.Algo(comm.last_algo).name, "folds": t["folds"], "fold_bytes": t["fold_bytes"],
+                         "bytes_per_fold": t["fold_bytes"] // max(1, t["folds"]),
+                         "fold_us": round(fold_us, 1), "fold_avg_us": round(fold_us / max(1, t["folds"]), 2),
+                         "fold_GBps": round(t["fold_bytes"] / (fold_us * 1e-6) / 1e9, 1) if fold_us else None,
+                         "fold_frac_hbm": round(t["fold_bytes"] / (fold_us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)
+                         if fold_us else None,
+                         "span_us": round(span_us, 1), "fold_busy_over_span": round(fold_us / span_us, 4)
+                         if span_us else None}
+    finally:
+        comm.set_config(H.Config.FOLD_TIMING, 0)
+        comm.set_algo(H.Algo.AUTO)
+    return out
 
 
 def bench_e2e_allreduce(comm, world, nbytes: int = 256 << 20, iters: int = 5, chunk: int = 32 << 20) -> dict:
@@ -810,12 +902,12 @@ def bench_c3_algos(comm, send, recv, world) -> dict:
                 row["barrier_timeouts"] = st & 1
                 row["longest_wait_polls_log2"] = (st >> 8) & 0xFF
             out[name] = row
-        # the headline's schedule with every call eager (no executor graph: HCCL_AMD_GRAPH_CACHE=0, read per call),
-        # beside the default, which replays one captured graph per repeated call
+        # the headline's schedule with every call eager (no executor graph: Config.GRAPH_CACHE 0), beside the default,
+        # which replays one captured graph per repeated call
         comm.set_algo(H.Algo.RING)
         comm.set_ipc_blocks(0)
-        saved = os.environ.get("HCCL_AMD_GRAPH_CACHE")
-        os.environ["HCCL_AMD_GRAPH_CACHE"] = "0"
+        saved = comm.get_config(H.Config.GRAPH_CACHE)
+        comm.set_config(H.Config.GRAPH_CACHE, 0)
         try:
             t = _timed(lambda: comm.all_reduce(send, recv, H.HcclReduceOp.SUM, s), 3, warmup=1)
             out["RING_EAGER"] = {"ms": round(t * 1e3, 3),
@@ -824,10 +916,7 @@ def bench_c3_algos(comm, send, recv, world) -> dict:
         except H.HcclError as e:
             out["RING_EAGER"] = {"error": str(e)}
         finally:
-            if saved is None:
-                os.environ.pop("HCCL_AMD_GRAPH_CACHE", None)
-            else:
-                os.environ["HCCL_AMD_GRAPH_CACHE"] = saved
+            comm.set_config(H.Config.GRAPH_CACHE, saved)
     finally:
         comm.set_algo(H.Algo.AUTO)
         comm.set_ipc_blocks(0)
@@ -1118,6 +1207,7 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
         # Each secondary config gets a communicator of its own: a failure in one (say an IPC barrier timeout, after
         # which the communicator answers HCCL_E_SUSPENDING) cannot take the others, or the headline, with it.
         for name, fn in (("c3_schedules", lambda cm: bench_c3_algos(cm, send, recv, world)),
+                         ("fold_piece", lambda cm: bench_fold_piece(cm, send, recv, world)),
                          ("c4", lambda cm: bench_c4(cm, send, recv, world)),
                          ("c5", lambda cm: bench_c5(cm, send, recv, world)),
                          ("end_to_end_host_buffers", lambda cm: bench_e2e_allreduce(cm, world))):

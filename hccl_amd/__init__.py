@@ -256,6 +256,14 @@ class Comm:
         the communicator was created)."""
         check("HcclAmdCommSetConfig", lib.HcclAmdCommSetConfig(self.handle, int(key), int(value)))
 
+    def fold_timing(self) -> dict:
+        """HcclAmdCommFoldTiming: the folds of the last executor program while Config.FOLD_TIMING is on."""
+        f, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        fu, su = ctypes.c_double(0), ctypes.c_double(0)
+        check("HcclAmdCommFoldTiming", lib.HcclAmdCommFoldTiming(self.handle, ctypes.byref(f), ctypes.byref(b),
+                                                                 ctypes.byref(fu), ctypes.byref(su)))
+        return {"folds": f.value, "fold_bytes": b.value, "fold_us": fu.value, "span_us": su.value}
+
     def get_config(self, key: int) -> int:
         v = ctypes.c_int64(0)
         check("HcclAmdCommGetConfig", lib.HcclAmdCommGetConfig(self.handle, int(key), ctypes.byref(v)))

@@ -105,6 +105,7 @@ class Config(enum.IntEnum):
     IPC_STAGING_CACHED = 13
     IPC_TRACE = 14
     IPC_L2_SCRUB = 15
+    FOLD_TIMING = 16
 
 
 class AivVariant(enum.IntEnum):
@@ -213,6 +214,8 @@ SIGNATURES = {
     "HcclAmdCommSetConfig": (_res, [_vp, _i32, ctypes.c_int64]),
     "HcclAmdCommGetConfig": (_res, [_vp, _i32, ctypes.POINTER(ctypes.c_int64)]),
     "HcclAmdSetDeviceCopyKernel": (_res, [_i32]),
+    "HcclAmdCommFoldTiming": (_res, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64), ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(ctypes.c_double)]),
     "HcclAmdCommCompileStats": (_res, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     "HcclAmdCommGraphStats": (_res, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     "HcclAmdCommExecute": (_res, [_vp, ctypes.POINTER(HcclAmdIrOp), _u64, _vp, _vp, _i32, _i32, _i32, _vp]),

@@ -142,6 +142,7 @@ Comm::~Comm()
     transport.reset();
     TeardownTrace(rank, "events, staging, streams", true);
     for (hipEvent_t e : events) (void)hipEventDestroy(e);
+    for (hipEvent_t e : foldTiming.pool) (void)hipEventDestroy(e);
     if (scratch != nullptr) (void)hipFree(scratch);
     if (commStream != nullptr) (void)hipStreamDestroy(commStream);
     if (reduceStream != nullptr) (void)hipStreamDestroy(reduceStream);

@@ -259,6 +259,19 @@ struct Comm {
     uint64_t graphLaunches = 0;
     uint64_t graphCaptures = 0;
 
+    // Fold timing (CommConfig::foldTiming, HCCL_AMD_FOLD_TIMING; diagnostics of the fold's operating point inside a
+    // program, bench.py's fold_piece row): the last eager Execute's fold launches, each bracketed by timing events on
+    // its stream, with their algorithmic bytes, and the program's span on the caller's stream (HcclAmdCommFoldTiming).
+    struct FoldTiming {
+        std::vector<hipEvent_t> pool;  // timing-enabled, reused call after call
+        size_t next = 0;
+        std::vector<std::pair<hipEvent_t, hipEvent_t>> folds;
+        std::vector<uint64_t> bytes;
+        hipEvent_t spanStart = nullptr;
+        hipEvent_t spanEnd = nullptr;
+        HcclResult Next(hipEvent_t* e);
+    } foldTiming;
+
     // The end of the last collective on its user stream: a call on another stream waits for it first, since every
     // call of a communicator shares its staging (OrderAfterTail / MarkTail).
     hipEvent_t tail = nullptr;

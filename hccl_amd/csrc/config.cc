@@ -76,6 +76,7 @@ CommConfig ReadCommConfig()
     c.ipcStagingCached = EnvIs("HCCL_AMD_IPC_STAGING_CACHED", "1", false);
     c.ipcTrace = EnvIs("HCCL_AMD_IPC_TRACE", "1", false);
     c.ipcL2Scrub = !EnvIs("HCCL_AMD_IPC_L2_SCRUB", "0", false);
+    c.foldTiming = EnvIs("HCCL_AMD_FOLD_TIMING", "1", false);
     return c;
 }
 
@@ -127,6 +128,7 @@ HcclResult SetConfigEntry(CommConfig& c, int32_t key, int64_t value)
         case HCCL_AMD_CFG_IPC_STAGING_CACHED: if (!flag()) return HCCL_E_PARA; c.ipcStagingCached = value != 0; break;
         case HCCL_AMD_CFG_IPC_TRACE: if (!flag()) return HCCL_E_PARA; c.ipcTrace = value != 0; break;
         case HCCL_AMD_CFG_IPC_L2_SCRUB: if (!flag()) return HCCL_E_PARA; c.ipcL2Scrub = value != 0; break;
+        case HCCL_AMD_CFG_FOLD_TIMING: if (!flag()) return HCCL_E_PARA; c.foldTiming = value != 0; break;
         default: return HCCL_E_PARA;
     }
     return HCCL_SUCCESS;
@@ -151,6 +153,7 @@ HcclResult GetConfigEntry(const CommConfig& c, int32_t key, int64_t* value)
         case HCCL_AMD_CFG_IPC_STAGING_CACHED: *value = c.ipcStagingCached; break;
         case HCCL_AMD_CFG_IPC_TRACE: *value = c.ipcTrace; break;
         case HCCL_AMD_CFG_IPC_L2_SCRUB: *value = c.ipcL2Scrub; break;
+        case HCCL_AMD_CFG_FOLD_TIMING: *value = c.foldTiming; break;
         default: return HCCL_E_PARA;
     }
     return HCCL_SUCCESS;

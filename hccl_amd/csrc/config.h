@@ -33,6 +33,7 @@ struct CommConfig {
     bool ipcStagingCached = false;                // HCCL_AMD_IPC_STAGING_CACHED (diagnostics)
     bool ipcTrace = false;                        // HCCL_AMD_IPC_TRACE (diagnostics)
     bool ipcL2Scrub = true;                       // HCCL_AMD_IPC_L2_SCRUB
+    bool foldTiming = false;                      // HCCL_AMD_FOLD_TIMING: time the executor's folds (diagnostics)
 };
 
 // The configuration a communicator created now takes.

@@ -122,7 +122,7 @@ size_t BatchRun(const std::vector<HcclAmdIrOp>& ops, size_t i, uint64_t es, void
 }
 
 // Launches REDUCE records ops[i, i+m) (one batch, or a single fold when m == 1).
-HcclResult LaunchFolds(const std::vector<HcclAmdIrOp>& ops, size_t i, size_t m, uint64_t es, void* const bufs[3],
+HcclResult LaunchFoldsRaw(const std::vector<HcclAmdIrOp>& ops, size_t i, size_t m, uint64_t es, void* const bufs[3],
                        HcclDataType dt, HcclReduceOp op, hipStream_t stream)
 {
     auto addr = [&](int32_t buf, uint64_t off) { return reinterpret_cast<uintptr_t>(bufs[buf]) + off * es; };
@@ -143,6 +143,24 @@ HcclResult LaunchFolds(const std::vector<HcclAmdIrOp>& ops, size_t i, size_t m, 
     return LaunchReduceNBatch(segs, static_cast<uint32_t>(m), static_cast<uint32_t>(ops[i].nsrc), dt, op, stream);
 }
 
+// LaunchFoldsRaw, bracketed by timing events when the communicator times its folds (Comm::FoldTiming).
+HcclResult LaunchFolds(Comm& c, bool timed, const std::vector<HcclAmdIrOp>& ops, size_t i, size_t m, uint64_t es,
+                       void* const bufs[3], HcclDataType dt, HcclReduceOp op, hipStream_t stream)
+{
+    if (!timed) return LaunchFoldsRaw(ops, i, m, es, bufs, dt, op, stream);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HCCL_CHK(c.foldTiming.Next(&e0));
+    HCCL_CHK(c.foldTiming.Next(&e1));
+    HIP_CHK(hipEventRecord(e0, stream));
+    HCCL_CHK(LaunchFoldsRaw(ops, i, m, es, bufs, dt, op, stream));
+    HIP_CHK(hipEventRecord(e1, stream));
+    uint64_t bytes = 0;
+    for (size_t g = i; g < i + m; ++g) bytes += uint64_t(ops[g].nsrc + 1) * ops[g].count * es;
+    c.foldTiming.folds.emplace_back(e0, e1);
+    c.foldTiming.bytes.push_back(bytes);
+    return HCCL_SUCCESS;
+}
+
 // HCCL_AMD_INJECT_STALL_GROUP=k (timeout tests): before the communicator's k-th transport group, outside capture, the
 // group's stream waits on the injected stall kernel, as if the peer never posted its half of the group.
 HcclResult MaybeInjectStall(Comm& c, hipStream_t s)
@@ -158,7 +176,7 @@ HcclResult MaybeInjectStall(Comm& c, hipStream_t s)
 // Small collectives have one pipeline piece, so the two-stream split cannot overlap anything: every unit goes on
 // the caller's stream in program order and no event is recorded or waited on (the latency floor of C5).
 static HcclResult ExecuteSingleStream(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const bufs[3],
-                                      HcclDataType dt, HcclReduceOp op, hipStream_t user, bool captured)
+                                      HcclDataType dt, HcclReduceOp op, hipStream_t user, bool captured, bool timed)
 {
     const uint64_t es = DataTypeSize(dt);
     auto addr = [&](int32_t buf, uint64_t off) -> uintptr_t {
@@ -192,7 +210,7 @@ static HcclResult ExecuteSingleStream(Comm& c, const std::vector<HcclAmdIrOp>& o
         } else if (o.kind == HCCL_AMD_IR_REDUCE) {
             HpScope hp(HCCL_AMD_HP_FOLD);
             const size_t m = BatchRun(ops, i, es, bufs);
-            HCCL_CHK(LaunchFolds(ops, i, m, es, bufs, dt, op, user));
+            HCCL_CHK(LaunchFolds(c, timed, ops, i, m, es, bufs, dt, op, user));
             i += m;
             continue;
         } else {
@@ -405,7 +423,23 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
     // call runs later, from a graph, outside any entry: not tracked.
     HpScope hpTotal(HCCL_AMD_HP_EXECUTE);
     WatchScope watch(captured ? nullptr : c.watchdog.get(), user, !singleStream);
-    if (singleStream) return ExecuteSingleStream(c, ops, bufs, dt, op, user, captured);
+    const bool timed = c.cfg.foldTiming && !captured;
+    if (timed) {
+        c.foldTiming.next = 0;
+        c.foldTiming.folds.clear();
+        c.foldTiming.bytes.clear();
+        c.foldTiming.spanEnd = nullptr;
+        HCCL_CHK(c.foldTiming.Next(&c.foldTiming.spanStart));
+        HIP_CHK(hipEventRecord(c.foldTiming.spanStart, user));
+    }
+    if (singleStream) {
+        HCCL_CHK(ExecuteSingleStream(c, ops, bufs, dt, op, user, captured, timed));
+        if (timed) {
+            HCCL_CHK(c.foldTiming.Next(&c.foldTiming.spanEnd));
+            HIP_CHK(hipEventRecord(c.foldTiming.spanEnd, user));
+        }
+        return HCCL_SUCCESS;
+    }
     const uint64_t es = DataTypeSize(dt);
     // Under stream capture the transport groups go on the capturing stream itself and only the folds on a forked
     // stream: an RCCL group captured on a stream joined to the capture (rather than its origin) brought down graph
@@ -458,7 +492,7 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
                 const void* src = reinterpret_cast<const void*>(addr(o.srcBuf[0], o.srcOff[0]));
                 HCCL_CHK(LaunchCopyBytes(dst, src, o.count * es, streams[x]));
             } else if (o.kind == HCCL_AMD_IR_REDUCE) {
-                HCCL_CHK(LaunchFolds(ops, u.first, u.count, es, bufs, dt, op, streams[x]));
+                HCCL_CHK(LaunchFolds(c, timed, ops, u.first, u.count, es, bufs, dt, op, streams[x]));
             } else {
                 return HCCL_E_INTERNAL;
             }
@@ -479,6 +513,21 @@ HcclResult Execute(Comm& c, const std::vector<HcclAmdIrOp>& ops, void* const buf
         HIP_CHK(hipEventRecord(end, streams[s]));
         HIP_CHK(hipStreamWaitEvent(user, end, 0));
     }
+    if (timed) {
+        HCCL_CHK(c.foldTiming.Next(&c.foldTiming.spanEnd));
+        HIP_CHK(hipEventRecord(c.foldTiming.spanEnd, user));
+    }
+    return HCCL_SUCCESS;
+}
+
+HcclResult Comm::FoldTiming::Next(hipEvent_t* e)
+{
+    if (next == pool.size()) {
+        hipEvent_t ev;
+        HIP_CHK(hipEventCreate(&ev));  // timing enabled
+        pool.push_back(ev);
+    }
+    *e = pool[next++];
     return HCCL_SUCCESS;
 }
 
@@ -590,7 +639,7 @@ HcclResult RunCompiled(Comm& c, const CompiledSchedule& cs, void* const bufs[3],
     const std::vector<UnitPlan>* plan = single ? nullptr : &cs.plan;
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     HIP_CHK(hipStreamIsCapturing(user, &st));
-    if (cap == 0 || st != hipStreamCaptureStatusNone || !c.transport->Abortable()) {
+    if (cap == 0 || st != hipStreamCaptureStatusNone || !c.transport->Abortable() || c.cfg.foldTiming) {
         return Execute(c, cs.sched.ops, bufs, dt, op, user, single, plan);
     }
     if (!c.retiredGraphs.empty()) ReapRetiredGraphs(c, false);
@@ -659,6 +708,33 @@ void ReleaseGraphs(Comm& c)
 }
 
 }  // namespace hccl_amd
+
+extern "C" HcclResult HcclAmdCommFoldTiming(HcclComm comm, uint64_t* folds, uint64_t* foldBytes, double* foldUs,
+                                            double* spanUs)
+{
+    hccl_amd::Comm* c = hccl_amd::AsComm(comm);
+    if (c == nullptr || folds == nullptr || foldBytes == nullptr || foldUs == nullptr || spanUs == nullptr) {
+        return HCCL_E_PTR;
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    const auto& t = c->foldTiming;
+    if (t.spanEnd == nullptr) return HCCL_E_NOT_SUPPORT;
+    HIP_CHK(hipEventSynchronize(t.spanEnd));
+    float ms = 0;
+    double sum = 0;
+    uint64_t bytes = 0;
+    for (size_t k = 0; k < t.folds.size(); ++k) {
+        HIP_CHK(hipEventElapsedTime(&ms, t.folds[k].first, t.folds[k].second));
+        sum += ms;
+        bytes += t.bytes[k];
+    }
+    HIP_CHK(hipEventElapsedTime(&ms, t.spanStart, t.spanEnd));
+    *folds = t.folds.size();
+    *foldBytes = bytes;
+    *foldUs = sum * 1e3;
+    *spanUs = double(ms) * 1e3;
+    return HCCL_SUCCESS;
+}
 
 extern "C" HcclResult HcclAmdCommGraphStats(HcclComm comm, uint64_t* launches, uint64_t* captures)
 {

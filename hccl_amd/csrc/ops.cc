@@ -614,13 +614,9 @@ HcclResult HcclAmdCommExecute(HcclComm comm,const HcclAmdIrOp* ops, uint64_t num
     const EntryScope entry(*c, static_cast<hipStream_t>(stream));
     HCCL_CHK(entry.status());
     void* bufs[3] = {sendBuf, recvBuf, c->scratch};
-    if (singleStream != 0) {
-        const std::vector<HcclAmdIrOp> prog(ops, ops + numOps);
-        return Execute(*c, prog, bufs, dataType, op, static_cast<hipStream_t>(stream), true);
-    }
     const CompiledSchedule* cs = nullptr;
     HCCL_CHK(CompileProgram(*c, ops, numOps, static_cast<uint32_t>(es), bufs, &cs));
-    return RunCompiled(*c, *cs, bufs, dataType, op, static_cast<hipStream_t>(stream));
+    return RunCompiled(*c, *cs, bufs, dataType, op, static_cast<hipStream_t>(stream), singleStream != 0);
 }
 
 HcclResult HcclAmdCommCompileStats(HcclComm comm, uint64_t* hits, uint64_t* misses)

@@ -905,9 +905,16 @@ void ReduceScatterNhr(const ScheduleParams& p, Builder& b)
 
 // ------------------------------------------------------------------------------------------- STRICT tree (O4)
 
-// Order-preserved tree fold (ins_temp_reduce_scatter_order_preserved_group.cc:305-399, RunLocalReduce): blocks are
-// indexed by source rank; while more than one remains, M = largest power of two below the count and block i >= M is
-// folded into block i % M as dst = src (op) dst. n = 8: ((x0+x4)+(x2+x6))+((x1+x5)+(x3+x7)). Rank-independent.
+// Order-preserved tree fold. At n <= 8 (MAX_RANK_NUM_FOR_ORDER_PRESERVED, order_preserved_common.h:22), which is every
+// single-node case, the reference selects AicpuReduceScatterStrictOrderedMesh / AicpuAllReduceStrictOrderedMesh
+// (reduce_scatter_auto_selector.cc:406-413, all_reduce_auto_selector.cc:412-418), i.e. the template
+// InsTempReduceScatterOrderPreservedLevel1: its all-to-all puts source s's block for receiver t into t's CCL slot
+// CalcOutputIndex(t, s) = (t + s) % n (…order_preserved_level1.cc:176-181, 274-278; own block :196-215), and its
+// RunLocalReduce reads virtual index v from slot CalcOutputIndex(v, t) (:322-400), so virtual index = source rank on
+// every receiver (tests/test_strict_level1.py restates the template and checks it against this schedule). Above 8
+// ranks the Group template folds the same tree (ins_temp_reduce_scatter_order_preserved_group.cc:305-399). The tree:
+// while more than one block remains, M = largest power of two below the count and block i >= M is folded into block
+// i % M as dst = src (op) dst. n = 8: ((x0+x4)+(x2+x6))+((x1+x5)+(x3+x7)). Rank-independent.
 // `blocks` must be writable (staging); the last fold writes `out`.
 void EmitTree(Builder& b, const std::vector<Ref>& blocks, Ref out, uint64_t count)
 {

@@ -232,10 +232,21 @@ typedef enum {
     HCCL_AMD_CFG_IPC_STAGING_CACHED = 13,  /* (=) HCCL_AMD_IPC_STAGING_CACHED (diagnostics); at the IPC set-up */
     HCCL_AMD_CFG_IPC_TRACE = 14,           /* HCCL_AMD_IPC_TRACE: phase stamps (diagnostics); at the IPC set-up */
     HCCL_AMD_CFG_IPC_L2_SCRUB = 15,        /* HCCL_AMD_IPC_L2_SCRUB: L2 maintenance at the IPC set-up (default 1) */
-    HCCL_AMD_CFG_COUNT = 16
+    HCCL_AMD_CFG_FOLD_TIMING = 16,         /* HCCL_AMD_FOLD_TIMING: time the executor's folds (diagnostics; calls run
+                                              eagerly, HcclAmdCommFoldTiming reads the last one) */
+    HCCL_AMD_CFG_COUNT = 17
 } HcclAmdConfigKey;
 extern HcclResult HcclAmdCommSetConfig(HcclComm comm, int32_t key, int64_t value);
 extern HcclResult HcclAmdCommGetConfig(HcclComm comm, int32_t key, int64_t* value);
+
+/* The folds of comm's last executor program while HCCL_AMD_CFG_FOLD_TIMING is on (diagnostics: the fold's operating
+ * point inside a program, on staging a transport group has just written). Waits for that program's end. *folds = fold
+ * launches (a batch counts once), *foldBytes = their algorithmic bytes (sum over records of (operands + 1) x count x
+ * element size), *foldUs = the sum of their durations (HIP events around each launch on its stream), *spanUs = the
+ * program's span on the caller's stream. HCCL_E_NOT_SUPPORT when no timed program ran (timing off, the one-sided
+ * kernel, a capture). */
+extern HcclResult HcclAmdCommFoldTiming(HcclComm comm, uint64_t* folds, uint64_t* foldBytes, double* foldUs,
+                                        double* spanUs);
 
 /* Process-wide: the device-to-device copies the library makes (loopback links, COPY records, one-operand folds, a
  * one-rank collective) run as its copy kernel (on != 0, the default) or as hipMemcpyAsync (0; diagnostics).

@@ -1145,3 +1145,34 @@ def test_calls_on_two_streams_are_ordered(worlds, algo):
     for r in range(n):
         assert O.equal_bits(O.FP32, to_host(O.FP32, oa[r]), wa[r]), r
         assert O.equal_bits(O.FP32, to_host(O.FP32, ob[r]), wb[r]), r
+
+
+def test_fold_timing_reports_the_programs_folds():
+    """Config.FOLD_TIMING (bench.py's fold_piece row): the executor brackets every fold launch of a program with timing
+    events; HcclAmdCommFoldTiming reports as many folds as the plan launches, their algorithmic bytes exactly as the IR
+    has them ((operands + 1) x count x size per REDUCE record), durations inside the program's span, and the result
+    stays bit-exact. Off, or on the one-sided kernel, there is nothing to report."""
+    n, count = 4, (8 << 20) // 4 + 5
+    comms = H.loopback_world(n)
+    try:
+        xs = [O.random_operands(O.FP32, count, seed=5100 + r, edge=False) for r in range(n)]
+        with pytest.raises(H.HcclError):
+            comms[0].fold_timing()
+        for c in comms:
+            c.set_config(H.Config.FOLD_TIMING, 1)
+        used, outs = collective(comms, AR, R.ALGO_MESHCHUNK, O.FP32, O.SUM, xs, count)
+        assert used == R.ALGO_MESHCHUNK
+        want = R.expected(AR, used, O.FP32, O.SUM, xs, count)
+        for r in range(n):
+            assert O.equal_bits(O.FP32, outs[r], want[r]), r
+        for r in range(n):
+            arr, nops, _, _ = H.build_schedule(AR, R.ALGO_MESHCHUNK, n, r, count, O.FP32)
+            ir_bytes = sum((o.nsrc + 1) * o.count * 4 for o in arr[:nops] if o.kind == H.IrKind.REDUCE)
+            t = comms[r].fold_timing()
+            assert t["fold_bytes"] == ir_bytes, (r, t, ir_bytes)
+            assert 0 < t["folds"] <= sum(1 for o in arr[:nops] if o.kind == H.IrKind.REDUCE), t
+            assert 0 < t["fold_us"] <= t["span_us"], t
+    finally:
+        torch.cuda.synchronize()
+        for c in comms:
+            c.destroy()

@@ -6,6 +6,9 @@ Programs (rank 0's program of an 8-rank schedule, peers mapped onto the self loo
            every call is eager
   oneshot  C5's 1 KiB fp16 AllReduce, one-shot (single-stream: one transport group + one 8-input fold)
   group1k  the one-shot's transport group alone (7 sends + 7 receives of 128 B): RCCL's own enqueue cost
+  rhd1k / rhd1m  C5's schedule, the 8-rank RHD AllReduce fp16 at 1 KiB and 1 MiB (single-stream: 6 transport groups and
+           the halving folds); since r05 single-stream programs replay from the executor graph cache too (the key's
+           second call on), so with the cache on the "eager" loop is graph launches
 For each: eager wall time per program (enqueue + GPU, K back-to-back programs then one sync), host enqueue time per
 program (the loop without the sync), the same program replayed from a HIP graph, and with HCCL_AMD_HOST_PROFILE=1 the
 executor's host time by category.
@@ -85,6 +88,11 @@ def main():
     measure(comm, "oneshot1k", arr, nops, xh, yh, True, s, H.HcclDataType.FP16)
     garr, gn = group_only(arr, nops)
     measure(comm, "group1k", garr, gn, xh, yh, True, s, H.HcclDataType.FP16)
+    for name, cnt in (("rhd1k", 512), ("rhd1m", 1 << 19)):
+        arr, nops, _ = self_looped(H.OpType.ALLREDUCE, int(H.Algo.RHD), 8, 0, cnt, H.HcclDataType.FP16)
+        xr = torch.rand(cnt, device="cuda").half()
+        yr = torch.empty_like(xr)
+        measure(comm, name, arr, nops, xr, yr, True, s, H.HcclDataType.FP16)
     comm.destroy()
 
 

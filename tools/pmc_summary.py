@@ -11,9 +11,22 @@ read, so the read side is doubled: hbm = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
 import argparse
 import csv
 import glob
+import hashlib
 import json
 import os
 import statistics
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def library_sha256(path=os.path.join(ROOT, "hccl_amd", "libhccl_amd.so")):
+    """Identity of the library the counters were taken on: bench.py compares it with the library it loads, so a
+    counter figure taken on other kernels is flagged in the line (VERDICT r04 next #5)."""
+    try:
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        return None
 
 
 def counter_values(path, kernel, name):
@@ -65,6 +78,10 @@ def main():
         "traffic_over_algorithmic": (hbm / a.algorithmic_bytes) if hbm else None,
         "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE counts half of a 16 B/lane stream)",
         "note": a.note,
+        # provenance: the library profiled and the source commit it was built from (HCCL_AMD_SOURCE_COMMIT, passed in
+        # by the GPU call: the GPU box has no .git)
+        "library_sha256": library_sha256(),
+        "source_commit": os.environ.get("HCCL_AMD_SOURCE_COMMIT"),
     }
     if st:
         out["achieved_GBps_from_trace"] = a.algorithmic_bytes / (float(st["AverageNs"]) * 1e-9) / 1e9
