@@ -132,3 +132,51 @@ def test_config_round_trip_and_ranges():
             assert e.value.code == H.HcclResult.HCCL_E_PARA
     finally:
         destroy(comms)
+
+
+def _random_small_cases(k):
+    rng = np.random.default_rng(20261018)
+    dts = [O.INT8, O.INT16, O.INT32, O.INT64, O.UINT64, O.FP16, O.BFP16, O.FP32, O.FP64]
+    out = []
+    for i in range(k):
+        n = int(rng.choice([2, 3, 4, 5, 6, 8]))
+        algo = int(rng.choice([H.Algo.AUTO, H.Algo.RHD])) if n in (2, 4, 8) else int(H.Algo.AUTO)
+        dtype = int(rng.choice(dts))
+        op = int(rng.choice(O.OPS))
+        if op == O.PROD and dtype in (O.INT16, O.BFP16):  # PROD is refused on these (CheckReduceOp)
+            op = O.MAX
+        es = np.dtype(O.NP_STORAGE[dtype]).itemsize
+        count = int(rng.integers(1, (1 << 20) // es + 1))  # up to the rule's 1 MiB per rank
+        inplace = bool(rng.integers(2))
+        out.append((i, n, algo, dtype, op, count, inplace))
+    return out
+
+
+@pytest.fixture(scope="module")
+def small_worlds():
+    cache = {}
+
+    def get(n):
+        if n not in cache:
+            cache[n] = world(n)
+        return cache[n]
+
+    yield get
+    torch.cuda.synchronize()
+    for comms in cache.values():
+        for c in comms:
+            c.destroy()
+
+
+@pytest.mark.parametrize("case", _random_small_cases(200), ids=lambda c: f"small{c[0]}")
+def test_random_small_allreduce_matches_the_schedule(small_worlds, case):
+    """Seeded draws over ranks x family (auto, RHD) x dtype x op x count (1 .. 1 MiB) x in-place: the one-sided kernel
+    the rule picks gives the schedule's bits (the oracle replaying that schedule's IR), edge values included."""
+    _, n, algo, dtype, op, count, inplace = case
+    comms = small_worlds(n)
+    xs = [O.random_operands(dtype, count, seed=12000 + 17 * case[0] + r) for r in range(n)]
+    used, outs = collective(comms, AR, algo, dtype, op, xs, count, inplace=inplace)
+    assert used == (H.Algo.IPC_RHD if algo == H.Algo.RHD else H.Algo.IPC), H.Algo(used).name
+    want = oracle_replay(AR, algo, n, count, dtype, op, xs, 0, 0)
+    for r in range(n):
+        assert O.equal_bits(dtype, outs[r], want[r]), (case, r)
