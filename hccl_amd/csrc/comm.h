@@ -94,6 +94,7 @@ struct CompiledSchedule {
     ScheduleParams params;
     Schedule sched;
     uint64_t extent[3] = {0, 0, 0};  // bytes of {sendBuf, recvBuf, scratch} the IR addresses
+    uint32_t groups = 0;             // transport groups of the program
     int64_t relation[3] = {0, 0, 0};  // pairs (0,1), (0,2), (1,2): kDisjoint or the base difference
     bool hasPlan = false;
     std::vector<UnitPlan> plan;

@@ -334,7 +334,13 @@ HcclResult FindOrCompile(Comm& c, const ScheduleParams& p, void* const bufs[3], 
         auto e = std::make_unique<CompiledSchedule>();
         e->params = p;
         HCCL_CHK(make(&e->sched));
+        int32_t lastGroup = -1;
+        bool inGroup = false;
         for (const HcclAmdIrOp& o : e->sched.ops) {
+            const bool p2p = o.kind == HCCL_AMD_IR_SEND || o.kind == HCCL_AMD_IR_RECV;
+            if (p2p && (!inGroup || o.group != lastGroup)) ++e->groups;
+            inGroup = p2p;
+            lastGroup = o.group;
             const uint64_t bytes = o.count * p.elemSize;
             if (o.dstBuf >= 0 && o.dstBuf < 3) {
                 e->extent[o.dstBuf] = std::max(e->extent[o.dstBuf], (o.dstOff + o.count) * p.elemSize);
@@ -639,7 +645,11 @@ HcclResult RunCompiled(Comm& c, const CompiledSchedule& cs, void* const bufs[3],
     const std::vector<UnitPlan>* plan = single ? nullptr : &cs.plan;
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     HIP_CHK(hipStreamIsCapturing(user, &st));
-    if (cap == 0 || st != hipStreamCaptureStatusNone || !c.transport->Abortable() || c.cfg.foldTiming) {
+    // A single-stream program with one transport group stays eager: its two launches enqueue faster than a graph
+    // launch (the C5 1 KiB one-shot over the RCCL self loop: 31.6 us eager, 36.2 us through the cache; an 8-rank RHD of
+    // 6 groups: 54.9 us eager, 43.9 us through the cache; profiles/r05_host_cost_selfloop.jsonl).
+    if (cap == 0 || st != hipStreamCaptureStatusNone || !c.transport->Abortable() || c.cfg.foldTiming ||
+        (single && cs.groups <= 1)) {
         return Execute(c, cs.sched.ops, bufs, dt, op, user, single, plan);
     }
     if (!c.retiredGraphs.empty()) ReapRetiredGraphs(c, false);

@@ -457,6 +457,65 @@ def test_executor_graph_cache_replays_bit_exact():
     assert launches and all(x >= 3 for x in launches), results
 
 
+def _single_stream_graph_worker(q):
+    """Single-stream programs (C5's latency end) through the executor graph cache: an 8-rank RHD at 1 KiB and 1 MiB
+    (6 and 7 transport groups) replays from the cache from its second call on; the 1 KiB one-shot (one group) stays
+    eager, where two launches enqueue faster than a graph launch (profiles/r05_host_cost_selfloop.jsonl)."""
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        import torch
+        import hccl_amd as H
+        from oracle import oracle as O
+        from tests._util import to_device, to_host
+        torch.cuda.set_device(0)
+        comm = H.comm_init_root_info(1, H.get_root_info(), 0)
+        s = torch.cuda.Stream()
+        dtype, op = O.FP16, O.SUM
+        st = O.NP_STORAGE[dtype]
+        results = []
+        for name, algo, count in (("rhd1k", int(H.Algo.RHD), 512), ("rhd1m", int(H.Algo.RHD), 1 << 19),
+                                  ("oneshot1k", int(H.Algo.MESH_ONESHOT), 512)):
+            arr, nops, scratch = self_looped(0, algo, 8, 0, count, dtype)
+            xd = to_device(dtype, np.zeros(count, st))
+            od = to_device(dtype, np.zeros(count, st))
+            before = comm.graph_stats()[0]
+            for rep in range(5):
+                x = O.random_operands(dtype, count, seed=7700 + rep, edge=False)
+                bufs = [[x.copy(), np.zeros(count, st), np.zeros(max(scratch, 1), st)]]
+                assert O.replay(1, dtype, op, [(arr, nops)], bufs) == 0
+                torch.cuda.synchronize()
+                xd.copy_(to_device(dtype, x))
+                od.zero_()
+                torch.cuda.synchronize()
+                comm.execute(arr, nops, xd, od, op, True, s, dtype=dtype)
+                torch.cuda.synchronize()
+                results.append((name, rep, "ok" if O.equal_bits(dtype, to_host(dtype, od), bufs[0][1]) else "mismatch"))
+            results.append((name, "graph_launches", comm.graph_stats()[0] - before))
+        comm.destroy()
+        q.put(("ok", results))
+    except Exception as e:  # noqa: BLE001
+        q.put(("err", f"{type(e).__name__}: {e}\n{traceback.format_exc()}"))
+
+
+def test_single_stream_programs_replay_from_the_graph_cache():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_single_stream_graph_worker, args=(q,))
+    p.start()
+    try:
+        status, results = q.get(timeout=300)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert status == "ok", results
+    assert not [r for r in results if r[-1] == "mismatch"], results
+    launches = {r[0]: r[2] for r in results if r[1] == "graph_launches"}
+    assert launches["rhd1k"] == 4 and launches["rhd1m"] == 4, results  # calls 2..5
+    assert launches["oneshot1k"] == 0, results
+
+
 def _graph_eviction_worker(q):
     """HCCL_AMD_GRAPH_CACHE=2 with more programs than that, called round-robin without a host synchronisation between
     calls: every capture evicts an executable whose last launch may still be in flight (RunCompiled waits for the
