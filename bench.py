@@ -380,6 +380,52 @@ def ipc_two_shot_roofline(dev, n: int = 2, mib: int = 512, reps: int = 10) -> di
             "result_ok": ok}
 
 
+def fold_piece_loopback(n: int = 8, mib: int = 256) -> dict:
+    """The fold at its operating point inside a program on one GPU: the reference's C3
+    selection (MeshChunk, O6) on an n-rank loopback world, `mib` MiB fp32 per rank, every fold launch of rank 0's
+    program timed on its reduce stream (Config.FOLD_TIMING). The folds read MeshChunk sub-slices that the world's links
+    (the library's copy kernel) have just written, so this is the fold on fresh staging at the schedule's piece sizes;
+    the span is the loopback harness's, not xGMI's (its host rendezvous per group), so only the fold figures mean
+    anything here. The N > 1 line's fold_piece row is the same measurement over RCCL on xGMI."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    comms = H.loopback_world(n)
+    count = (mib << 20) // 4
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0x5EED000A)
+    xs = [torch.rand(count, device=dev, generator=g) for _ in range(n)]
+    ys = [torch.empty_like(x) for x in xs]
+    streams = [torch.cuda.Stream() for _ in range(n)]
+    pool = ThreadPoolExecutor(n)
+    try:
+        for c in comms:
+            c.set_algo(H.Algo.MESH_CHUNK)
+            c.set_config(H.Config.FOLD_TIMING, 1)
+        torch.cuda.synchronize()
+        rows = []
+        for _ in range(3):
+            list(pool.map(lambda r: comms[r].all_reduce(xs[r], ys[r], H.HcclReduceOp.SUM, streams[r]), range(n)))
+            torch.cuda.synchronize()
+            rows.append(comms[0].fold_timing())
+        t = rows[-1]
+        ran = H.Algo(comms[0].last_algo).name
+    finally:
+        pool.shutdown()
+        torch.cuda.synchronize()
+        for c in comms:
+            c.destroy()
+    fold_us = float(np.median([r["fold_us"] for r in rows[1:]]))
+    return {"workload": f"C3 selection (MeshChunk) on a {n}-rank loopback world, {mib} MiB fp32 per rank; rank 0's folds",
+            "ran": ran, "folds": t["folds"], "fold_bytes": t["fold_bytes"],
+            "bytes_per_fold": t["fold_bytes"] // max(1, t["folds"]), "fold_us": round(fold_us, 1),
+            "fold_avg_us": round(fold_us / max(1, t["folds"]), 2),
+            "fold_GBps": round(t["fold_bytes"] / (fold_us * 1e-6) / 1e9, 1),
+            "fold_frac_hbm": round(t["fold_bytes"] / (fold_us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+            "span_us": round(t["span_us"], 1),
+            "note": "fold durations are HIP-event brackets of each fold launch on the reduce stream (median of the last "
+                    "two of three calls); the loopback span is harness-bound"}
+
+
 def bench_local(args) -> dict:
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
@@ -492,6 +538,10 @@ def bench_local(args) -> dict:
         res["other_kernels"]["ipc_two_shot"] = ipc_two_shot_roofline(dev)
     except Exception as e:  # noqa: BLE001
         res["other_kernels"]["ipc_two_shot"] = {"error": f"{type(e).__name__}: {e}"}
+    try:
+        res["other_kernels"]["fold_piece_loopback"] = fold_piece_loopback()
+    except Exception as e:  # noqa: BLE001
+        res["other_kernels"]["fold_piece_loopback"] = {"error": f"{type(e).__name__}: {e}"}
     if not args.no_e2e:
         try:
             res["end_to_end_host_buffers"] = end_to_end_host()

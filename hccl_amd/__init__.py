@@ -264,6 +264,10 @@ class Comm:
                                                                  ctypes.byref(fu), ctypes.byref(su)))
         return {"folds": f.value, "fold_bytes": b.value, "fold_us": fu.value, "span_us": su.value}
 
+    def reload_config(self) -> None:
+        """HcclAmdCommReloadConfig: the whole configuration from the environment again (test harnesses)."""
+        check("HcclAmdCommReloadConfig", lib.HcclAmdCommReloadConfig(self.handle))
+
     def get_config(self, key: int) -> int:
         v = ctypes.c_int64(0)
         check("HcclAmdCommGetConfig", lib.HcclAmdCommGetConfig(self.handle, int(key), ctypes.byref(v)))

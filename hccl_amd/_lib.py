@@ -213,6 +213,7 @@ SIGNATURES = {
     "HcclAmdCommLastAlgo": (_i32, [_vp]),
     "HcclAmdCommSetConfig": (_res, [_vp, _i32, ctypes.c_int64]),
     "HcclAmdCommGetConfig": (_res, [_vp, _i32, ctypes.POINTER(ctypes.c_int64)]),
+    "HcclAmdCommReloadConfig": (_res, [_vp]),
     "HcclAmdSetDeviceCopyKernel": (_res, [_i32]),
     "HcclAmdCommFoldTiming": (_res, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64), ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_double)]),

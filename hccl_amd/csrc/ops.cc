@@ -535,6 +535,15 @@ HcclResult HcclAmdCommSetConfig(HcclComm comm, int32_t key, int64_t value)
     return SetConfigEntry(c->cfg, key, value);
 }
 
+HcclResult HcclAmdCommReloadConfig(HcclComm comm)
+{
+    Comm* c = AsComm(comm);
+    if (c == nullptr) return HCCL_E_PTR;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->cfg = ReadCommConfig();
+    return HCCL_SUCCESS;
+}
+
 HcclResult HcclAmdCommGetConfig(HcclComm comm, int32_t key, int64_t* value)
 {
     Comm* c = AsComm(comm);

@@ -238,6 +238,9 @@ typedef enum {
 } HcclAmdConfigKey;
 extern HcclResult HcclAmdCommSetConfig(HcclComm comm, int32_t key, int64_t value);
 extern HcclResult HcclAmdCommGetConfig(HcclComm comm, int32_t key, int64_t* value);
+/* Re-reads comm's whole configuration from the environment, as at its creation (for test harnesses that keep one
+ * communicator across cases with different environments; never called by a collective). */
+extern HcclResult HcclAmdCommReloadConfig(HcclComm comm);
 
 /* The folds of comm's last executor program while HCCL_AMD_CFG_FOLD_TIMING is on (diagnostics: the fold's operating
  * point inside a program, on staging a transport group has just written). Waits for that program's end. *folds = fold

@@ -30,8 +30,12 @@ def worlds():
     cache = {}
 
     def get(n):
+        # the worlds outlive a test, the environment a test sets (monkeypatch) does not: a communicator reads its
+        # configuration when it is created, so every test's worlds read it again here
         if n not in cache:
             cache[n] = H.loopback_world(n)
+        for c in cache[n]:
+            c.reload_config()
         return cache[n]
 
     yield get
@@ -485,6 +489,7 @@ def test_fp32_sum(worlds, op_type, algo, n, count, streams, monkeypatch):
     if streams == "two":
         monkeypatch.setenv("HCCL_AMD_SINGLE_STREAM_BYTES", "0")
     comms = worlds(n)
+    assert comms[0].get_config(H.Config.SINGLE_STREAM_BYTES) == (0 if streams == "two" else 1 << 20)
     root = n - 1
     in_count = count * n if op_type == RS else count
     xs = [O.random_operands(O.FP32, in_count, seed=31 * n + r, edge=False) for r in range(n)]
@@ -530,6 +535,7 @@ def test_random_collectives_match_oracle(worlds, monkeypatch, case):
     if streams == "two":
         monkeypatch.setenv("HCCL_AMD_SINGLE_STREAM_BYTES", "0")
     comms = worlds(n)
+    assert comms[0].get_config(H.Config.SINGLE_STREAM_BYTES) == (0 if streams == "two" else 1 << 20)
     root = (count + n) % n
     in_count = count * n if op_type == RS else count
     xs = [O.random_operands(dtype, in_count, seed=7000 + 13 * case[0] + r, edge=False) for r in range(n)]

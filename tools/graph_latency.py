@@ -59,8 +59,10 @@ def main():
         dist.barrier()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
+        h0 = time.perf_counter()
         for _ in range(K):
             comm.all_reduce(x, y, H.HcclReduceOp.SUM, s)
+        enqueue = (time.perf_counter() - h0) / K * 1e3  # host ms per call (the calls return before the device work)
         e1.record(s)
         torch.cuda.synchronize()
         eager = e0.elapsed_time(e1) / K
@@ -85,13 +87,14 @@ def main():
         torch.cuda.synchronize()
         graph = e0.elapsed_time(e1) / (5 * K)
         ok = bool(torch.all(y == world).item())
-        t = torch.tensor([eager, graph])
+        t = torch.tensor([eager, graph, enqueue])
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         if rank == 0:
             print(json.dumps({"algo": H.Algo(comm.last_algo).name, "n": world, "bytes": nbytes, "eager_us": round(float(t[0]) * 1e3, 2),
-                              "graph_us": round(float(t[1]) * 1e3, 2), "ok": ok,
+                              "graph_us": round(float(t[1]) * 1e3, 2), "enqueue_us": round(float(t[2]) * 1e3, 2),
+                              "ok": ok,
                               "ipc_status_bit0": comm.ipc_status() & 1,
-                              "light_fence": os.environ.get("HCCL_AMD_IPC_LIGHT_FENCE", "0")}), flush=True)
+                              "light_fence": os.environ.get("HCCL_AMD_IPC_LIGHT_FENCE", "default")}), flush=True)
         del g
     torch.cuda.synchronize()
     dist.barrier()

@@ -8,14 +8,15 @@
 # Usage (GPU box, repo root): tools/probes/link_event_experiment.sh [REPS]
 set -uo pipefail
 REPS=${1:-2}
-OUT=gpurun_out/link_event_experiment.txt
+OUT=gpurun_out/link_event_${EXPERIMENT:-events}.txt
 mkdir -p gpurun_out
 : > "$OUT"
 IDS=$(cat tests/r03_failing_selection.txt)
-run() {  # NAME DEVICE_COPY EVENT_DESTROY
+run() {  # NAME DEVICE_COPY EVENT_DESTROY [VAR=VALUE ...]: extra environment for the HIP runtime
   local name=$1 copy=$2 destroy=$3 rep rc
+  shift 3
   for rep in $(seq 1 "$REPS"); do
-    env HCCL_AMD_IPC_STAGING_MIB=64 HCCL_AMD_DEVICE_COPY="$copy" HCCL_AMD_LOOPBACK_EVENT_DESTROY="$destroy" \
+    env HCCL_AMD_IPC_STAGING_MIB=64 HCCL_AMD_DEVICE_COPY="$copy" HCCL_AMD_LOOPBACK_EVENT_DESTROY="$destroy" "$@" \
       timeout -k 10 240 python3 -u -m pytest -x -q -p no:cacheprovider --timeout 120 --timeout-method thread $IDS \
       > "gpurun_out/link_event_${name}_${rep}.log" 2>&1
     rc=$?
@@ -25,4 +26,12 @@ run() {  # NAME DEVICE_COPY EVENT_DESTROY
   done
   return 0
 }
-run memcpy_immediate memcpy immediate && run memcpy_deferred memcpy deferred && run kernel_deferred kernel deferred
+case "${EXPERIMENT:-events}" in
+  events)
+    run memcpy_immediate memcpy immediate && run memcpy_deferred memcpy deferred && run kernel_deferred kernel deferred ;;
+  runtime)
+    # which part of the HIP runtime's device-to-device copy: the SDMA engines (HSA_ENABLE_SDMA=0 makes the runtime use
+    # blit kernels), or the copy's ordering against the next work (AMD_SERIALIZE_COPY=3 waits before and after each copy)
+    run memcpy_sdma_off memcpy deferred HSA_ENABLE_SDMA=0 && \
+      run memcpy_serialize_copy memcpy deferred AMD_SERIALIZE_COPY=3 && run memcpy_plain memcpy deferred ;;
+esac
