@@ -380,13 +380,22 @@ def ipc_two_shot_roofline(dev, n: int = 2, mib: int = 512, reps: int = 10) -> di
             "result_ok": ok}
 
 
+def _device_memory_outside_torch() -> int:
+    """Bytes in use on the current device that torch's caching allocator does not hold (hipMemGetInfo minus torch's
+    reserved bytes): RCCL's and this library's device allocations, plus the runtime's own."""
+    free, total = torch.cuda.mem_get_info()
+    return int(total - free - torch.cuda.memory_reserved())
+
+
 def fold_piece_loopback(n: int = 8, mib: int = 256) -> dict:
     """The fold at its operating point inside a program on one GPU: the reference's C3
     selection (MeshChunk, O6) on an n-rank loopback world, `mib` MiB fp32 per rank, every fold launch of rank 0's
     program timed on its reduce stream (Config.FOLD_TIMING). The folds read MeshChunk sub-slices that the world's links
     (the library's copy kernel) have just written, so this is the fold on fresh staging at the schedule's piece sizes;
-    the span is the loopback harness's, not xGMI's (its host rendezvous per group), so only the fold figures mean
-    anything here. The N > 1 line's fold_piece row is the same measurement over RCCL on xGMI."""
+    the span is the loopback harness's, not xGMI's (its host rendezvous per group). All n ranks' programs run on this
+    one GPU at once, so the fold figures are rank 0's share under contention (r05: 998 GB/s per fold with 8 ranks, about
+    1/8 of HBM); they show the program's fold count and piece sizes, not the kernel's speed. The N > 1 line's
+    fold_piece row is the same measurement over RCCL on xGMI, one rank per GPU."""
     from concurrent.futures import ThreadPoolExecutor
 
     comms = H.loopback_world(n)
@@ -422,8 +431,12 @@ def fold_piece_loopback(n: int = 8, mib: int = 256) -> dict:
             "fold_GBps": round(t["fold_bytes"] / (fold_us * 1e-6) / 1e9, 1),
             "fold_frac_hbm": round(t["fold_bytes"] / (fold_us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
             "span_us": round(t["span_us"], 1),
+            "concurrent_ranks": n,
             "note": "fold durations are HIP-event brackets of each fold launch on the reduce stream (median of the last "
-                    "two of three calls); the loopback span is harness-bound"}
+                    "two of three calls). All ranks share this GPU, so each fold runs beside the other ranks' folds and "
+                    "link copies: fold_GBps is rank 0's share of HBM under that contention, not the fold kernel's rate "
+                    "(C2 and fold_n8 are), and the span is harness-bound. The N > 1 line's fold_piece row is the "
+                    "uncontended operating point"}
 
 
 def bench_local(args) -> dict:
@@ -1108,6 +1121,9 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
 
     if not harness:
         _capture_rccl_init(rank)
+    # device memory outside torch's allocator before the communicator and after its first calls (the cost
+    # of the p2p channel setting, RCCL's per-peer buffers, plus this library's staging and scratch)
+    mem0 = _device_memory_outside_torch()
     comm = new_comm()
     count = C3_BYTES // 4
     g = torch.Generator(device=dev).manual_seed(0x5EED0003 + rank)
@@ -1147,6 +1163,8 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
         warm(comm, headline)
     dist.barrier()
     torch.cuda.synchronize()
+    comm_mem = torch.tensor([_device_memory_outside_torch() - mem0], dtype=torch.float64)
+    dist.all_reduce(comm_mem, op=dist.ReduceOp.MAX)
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     e0, e1 = evs[0], evs[-1]
     t0 = time.perf_counter()
@@ -1224,7 +1242,11 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
                     "p10": round(float(np.percentile(steps_ms.numpy(), 10)), 3),
                     "p90": round(float(np.percentile(steps_ms.numpy(), 90)), 3),
                     "note": "per-step HIP-event durations on the launch stream, max over ranks per step"},
-        "transport": _transport_info(),
+        "transport": dict(_transport_info(), device_memory={
+            "communicator_GiB": round(float(comm_mem.item()) / GIB, 3),
+            "note": "device memory in use outside torch's caching allocator after the headline warm-up minus before "
+                    "the communicator (RCCL's per-peer channel buffers + this library's staging and scratch), max over "
+                    "ranks"}),
         "executor_graphs": {"launches": graph_launches, "captures": graph_captures,
                             "note": "rank 0's calls served by one hipGraphLaunch of the captured executor program "
                                     "(HCCL_AMD_GRAPH_CACHE); the first call of a shape runs eagerly"},
