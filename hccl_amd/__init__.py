@@ -445,7 +445,7 @@ def pending_destroys() -> int:
     return int(lib.HcclAmdCommPendingDestroys())
 
 
-HOST_PROFILE_CATEGORIES = ("execute", "group", "fold", "copy", "record", "wait", "plan")
+HOST_PROFILE_CATEGORIES = ("execute", "group", "fold", "copy", "record", "wait", "plan", "entry", "ipc")
 
 
 def host_profile(reset: bool = True) -> dict:

@@ -22,8 +22,9 @@ namespace hccl_amd {
 
 // ------------------------------------------------------------------------------------------------ host profile
 
-// HCCL_AMD_HOST_PROFILE=1: host time of Execute by category (HcclAmdHostProfile), for the breakdown of the RCCL path's
-// enqueue cost. Off by default: one cached flag test per site.
+// HCCL_AMD_HOST_PROFILE=1: host time by category (HcclAmdHostProfile): the executor's parts, and whole collective
+// entries and one-sided launches (ops.cc, ipc.cc), for the breakdown of the enqueue cost. Off by default: one cached
+// flag test per site.
 namespace {
 
 struct HostProfile {
@@ -37,7 +38,11 @@ HostProfile& Hp()
     return p;
 }
 
-bool HpOn()
+using HpScope = HostProfileScope;
+
+}  // namespace
+
+bool HostProfileOn()
 {
     static const bool on = [] {
         const char* e = std::getenv("HCCL_AMD_HOST_PROFILE");
@@ -46,28 +51,11 @@ bool HpOn()
     return on;
 }
 
-class HpScope {
-public:
-    explicit HpScope(int cat) : cat_(HpOn() ? cat : -1)
-    {
-        if (cat_ >= 0) t0_ = std::chrono::steady_clock::now();
-    }
-    ~HpScope()
-    {
-        if (cat_ < 0) return;
-        const auto ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0_);
-        Hp().ns[cat_].fetch_add(static_cast<uint64_t>(ns.count()), std::memory_order_relaxed);
-        Hp().calls[cat_].fetch_add(1, std::memory_order_relaxed);
-    }
-    HpScope(const HpScope&) = delete;
-    HpScope& operator=(const HpScope&) = delete;
-
-private:
-    int cat_;
-    std::chrono::steady_clock::time_point t0_;
-};
-
-}  // namespace
+void HostProfileAdd(int cat, uint64_t ns)
+{
+    Hp().ns[cat].fetch_add(ns, std::memory_order_relaxed);
+    Hp().calls[cat].fetch_add(1, std::memory_order_relaxed);
+}
 
 namespace {
 
@@ -581,7 +569,12 @@ EntryScope::EntryScope(Comm& c, hipStream_t s) : c_(c), s_(s)
 EntryScope::~EntryScope()
 {
     if (captured_ || status_ != HCCL_SUCCESS) return;
-    if (c_.tail == nullptr && hipEventCreateWithFlags(&c_.tail, hipEventDisableTiming) != hipSuccess) {
+    // The tail only orders this communicator's own work on this device (a later call's stream waits for it, teardown
+    // waits for its completion); nothing on the host or another device reads through it, so it records without the
+    // system-scope fence: 1.0 us of device time per call instead of 3.0 us behind a device-bound kernel
+    // (tools/probes/event_record_cost.py, profiles/r05_event_record_cost.jsonl), on every eager call's critical path.
+    if (c_.tail == nullptr &&
+        hipEventCreateWithFlags(&c_.tail, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
         c_.tail = nullptr;
         return;
     }

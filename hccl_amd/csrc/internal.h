@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -11,6 +12,31 @@
 #include "../../include/hccl_amd.h"
 
 namespace hccl_amd {
+
+// ---- host profile (executor.cc; HCCL_AMD_HOST_PROFILE=1, read once): host time per HCCL_AMD_HP_* category,
+// reported by HcclAmdHostProfile.
+bool HostProfileOn();
+void HostProfileAdd(int cat, uint64_t ns);
+
+class HostProfileScope {
+public:
+    explicit HostProfileScope(int cat) : cat_(HostProfileOn() ? cat : -1)
+    {
+        if (cat_ >= 0) t0_ = std::chrono::steady_clock::now();
+    }
+    ~HostProfileScope()
+    {
+        if (cat_ < 0) return;
+        const auto d = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0_);
+        HostProfileAdd(cat_, static_cast<uint64_t>(d.count()));
+    }
+    HostProfileScope(const HostProfileScope&) = delete;
+    HostProfileScope& operator=(const HostProfileScope&) = delete;
+
+private:
+    int cat_;
+    std::chrono::steady_clock::time_point t0_;
+};
 
 // Reduce ops in the same numbering as HcclReduceOp.
 enum ROp : int { R_SUM = 0, R_PROD = 1, R_MAX = 2, R_MIN = 3 };

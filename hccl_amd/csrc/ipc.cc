@@ -444,6 +444,7 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
                       uint64_t count, HcclDataType dt, HcclReduceOp op, uint32_t root, hipStream_t stream,
                       const uint64_t* vCounts, const uint64_t* vDispls)
 {
+    const HostProfileScope hp(HCCL_AMD_HP_IPC);
     if (plan.geom == kIpcGeomV && (vCounts == nullptr || vDispls == nullptr || plan.loopElems != 0)) {
         return HCCL_E_INTERNAL;
     }

@@ -103,6 +103,7 @@ HcclResult CopyUserBuffer(void* dst, const void* src, uint64_t bytes, hipStream_
 HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, uint64_t count, HcclDataType dt,
                          HcclReduceOp op, uint32_t root, hipStream_t stream)
 {
+    const HostProfileScope hp(HCCL_AMD_HP_ENTRY);
     std::lock_guard<std::mutex> lk(c.mu);
     HCCL_CHK(c.Gate());  // a failed communicator takes no more work (op_common.cc:89-97)
     HIP_CHK(hipSetDevice(c.device));
@@ -235,6 +236,7 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
 HcclResult RunReduceScatterV(Comm& c, void* sendBuf, const uint64_t* counts, const uint64_t* displs, void* recvBuf,
                              HcclDataType dt, HcclReduceOp op, hipStream_t stream)
 {
+    const HostProfileScope hp(HCCL_AMD_HP_ENTRY);
     std::lock_guard<std::mutex> lk(c.mu);
     HCCL_CHK(c.Gate());
     HIP_CHK(hipSetDevice(c.device));

@@ -310,8 +310,8 @@ extern HcclResult HcclAmdLastBootstrap(uint64_t* idDigest, int32_t* stage);
  * rank of the table, which receive them into id128. Same addresses and bounds as HcclCommInitClusterInfo. */
 extern HcclResult HcclAmdBootstrapExchangeId(const char* clusterInfo, uint32_t rank, void* id128);
 
-/* Host time of the executor by category, accumulated while HCCL_AMD_HOST_PROFILE=1 (read at library load): ns[i]
- * and calls[i] for i < n of the categories below; reset != 0 zeroes them afterwards. Diagnostics of the enqueue cost. */
+/* Host time by category, accumulated while HCCL_AMD_HOST_PROFILE=1 (read at library load): ns[i] and calls[i] for
+ * i < n of the categories below; reset != 0 zeroes them afterwards. Diagnostics of the enqueue cost. */
 enum {
     HCCL_AMD_HP_EXECUTE = 0, /* a whole Execute call */
     HCCL_AMD_HP_GROUP = 1,   /* transport groups (ncclGroupStart .. ncclGroupEnd) */
@@ -320,19 +320,24 @@ enum {
     HCCL_AMD_HP_RECORD = 4,  /* unit event records */
     HCCL_AMD_HP_WAIT = 5,    /* cross-stream waits */
     HCCL_AMD_HP_PLAN = 6,    /* planning outside the compiled-collective cache */
-    HCCL_AMD_HP_COUNT = 7
+    HCCL_AMD_HP_ENTRY = 7,   /* a whole collective call past its argument checks (HcclAllReduce, HcclReduceScatter,
+                                HcclReduceScatterV, HcclReduce, HcclAllGather): lock, selection, every enqueue */
+    HCCL_AMD_HP_IPC = 8,     /* the one-sided kernel's host side: launch arguments and the launch (RunIpcPlan) */
+    HCCL_AMD_HP_COUNT = 9
 };
 extern HcclResult HcclAmdHostProfile(uint64_t* ns, uint64_t* calls, uint32_t n, int32_t reset);
 
 /* Communicators whose HcclCommDestroy is waiting for the graphs captured on them to be destroyed. */
 extern uint32_t HcclAmdCommPendingDestroys(void);
 
-/* RCCL's p2p channel settings of this process: *perPeer = NCCL_NCHANNELS_PER_PEER, *minP2pChannels =
- * NCCL_MIN_P2P_NCHANNELS. Unless the environment already sets them, the library sets them when it is loaded (RCCL reads
- * them once, at the process's first communicator, whoever creates it): HCCL_AMD_P2P_CHANNELS_PER_PEER (default 16: RCCL's
- * p2p kernel streams about 43 GB/s per channel, an xGMI link 76.8 GB/s per direction) and per peer x 7 (an 8-GPU
- * node's peers) rounded up to a power of two, at most 64. HCCL_AMD_P2P_CHANNELS_PER_PEER=0 sets neither (both report
- * 0). Child processes inherit them. */
+/* RCCL's p2p channel settings of this process as requested through the environment: *perPeer =
+ * NCCL_NCHANNELS_PER_PEER, *minP2pChannels = NCCL_MIN_P2P_NCHANNELS (0 when unset). Opt-in: only when
+ * HCCL_AMD_P2P_CHANNELS_PER_PEER=k > 0 does the library, when it is loaded, set NCCL_NCHANNELS_PER_PEER = k rounded
+ * up to a power of two and
+ * NCCL_MIN_P2P_NCHANNELS = (the per-peer value in effect) x 7 rounded up to a power of two, at most 64, each unless the
+ * caller set it (RCCL's p2p kernel streams about 43 GB/s per channel, an xGMI link 76.8 GB/s per direction). RCCL reads
+ * them once per process, at its first communicator, so these are requests: RCCL's INIT log says what it set up.
+ * Child processes inherit them. */
 extern HcclResult HcclAmdRcclP2pChannels(uint32_t* perPeer, uint32_t* minP2pChannels);
 
 /* The executor staging of comm (diagnostics): *ptr = its device address (NULL until allocated), *bytes = its size. */

@@ -67,7 +67,7 @@ step_latency() {
   for n in 2 4; do
     for algo in RHD AUTO; do
       port=$((port + 1))
-      run "graph_latency_${algo}_n$n" 240 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" \
+      run "graph_latency_${algo}_n$n" 240 env HCCL_AMD_HOST_PROFILE=1 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" \
         --master-addr 127.0.0.1 --master-port $port tools/graph_latency.py --algo "$algo" \
         --sizes 1024,16384,131072,1048576
       grep -h '^{' "$OUT/graph_latency_${algo}_n$n.log" >> "$OUT/small_call_latency_rank_mode.jsonl" || true

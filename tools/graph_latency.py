@@ -59,10 +59,15 @@ def main():
         dist.barrier()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
+        H.host_profile(reset=True)
         h0 = time.perf_counter()
         for _ in range(K):
             comm.all_reduce(x, y, H.HcclReduceOp.SUM, s)
         enqueue = (time.perf_counter() - h0) / K * 1e3  # host ms per call (the calls return before the device work)
+        # with HCCL_AMD_HOST_PROFILE=1: the library's own host time per call (the entry past its argument checks, and
+        # the one-sided launch within it); the rest of `enqueue` is this script's Python and ctypes
+        prof = H.host_profile(reset=True)
+        lib_us = {k: round(prof[k][0] / max(1, prof[k][1]) / 1e3, 2) for k in ("entry", "ipc") if prof[k][1]}
         e1.record(s)
         torch.cuda.synchronize()
         eager = e0.elapsed_time(e1) / K
@@ -92,6 +97,7 @@ def main():
         if rank == 0:
             print(json.dumps({"algo": H.Algo(comm.last_algo).name, "n": world, "bytes": nbytes, "eager_us": round(float(t[0]) * 1e3, 2),
                               "graph_us": round(float(t[1]) * 1e3, 2), "enqueue_us": round(float(t[2]) * 1e3, 2),
+                              "library_host_us": lib_us,
                               "ok": ok,
                               "ipc_status_bit0": comm.ipc_status() & 1,
                               "light_fence": os.environ.get("HCCL_AMD_IPC_LIGHT_FENCE", "default")}), flush=True)
