@@ -444,3 +444,72 @@ def test_ipc_rank_mode_default_staging():
     detail = json.dumps({r: got[r][1] for r in range(n)})
     for r in range(n):
         assert got[r][1] == [("IPC_TWOSHOT", True, 0)] * len(DEFAULT_STAGING_CALLS), detail
+
+
+def _alternating_main(rank, n, port, q, calls, count):
+    os.environ["HCCL_AMD_IPC_TIMEOUT_MS"] = "20000"
+    try:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n,
+                                timeout=datetime.timedelta(seconds=120))
+        torch.cuda.set_device(0)
+        import hccl_amd as H
+
+        def all_gather(b):
+            out = [None] * n
+            dist.all_gather_object(out, b)
+            return out
+
+        comm = H.comm_init_host_exchange(n, rank, all_gather)
+        comm.set_algo(H.Algo.IPC)  # the auto family's order, the path the small-call rule takes
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        # integer-valued fp32: every order gives the same bits, so a wrong value can only be a call that ran into
+        # another call's staging
+        xs = [torch.full((count,), float((rank + 1) * (k + 1)), device="cuda") for k in range(calls)]
+        ys = [torch.full((count,), -1.0, device="cuda") for _ in range(calls)]
+        comm.all_reduce(xs[0], ys[0], H.HcclReduceOp.SUM, stream=streams[0])  # the collective set-up
+        torch.cuda.synchronize()
+        dist.barrier()
+        for k in range(calls):  # back to back, alternating streams, no host wait
+            comm.all_reduce(xs[k], ys[k], H.HcclReduceOp.SUM, stream=streams[k % 2])
+        torch.cuda.synchronize()
+        tot = n * (n + 1) // 2
+        bad = [k for k in range(calls) if not bool(torch.all(ys[k] == float(tot * (k + 1))).item())]
+        res = {"bad_calls": bad, "algo": H.Algo(comm.last_algo).name, "status_bit0": comm.ipc_status() & 1}
+        dist.barrier()
+        comm.destroy()
+        dist.destroy_process_group()
+        q.put((rank, "ok", res))
+    except Exception:  # noqa: BLE001
+        q.put((rank, traceback.format_exc(), None))
+        time.sleep(10)
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("count", [256, (1 << 20) // 4, (8 << 20) // 4 + 3])
+def test_rank_mode_calls_on_alternating_streams_are_ordered(count):
+    """Rank mode, the one-sided kernel: 32 AllReduces of one communicator issued back to back on two streams in turn
+    with no host wait. Every call shares the communicator's staging, so each waits for the previous call's end through
+    the communicator's tail event (EntryScope, recorded without the system-scope fence since r05): every
+    result exact, no barrier timeout. 1 KiB and 1 MiB are the small-call rule's range, 8 MiB a two-shot call."""
+    n, calls = 2, 32
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_alternating_main, args=(r, n, port, q, calls, count)) for r in range(n)]
+    for p in procs:
+        p.start()
+    try:
+        got = {}
+        for _ in procs:
+            rank, msg, res = q.get(timeout=200)
+            got[rank] = (msg, res)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(n):
+        assert got[r][0] == "ok", f"rank {r}:\n{got[r][0]}"
+        assert got[r][1] == {"bad_calls": [], "algo": "IPC", "status_bit0": 0}, (r, got[r][1])
