@@ -56,11 +56,25 @@ HcclResult Comm::Init(int dev)
     return HCCL_SUCCESS;
 }
 
+// The executor's ordering events (a program's start, its cross-stream unit events and stream joins) keep the runtime's
+// default system-scope fence: unlike the communicator's tail (EntryScope), they order data one stream's kernel or
+// transport group wrote before another stream's kernel reads it. HCCL_AMD_EXECUTOR_EVENT_FENCE=0 (read once; a
+// diagnostic) creates them with hipEventDisableSystemFence, to measure what the fences cost a program.
+static unsigned ExecutorEventFlags()
+{
+    static const unsigned flags = [] {
+        const char* e = std::getenv("HCCL_AMD_EXECUTOR_EVENT_FENCE");
+        const bool off = e != nullptr && std::strcmp(e, "0") == 0;
+        return off ? unsigned(hipEventDisableTiming | hipEventDisableSystemFence) : unsigned(hipEventDisableTiming);
+    }();
+    return flags;
+}
+
 HcclResult Comm::NextEvent(hipEvent_t* e)
 {
     if (nextEvent == events.size()) {
         hipEvent_t ev;
-        HIP_CHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIP_CHK(hipEventCreateWithFlags(&ev, ExecutorEventFlags()));
         events.push_back(ev);
     }
     *e = events[nextEvent++];

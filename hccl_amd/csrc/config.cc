@@ -69,7 +69,7 @@ CommConfig ReadCommConfig()
     if (const char* f = Env("HCCL_AMD_IPC_LIGHT_FENCE")) c.ipcLightFence = std::strcmp(f, "0") != 0 ? 1 : 0;
     c.ipcNt = !EnvIs("HCCL_AMD_IPC_NT", "0", false);
     c.ipcThreads = EnvIs("HCCL_AMD_IPC_THREADS", "512", false) ? 512u : 256u;
-    if (EnvU64("HCCL_AMD_IPC_TILE_KIB", &v)) c.ipcTileBytes = v << 10;
+    if (EnvU64("HCCL_AMD_IPC_TILE_KIB", &v) && v <= (1u << 20)) c.ipcTileBytes = v << 10;  // the setter's range
     c.ipcTimeoutMs = IpcTimeoutMsFromEnv();
     // the staging allocation stays below 2 GiB (ipc.cc IpcSetup): areas of 16 .. 1000 MiB
     if (EnvU64("HCCL_AMD_IPC_STAGING_MIB", &v) && v >= 16 && v <= 1000) c.ipcStagingBytes = v << 20;
