@@ -314,6 +314,12 @@ class Comm:
         check("HcclAmdCommIpcStatus", lib.HcclAmdCommIpcStatus(self.handle, ctypes.byref(v)))
         return v.value
 
+    def ipc_ll_launches(self) -> int:
+        """HcclAmdCommIpcLlLaunches: one-sided launches of this communicator that ran in the LL form so far."""
+        v = ctypes.c_uint32(0)
+        check("HcclAmdCommIpcLlLaunches", lib.HcclAmdCommIpcLlLaunches(self.handle, ctypes.byref(v)))
+        return v.value
+
     def ipc_trace(self):
         """Phase stamps of the last one-sided launch (HCCL_AMD_IPC_TRACE=1 at the first IPC call): a uint64 array
         [16 ranks][512 blocks][8 slots] of 100 MHz ticks and the workgroups per rank of that launch."""

@@ -106,6 +106,7 @@ class Config(enum.IntEnum):
     IPC_TRACE = 14
     IPC_L2_SCRUB = 15
     FOLD_TIMING = 16
+    IPC_LL_BYTES = 17
 
 
 class AivVariant(enum.IntEnum):
@@ -221,6 +222,7 @@ SIGNATURES = {
     "HcclAmdCommGraphStats": (_res, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     "HcclAmdCommExecute": (_res, [_vp, ctypes.POINTER(HcclAmdIrOp), _u64, _vp, _vp, _i32, _i32, _i32, _vp]),
     "HcclAmdCommIpcStatus": (_res, [_vp, ctypes.POINTER(_u32)]),
+    "HcclAmdCommIpcLlLaunches": (_res, [_vp, ctypes.POINTER(_u32)]),
     "HcclAmdCommIpcTrace": (_res, [_vp, ctypes.POINTER(_u64), _u64, ctypes.POINTER(_u32)]),
     "HcclAmdIpcTimeoutMs": (_u64, []),
     "HcclAmdCommInitHostExchange": (_res, [_u32, _u32, _vp, _vp, ctypes.POINTER(_vp)]),

@@ -1,5 +1,6 @@
 // config.cc — the environment, read once per communicator (config.h).
 #include "config.h"
+#include "ipc.h"
 
 #include <strings.h>
 
@@ -77,6 +78,7 @@ CommConfig ReadCommConfig()
     c.ipcTrace = EnvIs("HCCL_AMD_IPC_TRACE", "1", false);
     c.ipcL2Scrub = !EnvIs("HCCL_AMD_IPC_L2_SCRUB", "0", false);
     c.foldTiming = EnvIs("HCCL_AMD_FOLD_TIMING", "1", false);
+    if (EnvU64("HCCL_AMD_IPC_LL_BYTES", &v) && v <= kIpcLlMaxBytes) c.ipcLlBytes = v;
     return c;
 }
 
@@ -129,6 +131,10 @@ HcclResult SetConfigEntry(CommConfig& c, int32_t key, int64_t value)
         case HCCL_AMD_CFG_IPC_TRACE: if (!flag()) return HCCL_E_PARA; c.ipcTrace = value != 0; break;
         case HCCL_AMD_CFG_IPC_L2_SCRUB: if (!flag()) return HCCL_E_PARA; c.ipcL2Scrub = value != 0; break;
         case HCCL_AMD_CFG_FOLD_TIMING: if (!flag()) return HCCL_E_PARA; c.foldTiming = value != 0; break;
+        case HCCL_AMD_CFG_IPC_LL_BYTES:
+            if (!in(0, int64_t(kIpcLlMaxBytes))) return HCCL_E_PARA;
+            c.ipcLlBytes = static_cast<uint64_t>(value);
+            break;
         default: return HCCL_E_PARA;
     }
     return HCCL_SUCCESS;
@@ -154,6 +160,7 @@ HcclResult GetConfigEntry(const CommConfig& c, int32_t key, int64_t* value)
         case HCCL_AMD_CFG_IPC_TRACE: *value = c.ipcTrace; break;
         case HCCL_AMD_CFG_IPC_L2_SCRUB: *value = c.ipcL2Scrub; break;
         case HCCL_AMD_CFG_FOLD_TIMING: *value = c.foldTiming; break;
+        case HCCL_AMD_CFG_IPC_LL_BYTES: *value = static_cast<int64_t>(c.ipcLlBytes); break;
         default: return HCCL_E_PARA;
     }
     return HCCL_SUCCESS;

@@ -34,6 +34,8 @@ struct CommConfig {
     bool ipcTrace = false;                        // HCCL_AMD_IPC_TRACE (diagnostics)
     bool ipcL2Scrub = true;                       // HCCL_AMD_IPC_L2_SCRUB
     bool foldTiming = false;                      // HCCL_AMD_FOLD_TIMING: time the executor's folds (diagnostics)
+    uint64_t ipcLlBytes = 64ull << 10;            // HCCL_AMD_IPC_LL_BYTES: one-shot AllReduces up to this many bytes
+                                                  // per rank (at most 64 KiB) in the LL form (ipc_kernel_body.h)
 };
 
 // The configuration a communicator created now takes.

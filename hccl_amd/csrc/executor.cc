@@ -569,12 +569,12 @@ EntryScope::EntryScope(Comm& c, hipStream_t s) : c_(c), s_(s)
 EntryScope::~EntryScope()
 {
     if (captured_ || status_ != HCCL_SUCCESS) return;
-    // The tail only orders this communicator's own work on this device (a later call's stream waits for it, teardown
-    // waits for its completion); nothing on the host or another device reads through it, so it records without the
-    // system-scope fence: 1.0 us of device time per call instead of 3.0 us behind a device-bound kernel
-    // (tools/probes/event_record_cost.py, profiles/r05_event_record_cost.jsonl), on every eager call's critical path.
-    if (c_.tail == nullptr &&
-        hipEventCreateWithFlags(&c_.tail, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
+    // The tail keeps the runtime's default system-scope fence although it costs 3.0 us of device time per call behind
+    // a device-bound kernel against 1.0 us without (tools/probes/event_record_cost.py,
+    // profiles/r05_event_record_cost.jsonl): it is the last command of every eager call on the caller's stream, the
+    // one a caller's later synchronisation and host read follow, and HIP documents an event recorded without the fence
+    // as not synchronising memory with the host.
+    if (c_.tail == nullptr && hipEventCreateWithFlags(&c_.tail, hipEventDisableTiming) != hipSuccess) {
         c_.tail = nullptr;
         return;
     }

@@ -10,12 +10,57 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <utility>
 
 #include "comm.h"
 
 namespace hccl_amd {
 
 namespace {
+
+// The uncached allocations of the IPC path (staging; flags and LL area) are kept for the life of the process and
+// handed to the next communicator's set-up that asks for the same size on the same device, instead of going back to
+// the runtime. r05: with the flags allocation grown from 32 KiB to 4 MiB (the LL area), the r03 failing order failed
+// 2 of 3 runs in an executor test that follows the IPC tests (test_ownership_orders_follow_executor_loops: rank 0's
+// output missed one rank's contribution in 384 elements, profiles/r05_uncached_reuse_bisect.txt), and passed with the
+// 32 KiB allocation; that test is the only one whose executor staging (2 MiB) fits in a freed 4 MiB block. Memory that
+// was mapped uncached is therefore never handed back for a cached allocation while the process runs.
+struct UncachedPool {
+    std::mutex mu;
+    std::multimap<std::pair<int, size_t>, void*> idle;  // (device, bytes) -> allocation
+};
+
+UncachedPool& Pool()
+{
+    static UncachedPool* p = new UncachedPool;  // never destroyed: the runtime frees device memory at exit
+    return *p;
+}
+
+bool UncachedAlloc(int device, void** ptr, size_t bytes)
+{
+    {
+        UncachedPool& pool = Pool();
+        std::lock_guard<std::mutex> lk(pool.mu);
+        auto it = pool.idle.find({device, bytes});
+        if (it != pool.idle.end()) {
+            *ptr = it->second;
+            pool.idle.erase(it);
+            return true;
+        }
+    }
+    return hipExtMallocWithFlags(ptr, bytes, hipDeviceMallocUncached) == hipSuccess;
+}
+
+void UncachedRelease(int device, void* ptr, size_t bytes)
+{
+    UncachedPool& pool = Pool();
+    std::lock_guard<std::mutex> lk(pool.mu);
+    pool.idle.insert({{device, bytes}, ptr});
+}
+
+size_t FlagAllocBytes() { return size_t(kIpcFlagBytes + 2 * kIpcLlParityBytes); }
 
 struct Exported {
     hipIpcMemHandle_t stg;
@@ -52,7 +97,8 @@ HcclResult IpcSetup(Comm& c)
     // slots of the single-barrier kinds, two areas used alternately: as large as the others, within the one
     // allocation's bound below (the default 512 MiB areas leave them 511.5 MiB)
     s.stgAltBytes = std::min<uint64_t>(area, (kIpcStagingMaxBytes - 2 * area) / 2 / (64ull << 10) * (64ull << 10));
-    const size_t flagBytes = size_t(kIpcMaxBlocks) * kIpcMaxRanks * sizeof(uint32_t);
+    // the flags and, behind them, the LL area (one allocation, one IPC handle; zeroed like the flags)
+    const size_t flagBytes = FlagAllocBytes();
     // The fresh uncached pages may carry lines of a freed cached buffer in some XCD's L2: scrub the L2s before the
     // flags are zeroed (ScrubL2), so that no stale line is ever read or written back over them.
     // HCCL_AMD_IPC_STAGING_CACHED=1 (diagnostics, one device only: the r03 A/B of what uncached staging costs) puts
@@ -67,13 +113,12 @@ HcclResult IpcSetup(Comm& c)
     // link's hipMemcpyAsync, not the layout: DESIGN.md §5b, root cause.)
     const uint64_t stgBytes = s.stgInBytes + s.stgResBytes + 2 * s.stgAltBytes;
     void* base = nullptr;
-    bool ok = (cached ? hipMalloc(&base, stgBytes) : hipExtMallocWithFlags(&base, stgBytes, hipDeviceMallocUncached)) ==
-              hipSuccess;
+    bool ok = cached ? hipMalloc(&base, stgBytes) == hipSuccess : UncachedAlloc(c.device, &base, stgBytes);
     if (ok) AreasOf(s, base, s.area);
     ok = ok &&
-              hipExtMallocWithFlags(reinterpret_cast<void**>(&s.flags), flagBytes, hipDeviceMallocUncached) ==
-                  hipSuccess &&
+              UncachedAlloc(c.device, reinterpret_cast<void**>(&s.flags), flagBytes) &&
               hipMalloc(reinterpret_cast<void**>(&s.status), kIpcStatusBytes) == hipSuccess &&
+              hipMalloc(&s.llUnpack, kIpcLlUnpackBytes) == hipSuccess &&
               hipHostMalloc(reinterpret_cast<void**>(&s.failHost), 64, hipHostMallocCoherent | hipHostMallocMapped) ==
                   hipSuccess &&
               hipHostGetDevicePointer(reinterpret_cast<void**>(&s.failDev), s.failHost, 0) == hipSuccess &&
@@ -234,10 +279,17 @@ void IpcRelease(Comm& c)
             s.opened[r] = false;
         }
     }
-    if (s.area[0] != nullptr) (void)hipFree(s.area[0]);  // the areas are parts of this one allocation
-    if (s.flags != nullptr) (void)hipFree(s.flags);
+    if (s.area[0] != nullptr) {  // the areas are parts of this one allocation
+        if (s.cachedStaging) {
+            (void)hipFree(s.area[0]);
+        } else {
+            UncachedRelease(c.device, s.area[0], s.stgInBytes + s.stgResBytes + 2 * s.stgAltBytes);
+        }
+    }
+    if (s.flags != nullptr) UncachedRelease(c.device, s.flags, FlagAllocBytes());
     if (s.status != nullptr) (void)hipFree(s.status);
     if (s.trace != nullptr) (void)hipFree(s.trace);
+    if (s.llUnpack != nullptr) (void)hipFree(s.llUnpack);
     // the word is no longer watched before it is freed (a failure already seen stays in Comm::failCode)
     c.failWord.store(nullptr, std::memory_order_release);
     if (s.failHost != nullptr) (void)hipHostFree(s.failHost);
@@ -249,10 +301,23 @@ void IpcRelease(Comm& c)
 // Default workgroups per launch by the bytes of one rank's input. Every block runs its own cross-rank barrier (a
 // system-scope release, one flag store per peer, a poll), so small calls pay per block: 16 blocks run a 1 KiB
 // AllReduce in 11 us where 128 take 25 us and 256 take 42 us; large calls want the whole chip (1 GiB: 256 blocks
-// 10 % ahead of 128). Rank-mode sweep on one GPU, n = 2 and 4 (tools/sweep_ipc_blocks.py,
-// profiles/r01_sweep_ipc_blocks.jsonl); the best count agreed between n = 2 and 4 at every size.
+// 10 % ahead of 128). Rank-mode sweep on one GPU, n = 2 and 4 (tools/probes/sweep_ipc_blocks.py,
+// profiles/r01_sweep_ipc_blocks.jsonl); the best count agreed between n = 2 and 4 at every size. Below 16 blocks (r05,
+// profiles/r05_sweep_small_blocks.jsonl): up to 64 KiB, 4 blocks are 0.2-0.5 us faster than 16 at n = 2 (1 KiB
+// 10.26 vs 10.71 us) and no slower at n = 4; from 256 KiB on, fewer than 16 lose bandwidth.
+// Workgroups of an LL launch: about two polled words per thread, (n - 1) x bytes / 4 words over 256-thread blocks. A
+// block's pull, unpack and fold are serial latencies, so the LL form wants many small blocks where the staged kernel
+// wants few: rank mode, n = 2 and 4 on one GPU (tools/probes/sweep_ipc_blocks.py with HCCL_AMD_IPC_LL_BYTES,
+// profiles/r05_ll_sweep_blocks.jsonl): 1 KiB best at 1-2 blocks (7.4 us), 64 KiB at 32 (9.4 us; 55.5 us with 1).
+uint32_t LlIpcBlocks(uint32_t n, uint64_t bytes)
+{
+    const uint64_t items = uint64_t(n > 1 ? n - 1 : 1) * ((bytes + 3) / 4);
+    return static_cast<uint32_t>(std::min<uint64_t>(128, std::max<uint64_t>(1, (items + 511) / 512)));
+}
+
 uint32_t DefaultIpcBlocks(uint64_t bytes)
 {
+    if (bytes <= (64ull << 10)) return 4;
     if (bytes <= (512ull << 10)) return 16;
     if (bytes <= (2ull << 20)) return 32;
     if (bytes <= (32ull << 20)) return 64;
@@ -487,7 +552,15 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
         callBytes = 0;
         for (uint32_t q = 0; q < c.nRanks; ++q) callBytes += vCounts[q] * es;
     }
-    s.blocks = c.ipcBlocks != 0 ? c.ipcBlocks : DefaultIpcBlocks(callBytes);
+    // The LL form (HCCL_AMD_IPC_LL_BYTES; LlOneShot): a one-shot AllReduce of at most that many bytes per rank (and
+    // kIpcLlMaxBytes), one launch of one round. The decision depends only on the call's arguments and the
+    // configuration, which every rank shares, so every rank takes the same form.
+    IpcArgs a{};
+    a.ll = (kind == kIpcAllReduceOneShot && opType == HCCL_AMD_OP_ALLREDUCE && plan.geom == kIpcGeomWhole &&
+            loopElems == 0 && count * es <= std::min<uint64_t>(c.cfg.ipcLlBytes, kIpcLlMaxBytes))
+               ? 1u
+               : 0u;
+    s.blocks = c.ipcBlocks != 0 ? c.ipcBlocks : a.ll != 0 ? LlIpcBlocks(n, callBytes) : DefaultIpcBlocks(callBytes);
     if (c.transport->SharedDevice() && c.ipcBlocks == 0) s.blocks = std::min(s.blocks, kIpcBlocks);
     // Co-residency: every block waits at barriers for its peers' blocks, so all blocks on this device must be resident
     // at once (a loopback world puts every rank's blocks on it; in rank mode, the ranks whose processes share this
@@ -495,12 +568,11 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
     // so ranks of a node agree on it.
     {
         const uint32_t here = c.transport->SharedDevice() ? n : std::max<uint32_t>(1, s.ranksOnDevice);
-        const uint32_t resident = IpcResidentBlocks(dt, op, plan.order == kIpcRhd, c.cfg.ipcThreads);
+        const uint32_t resident = IpcResidentBlocks(dt, op, plan.order == kIpcRhd, a.ll != 0, c.cfg.ipcThreads);
         if (resident != 0) s.blocks = std::max<uint32_t>(1, std::min(s.blocks, resident / here));
     }
     const uint64_t V = 16 / es;
 
-    IpcArgs a{};
     for (uint32_t r = 0; r < n; ++r) {
         a.stgIn[r] = s.peerArea[kIpcAreaIn][r];
         a.stgRes[r] = s.peerArea[kIpcAreaRes][r];
@@ -534,6 +606,7 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
     }
     const bool single = SingleBarrierKind(kind);
     const uint64_t slotCap = ((single ? s.stgAltBytes : s.stgInBytes) / es / n) / V * V;
+
 
     // One launch per executor loop [off, off + cnt) of the reference template whose order the fold follows: its
     // slicing is per loop (schedule.cc RefLoopElems and the MeshChunk loops). A ReduceScatter loop takes elements
@@ -609,12 +682,19 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
         g.threads = c.cfg.ipcThreads;                    // HCCL_AMD_IPC_THREADS
         g.rounds = static_cast<uint32_t>((widest + g.piece - 1) / g.piece);
         g.epochSpan = (single ? 1 : 2) * g.rounds;
+        if (g.ll != 0 && g.rounds == 1) {  // one window per block, no barrier epochs (the LL sequence advances)
+            g.tileElems = 0;
+            g.epochSpan = 0;
+        } else {
+            g.ll = 0;
+        }
     };
     auto at = [es](const void* p, uint64_t off) { return static_cast<char*>(const_cast<void*>(p)) + off * es; };
 
     if (!c.transport->SharedDevice()) {
         a.me = static_cast<int32_t>(c.rank);
         a.aligned = Aligned16(sendBuf, recvBuf);
+        a.llUnpack[c.rank] = s.llUnpack;
         for (const Launch& l : launches) {
             a.in[c.rank] = at(sendBuf, l.off);
             a.out[c.rank] = at(recvBuf, l.off);
@@ -630,10 +710,11 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
     struct Part {
         const void* in;
         void* out;
+        void* unpack;
         hipEvent_t ready;
         int32_t code;
     };
-    Part mine{sendBuf, recvBuf, nullptr, HCCL_SUCCESS};
+    Part mine{sendBuf, recvBuf, s.llUnpack, nullptr, HCCL_SUCCESS};
     c.nextEvent = 0;
     mine.code = c.NextEvent(&mine.ready);
     if (mine.code == HCCL_SUCCESS && hipEventRecord(mine.ready, stream) != hipSuccess) mine.code = HCCL_E_RUNTIME;
@@ -657,6 +738,7 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
             for (uint32_t r = 0; r < n; ++r) {
                 a.in[r] = at(all[r].in, launches[k].off);
                 a.out[r] = at(all[r].out, launches[k].off);
+                a.llUnpack[r] = all[r].unpack;
             }
             geometry(a, launches[k].cnt);
             done.code = LaunchIpcCollective(a, s.blocks, n, dt, op, stream);
@@ -688,6 +770,17 @@ extern "C" HcclResult HcclAmdCommIpcStatus(HcclComm comm, uint32_t* status)
     uint32_t lg = 0;
     while (lg < 32 && (uint64_t(1) << lg) <= wait) ++lg;  // bit length of the longest wait
     *status = (w[0] & 0xFFu) | (lg << 8);
+    return HCCL_SUCCESS;
+}
+
+extern "C" HcclResult HcclAmdCommIpcLlLaunches(HcclComm comm, uint32_t* launches)
+{
+    Comm* c = AsComm(comm);
+    if (c == nullptr || launches == nullptr) return HCCL_E_PTR;
+    *launches = 0;
+    if (!c->ipc.ready) return HCCL_SUCCESS;
+    HIP_CHK(hipSetDevice(c->device));
+    HIP_CHK(hipMemcpy(launches, c->ipc.status + kIpcLlSeqWord, sizeof *launches, hipMemcpyDeviceToHost));
     return HCCL_SUCCESS;
 }
 

@@ -144,6 +144,8 @@ struct IpcArgs {
     uint8_t rhdReal[kIpcMaxRanks - 1][kIpcMaxRanks];  // kIpcRhd: per instance j, virtual rank -> real rank
     uint64_t* trace;  // HCCL_AMD_IPC_TRACE=1: per rank and block, kIpcTraceSlots s_memrealtime stamps of the phases
                       // (IpcTraceSlot); nullptr = off
+    uint32_t ll;      // 1: the one-shot AllReduce through the LL area (flags beside the data, no barrier; LlOneShot)
+    void* llUnpack[kIpcMaxRanks];  // ll: each rank's own cached unpack area, slot q at q * piece elements
 };
 
 // Phase stamps of one block (HCCL_AMD_IPC_TRACE, HcclAmdCommIpcTrace): 100 MHz s_memrealtime ticks, lane 0 of the
@@ -165,10 +167,10 @@ HcclResult LaunchIpcCollective(const IpcArgs& a, uint32_t blocks, uint32_t world
                               HcclReduceOp op, hipStream_t stream);
 
 // Per-dtype entry points of the kernels (ipc_k_*.hip, one translation unit per dtype group): the launch by op, and the
-// kernel's address for the occupancy query (rhd: the kIpcRhd instantiation).
+// kernel's address for the occupancy query (rhd: the kIpcRhd instantiation; ll: the LL kernel).
 #define HCCL_AMD_IPC_DTYPE_DECL(NAME)                                                          \
     hipError_t LaunchIpc_##NAME(int op, const IpcArgs& a, dim3 grid, hipStream_t s); \
-    const void* IpcKernel_##NAME(int op, bool rhd);
+    const void* IpcKernel_##NAME(int op, bool rhd, bool ll);
 HCCL_AMD_IPC_DTYPE_DECL(Int8)
 HCCL_AMD_IPC_DTYPE_DECL(Int16)
 HCCL_AMD_IPC_DTYPE_DECL(Int32)
@@ -182,7 +184,7 @@ HCCL_AMD_IPC_DTYPE_DECL(Fp64)
 
 // Workgroups of the IPC kernel for (dt, op) that the device holds at once (occupancy x CUs; 0 if unknown). Every
 // block of a launch waits at barriers for its peers' blocks, so the blocks that share a device must all be resident.
-uint32_t IpcResidentBlocks(HcclDataType dt, HcclReduceOp op, bool rhd, uint32_t threads);
+uint32_t IpcResidentBlocks(HcclDataType dt, HcclReduceOp op, bool rhd, bool ll, uint32_t threads);
 
 // Writes back and invalidates every XCD's L2 at system scope (one maintenance block per CU); synchronous on `stream`.
 HcclResult ScrubL2(hipStream_t stream);
@@ -209,14 +211,26 @@ struct IpcState {
     uint32_t ranksOnDevice = 1;    // rank mode: the most ranks that share one device (by PCI bus id), same on all ranks
     bool cachedStaging = false;    // HCCL_AMD_IPC_STAGING_CACHED=1 at set-up (diagnostics): barriers keep full fences
     uint64_t* trace = nullptr;     // HCCL_AMD_IPC_TRACE=1 at set-up: [kIpcMaxRanks][kIpcMaxBlocks][kIpcTraceSlots]
+    void* llUnpack = nullptr;      // own unpack area of the LL path (cached, kIpcLlUnpackBytes)
 };
 
 constexpr uint32_t kIpcBlocks = 128;     // workgroups per rank and launch in a loopback world (cap)
 constexpr uint32_t kIpcMaxBlocks = 512;  // flags are sized for this many (HcclAmdCommSetIpcBlocks)
 uint32_t DefaultIpcBlocks(uint64_t bytes);  // workgroups per launch when the communicator sets none (ipc.cc)
+uint32_t LlIpcBlocks(uint32_t n, uint64_t bytes);  // the same for a launch in the LL form (ipc.cc)
 constexpr size_t kIpcStatusBytes = 32;  // status words (IpcArgs::status)
 constexpr int kIpcEpochWord = 4;
 constexpr int kIpcDoneWord = 5;
+constexpr int kIpcLlSeqWord = 6;  // LL launches so far (each advances it by one; the flag of launch s is s + 1)
+// Flag words of a rank: [kIpcMaxBlocks][kIpcMaxRanks], at the start of its flag allocation.
+constexpr uint64_t kIpcFlagBytes = uint64_t(kIpcMaxBlocks) * kIpcMaxRanks * sizeof(uint32_t);
+// LL area (HCCL_AMD_IPC_LL_BYTES): behind the flags in the same uncached allocation (one IPC handle), two parities of
+// kIpcMaxRanks source slots; a slot holds a call's input as 8-byte words {4 data bytes, 32-bit flag}, so twice the
+// bytes of the largest LL call. The unpack area (own, cached) holds the n operands in the fold's slot layout.
+constexpr uint64_t kIpcLlMaxBytes = 64ull << 10;
+constexpr uint64_t kIpcLlSlotBytes = 2 * kIpcLlMaxBytes;
+constexpr uint64_t kIpcLlParityBytes = uint64_t(kIpcMaxRanks) * kIpcLlSlotBytes;
+constexpr uint64_t kIpcLlUnpackBytes = uint64_t(kIpcMaxRanks) * (kIpcLlMaxBytes + 256);
 // The staging allocation of a rank (slot, result and two alternate areas) stays below 2 GiB: hipIpcOpenMemHandle never
 // returned for a 2 GiB allocation on this stack (IpcSetup). The area size is CommConfig::ipcStagingBytes.
 constexpr uint64_t kIpcStagingMaxBytes = 2047ull << 20;

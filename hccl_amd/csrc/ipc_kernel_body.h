@@ -156,7 +156,9 @@ __device__ __forceinline__ void EndLaunch(const IpcArgs& a, uint32_t arrivedBefo
 {
     if (threadIdx.x == 0 && arrivedBefore + 1 == gridDim.x * gridDim.y) {
         __hip_atomic_store(a.status + kIpcDoneWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(a.status + kIpcEpochWord, a.epochSpan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // an LL launch has no barrier epochs; it advances the LL sequence instead (LlOneShot)
+        __hip_atomic_fetch_add(a.status + (a.ll != 0 ? kIpcLlSeqWord : kIpcEpochWord), a.ll != 0 ? 1u : a.epochSpan,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -507,6 +509,158 @@ __device__ __forceinline__ void FoldRange(const IpcArgs& a, uint32_t me, uint64_
     }
 }
 
+// The LL word w of source rank q in rank c's LL area for parity p: 8 bytes {data bytes 4w .. 4w+3, flag}.
+__device__ __forceinline__ uint64_t* LlWord(const IpcArgs& a, uint32_t c, uint32_t p, uint32_t q, uint64_t w)
+{
+    char* area = reinterpret_cast<char*>(a.flags[c]) + kIpcFlagBytes;
+    return reinterpret_cast<uint64_t*>(area + p * kIpcLlParityBytes + q * kIpcLlSlotBytes) + w;
+}
+
+// Bytes 4w .. 4w+3 of a buffer of `bytes` bytes, little-endian in a word (zeros past the end; a base that is not
+// 4-byte aligned reads bytewise).
+__device__ __forceinline__ uint32_t LoadWord(const uint8_t* b, uint64_t bytes, uint64_t w)
+{
+    const uint64_t o = 4 * w;
+    if ((reinterpret_cast<uintptr_t>(b) & 3u) == 0 && o + 4 <= bytes) return *reinterpret_cast<const uint32_t*>(b + o);
+    uint32_t v = 0;
+    for (uint32_t i = 0; i < 4 && o + i < bytes; ++i) v |= uint32_t(b[o + i]) << (8 * i);
+    return v;
+}
+
+// The one-shot AllReduce (kIpcAllReduceOneShot, its own order or kIpcRhd) in the LL form (IpcArgs::ll; calls of at most
+// kIpcLlMaxBytes, one round, windows of BlockWindow). Each block pushes its window of this rank's input to every peer's
+// LL slot `me` as 8-byte words {4 data bytes, flag}, one atomic store each, so a word's data is visible exactly when its
+// flag is: no drain, release or separate flag store, and no barrier. It then polls its window of every peer's slot
+// in its own LL area until the flags equal this launch's, unpacks the data into its own cached unpack area (the fold's
+// slot layout) and folds exactly as the staged one-shot does (FoldRange), so the bits are the same.
+// Flags and reuse: launch s (the device's LL sequence word, identical on every rank: every rank makes the same LL
+// calls) writes parity s & 1 with flag s + 1. Rank i writes launch s + 2 into peer p's area only after its launch s + 1
+// has received p's words of s + 1, which p pushed from a launch that its stream started after its launch s had ended,
+// so p has finished reading parity s & 1 by then. A stale word in the polled range carries an older flag of the same
+// parity: equal to the current one only after 2^32 LL launches.
+template <class E, int OP, bool kRhd>
+__device__ __forceinline__ void LlOneShot(const IpcArgs& a, uint32_t me)
+{
+    using S = typename E::S;
+    const uint32_t n = a.n;
+    Stamp(a, me, kTrEntry);
+    const uint32_t seq = __hip_atomic_load(a.status + kIpcLlSeqWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t arrivedBefore = Arrive(a, seq);
+    const uint32_t par = seq & 1u, flag = seq + 1u;
+    const Range r = BlockWindow(a, a.total);
+    const uint64_t bytes = a.total * sizeof(S);
+    // words [wlo, whi) of the window; an empty window (a block past the end) has none, so the partial last word is
+    // the last non-empty window's alone
+    const uint64_t wlo = r.lo * sizeof(S) / 4, whi = r.hi > r.lo ? (r.hi * sizeof(S) + 3) / 4 : wlo, nw = whi - wlo;
+    const uint8_t* in = static_cast<const uint8_t*>(a.in[me]);
+    // kLlBatch words per thread in flight at once: the first look at a batch costs one memory latency, not one per word
+    constexpr uint32_t kLlBatch = 8;
+    // push: each word of the window, loaded once, to every peer's slot `me`
+    for (uint64_t base = wlo + threadIdx.x; base < whi; base += uint64_t(kLlBatch) * blockDim.x) {
+        uint32_t d[kLlBatch];
+#pragma unroll
+        for (uint32_t k = 0; k < kLlBatch; ++k) {
+            const uint64_t w = base + uint64_t(k) * blockDim.x;
+            if (w < whi) d[k] = LoadWord(in, bytes, w);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kLlBatch; ++k) {
+            const uint64_t w = base + uint64_t(k) * blockDim.x;
+            if (w >= whi) continue;
+            const uint64_t v = uint64_t(d[k]) | (uint64_t(flag) << 32);
+            for (uint32_t j = 1; j < n; ++j) {
+                __hip_atomic_store(LlWord(a, (me + j) % n, par, me, w), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
+    Stamp(a, me, kTrPhase0);
+    // pull: every peer's words of this window, once their flag is this launch's, into the unpack slots
+    uint32_t* unpack = static_cast<uint32_t*>(a.llUnpack[me]);
+    const uint64_t slotWords = a.piece * sizeof(S) / 4;  // piece is a multiple of 16 B
+    uint32_t polls = 0;
+    bool cut = false;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t items = uint64_t(n - 1) * nw;
+    for (uint64_t base = threadIdx.x; base < items && !cut; base += uint64_t(kLlBatch) * blockDim.x) {
+        uint64_t v[kLlBatch];
+        const uint64_t* src[kLlBatch];
+        uint32_t dst[kLlBatch];
+        uint32_t pending = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kLlBatch; ++k) {
+            const uint64_t i = base + uint64_t(k) * blockDim.x;
+            src[k] = nullptr;
+            if (i < items) {
+                const uint32_t q = (me + 1 + static_cast<uint32_t>(i / nw)) % n;
+                const uint64_t w = wlo + i % nw;
+                src[k] = LlWord(a, me, par, q, w);
+                dst[k] = static_cast<uint32_t>(q * slotWords + w);
+                pending |= 1u << k;
+            }
+        }
+        // every pending word of the batch is (re)loaded in one round, so a round costs one memory latency however
+        // many of the batch's words are still on their way
+        for (;;) {
+#pragma unroll
+            for (uint32_t k = 0; k < kLlBatch; ++k) {
+                if (pending & (1u << k)) v[k] = __hip_atomic_load(src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kLlBatch; ++k) {
+                if ((pending & (1u << k)) && static_cast<uint32_t>(v[k] >> 32) == flag) {
+                    unpack[dst[k]] = static_cast<uint32_t>(v[k]);
+                    pending &= ~(1u << k);
+                }
+            }
+            if (pending == 0) break;
+            ++polls;
+            if ((polls & 63u) == 0) {
+                if ((__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 1u) != 0) {
+                    cut = true;
+                    break;
+                }
+                if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeoutTicks) {
+                    __hip_atomic_fetch_or(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(a.failHost, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    cut = true;
+                    break;
+                }
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __shared__ uint32_t failed;
+    if (threadIdx.x == 0) failed = 0;
+    __syncthreads();
+    if (cut) failed = 1;
+    __syncthreads();  // the unpacked words are the block's own stores: visible to its waves after the barrier
+    Stamp(a, me, kTrBarrier1);
+    if (failed == 0) {
+        const S* own = static_cast<const S*>(a.in[me]);
+        S* out = static_cast<S*>(a.out[me]);
+        FoldRange<E, OP, kRhd>(a, me, 0, own, reinterpret_cast<const S*>(unpack), [out](uint32_t) { return out; },
+                               1u, r, ChunkVec<S>(a, me));
+    }
+    Stamp(a, me, kTrPhase1);
+    if (a.trace != nullptr) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        Stamp(a, me, kTrExit);
+    }
+    PublishWait(a, polls);
+    EndLaunch(a, arrivedBefore);
+}
+
+// The LL form as a kernel of its own (IpcArgs::ll): its batched polling needs more registers than the staged kernel,
+// whose occupancy it must not lower.
+template <class E, int OP, bool kRhd>
+__global__ __launch_bounds__(kIpcMaxThreads) void k_ipc_ll(IpcArgs a)
+{
+    const uint32_t me = a.me >= 0 ? static_cast<uint32_t>(a.me) : blockIdx.y;
+    // a communicator whose IPC wait ever timed out stays failed (sticky bit): never wait on its peers again
+    if ((__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 1u) != 0) return;
+    LlOneShot<E, OP, kRhd>(a, me);
+}
+
 // kRhd: the kIpcRhd instantiation (one-shot AllReduce only, kind and order fixed at compile time). It is a kernel of
 // its own so that the RHD tree's register use never lowers the occupancy of the others: a loopback world needs every
 // rank's blocks resident at once.
@@ -622,9 +776,22 @@ __global__ __launch_bounds__(kIpcMaxThreads) void k_ipc_collective(IpcArgs a)
     EndLaunch(a, arrivedBefore);
 }
 
+template <class E, bool kRhd>
+hipError_t LaunchIpcLl(int op, const IpcArgs& a, dim3 grid, hipStream_t s)
+{
+    switch (op) {
+        case R_SUM: hipLaunchKernelGGL((k_ipc_ll<E, R_SUM, kRhd>), grid, dim3(a.threads), 0, s, a); break;
+        case R_PROD: hipLaunchKernelGGL((k_ipc_ll<E, R_PROD, kRhd>), grid, dim3(a.threads), 0, s, a); break;
+        case R_MAX: hipLaunchKernelGGL((k_ipc_ll<E, R_MAX, kRhd>), grid, dim3(a.threads), 0, s, a); break;
+        default: hipLaunchKernelGGL((k_ipc_ll<E, R_MIN, kRhd>), grid, dim3(a.threads), 0, s, a); break;
+    }
+    return hipGetLastError();
+}
+
 template <class E>
 hipError_t LaunchIpcT(int op, const IpcArgs& a, dim3 grid, hipStream_t s)
 {
+    if (a.ll != 0) return a.order == kIpcRhd ? LaunchIpcLl<E, true>(op, a, grid, s) : LaunchIpcLl<E, false>(op, a, grid, s);
     if (a.order == kIpcRhd) {
         switch (op) {
             case R_SUM: hipLaunchKernelGGL((k_ipc_collective<E, R_SUM, true>), grid, dim3(a.threads), 0, s, a); break;
@@ -643,9 +810,21 @@ hipError_t LaunchIpcT(int op, const IpcArgs& a, dim3 grid, hipStream_t s)
     return hipGetLastError();
 }
 
-template <class E>
-const void* IpcKernelT(int op, bool rhd)
+template <class E, bool kRhd>
+const void* IpcLlKernelT(int op)
 {
+    switch (op) {
+        case R_SUM: return reinterpret_cast<const void*>(&k_ipc_ll<E, R_SUM, kRhd>);
+        case R_PROD: return reinterpret_cast<const void*>(&k_ipc_ll<E, R_PROD, kRhd>);
+        case R_MAX: return reinterpret_cast<const void*>(&k_ipc_ll<E, R_MAX, kRhd>);
+        default: return reinterpret_cast<const void*>(&k_ipc_ll<E, R_MIN, kRhd>);
+    }
+}
+
+template <class E>
+const void* IpcKernelT(int op, bool rhd, bool ll)
+{
+    if (ll) return rhd ? IpcLlKernelT<E, true>(op) : IpcLlKernelT<E, false>(op);
     if (rhd) {
         switch (op) {
             case R_SUM: return reinterpret_cast<const void*>(&k_ipc_collective<E, R_SUM, true>);
@@ -670,6 +849,6 @@ const void* IpcKernelT(int op, bool rhd)
     {                                                                                                            \
         return LaunchIpcT<__VA_ARGS__>(op, a, grid, s);                                                              \
     }                                                                                                            \
-    const void* IpcKernel_##NAME(int op, bool rhd) { return IpcKernelT<__VA_ARGS__>(op, rhd); }
+    const void* IpcKernel_##NAME(int op, bool rhd, bool ll) { return IpcKernelT<__VA_ARGS__>(op, rhd, ll); }
 
 }  // namespace hccl_amd

@@ -40,26 +40,26 @@ HcclResult ScrubL2(hipStream_t stream)
     return HCCL_SUCCESS;
 }
 
-uint32_t IpcResidentBlocks(HcclDataType dt, HcclReduceOp op, bool rhd, uint32_t threads)
+uint32_t IpcResidentBlocks(HcclDataType dt, HcclReduceOp op, bool rhd, bool ll, uint32_t threads)
 {
     // per process and (dtype, op, kind of kernel, block size); one device model per node (0 = not yet asked)
-    static std::atomic<uint32_t> cache[32][4][2][2];
+    static std::atomic<uint32_t> cache[32][4][2][2][2];
     const uint32_t di = static_cast<uint32_t>(dt), oi = static_cast<uint32_t>(op), ti = threads > kIpcBlock ? 1 : 0;
     if (di < 32 && oi < 4) {
-        const uint32_t v = cache[di][oi][rhd ? 1 : 0][ti].load(std::memory_order_relaxed);
+        const uint32_t v = cache[di][oi][rhd ? 1 : 0][ll ? 1 : 0][ti].load(std::memory_order_relaxed);
         if (v != 0) return v;
     }
     const void* k = nullptr;
     switch (dt) {
-        case HCCL_DATA_TYPE_INT8: k = IpcKernel_Int8(op, rhd); break;
-        case HCCL_DATA_TYPE_INT16: k = IpcKernel_Int16(op, rhd); break;
-        case HCCL_DATA_TYPE_INT32: k = IpcKernel_Int32(op, rhd); break;
-        case HCCL_DATA_TYPE_INT64: k = IpcKernel_Int64(op, rhd); break;
-        case HCCL_DATA_TYPE_UINT64: k = IpcKernel_Uint64(op, rhd); break;
-        case HCCL_DATA_TYPE_FP16: k = IpcKernel_Fp16(op, rhd); break;
-        case HCCL_DATA_TYPE_BFP16: k = IpcKernel_Bf16(op, rhd); break;
-        case HCCL_DATA_TYPE_FP32: k = IpcKernel_Fp32(op, rhd); break;
-        case HCCL_DATA_TYPE_FP64: k = IpcKernel_Fp64(op, rhd); break;
+        case HCCL_DATA_TYPE_INT8: k = IpcKernel_Int8(op, rhd, ll); break;
+        case HCCL_DATA_TYPE_INT16: k = IpcKernel_Int16(op, rhd, ll); break;
+        case HCCL_DATA_TYPE_INT32: k = IpcKernel_Int32(op, rhd, ll); break;
+        case HCCL_DATA_TYPE_INT64: k = IpcKernel_Int64(op, rhd, ll); break;
+        case HCCL_DATA_TYPE_UINT64: k = IpcKernel_Uint64(op, rhd, ll); break;
+        case HCCL_DATA_TYPE_FP16: k = IpcKernel_Fp16(op, rhd, ll); break;
+        case HCCL_DATA_TYPE_BFP16: k = IpcKernel_Bf16(op, rhd, ll); break;
+        case HCCL_DATA_TYPE_FP32: k = IpcKernel_Fp32(op, rhd, ll); break;
+        case HCCL_DATA_TYPE_FP64: k = IpcKernel_Fp64(op, rhd, ll); break;
         default: return 0;
     }
     int perCu = 0, cus = 0, dev = 0;
@@ -78,7 +78,7 @@ uint32_t IpcResidentBlocks(HcclDataType dt, HcclReduceOp op, bool rhd, uint32_t 
         return 0;
     }
     const uint32_t v = static_cast<uint32_t>(perCu) * static_cast<uint32_t>(cus);
-    if (di < 32 && oi < 4) cache[di][oi][rhd ? 1 : 0][ti].store(v, std::memory_order_relaxed);
+    if (di < 32 && oi < 4) cache[di][oi][rhd ? 1 : 0][ll ? 1 : 0][ti].store(v, std::memory_order_relaxed);
     return v;
 }
 

@@ -234,7 +234,10 @@ typedef enum {
     HCCL_AMD_CFG_IPC_L2_SCRUB = 15,        /* HCCL_AMD_IPC_L2_SCRUB: L2 maintenance at the IPC set-up (default 1) */
     HCCL_AMD_CFG_FOLD_TIMING = 16,         /* HCCL_AMD_FOLD_TIMING: time the executor's folds (diagnostics; calls run
                                               eagerly, HcclAmdCommFoldTiming reads the last one) */
-    HCCL_AMD_CFG_COUNT = 17
+    HCCL_AMD_CFG_IPC_LL_BYTES = 17,        /* (=) HCCL_AMD_IPC_LL_BYTES, 0..65536 (default 65536): one-shot
+                                              AllReduces of at most this many bytes per rank run in the LL form (data
+                                              and flag in one 8-byte store, no barrier; same bits); 0 = off */
+    HCCL_AMD_CFG_COUNT = 18
 } HcclAmdConfigKey;
 extern HcclResult HcclAmdCommSetConfig(HcclComm comm, int32_t key, int64_t value);
 extern HcclResult HcclAmdCommGetConfig(HcclComm comm, int32_t key, int64_t* value);
@@ -278,11 +281,16 @@ extern HcclResult HcclAmdCommCompileStats(HcclComm comm, uint64_t* hits, uint64_
  * (default 16, least recently used evicted; 0 = every call eager). */
 extern HcclResult HcclAmdCommGraphStats(HcclComm comm, uint64_t* launches, uint64_t* captures);
 
-/* Status of the IPC path of comm (synchronous read). Bit 0: a cross-rank barrier wait exceeded HCCL_AMD_IPC_TIMEOUT_MS
- * (default 60000) — the results of that and every later IPC AllReduce on comm are invalid (sticky: the communicator is
- * failed, as after an asynchronous error). Bits 8-15: bit length of the longest barrier wait of the last IPC
- * AllReduce, in polls (diagnostic; 0 = no block ever waited). */
+/* Status of the IPC path of comm (synchronous read). Bit 0: a cross-rank wait exceeded the communicator's bound
+ * (HCCL_AMD_CFG_IPC_TIMEOUT_MS: HCCL_AMD_IPC_TIMEOUT_MS, else HCCL_EXEC_TIMEOUT's AIV rule, default 1091 s) — the
+ * results of that and every later IPC collective on comm are invalid (sticky: the communicator is failed, as after an
+ * asynchronous error). Bits 8-15: bit length of the longest wait of the last IPC collective, in polls (diagnostic;
+ * 0 = no block ever waited). */
 extern HcclResult HcclAmdCommIpcStatus(HcclComm comm, uint32_t* status);
+
+/* One-sided launches of comm that ran in the LL form so far (HCCL_AMD_CFG_IPC_LL_BYTES; synchronous read of the
+ * device's LL sequence word; in a loopback world the launches count on rank 0's communicator, which issues them). */
+extern HcclResult HcclAmdCommIpcLlLaunches(HcclComm comm, uint32_t* launches);
 
 /* Phase timeline of the one-sided kernel (diagnostics). With HCCL_AMD_IPC_TRACE=1 set when comm makes its first IPC
  * call, every launch stamps, per rank and workgroup, 8 s_memrealtime values (100 MHz) of its last staging round:

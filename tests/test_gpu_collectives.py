@@ -8,6 +8,7 @@ schedules, stream/event dependencies, reduce kernels — is the code the RCCL pa
 Every output is compared bit-for-bit with (a) the CPU oracle replaying the same schedule IR and (b) the closed-form
 association order of the reference template (tests/sched_ref.py).
 """
+import itertools
 import os
 import threading
 
@@ -254,16 +255,56 @@ def test_ownership_orders_follow_executor_loops(monkeypatch, op_type, algo, n, c
         root = 1
         in_count = count * n if op_type == RS else count
         xs = [O.random_operands(O.FP32, in_count, seed=700 + r, edge=False) for r in range(n)]
-        used, outs = collective(comms, op_type, algo, O.FP32, O.SUM, xs, count, root=root)
+        run = {"tensors": True}
+        used, outs = collective(comms, op_type, algo, O.FP32, O.SUM, xs, count, root=root, keep=run)
         assert used == algo
         if algo == 7:
             assert ipc_status(comms[0]) & 1 == 0
         want = R.expected(op_type, used, O.FP32, O.SUM, xs, count, root=root)
+        per_rank = [int(np.count_nonzero(outs[q].view(np.uint32) != want[q].view(np.uint32)))
+                    if not (op_type == RED and q != root) else 0 for q in range(n)]
+        diag = None
+        if any(per_rank) and op_type != RED and algo != 7:
+            from tests._stale_diag import _d2h, diagnose  # everything the failing run left behind, in the message
+            diag = diagnose(comms, op_type, algo, xs, count, root, want, outs, run["sends"], run["recvs"])
+            # the executor staging of each wrong rank as memory holds it now, at the first wrong elements and where the
+            # program's receives landed (a later fold or copy would have read these words)
+            diag["staging_now"] = {}
+            for q in range(n):
+                if not per_rank[q]:
+                    continue
+                bad = np.nonzero(outs[q].view(np.uint32) != want[q].view(np.uint32))[0]
+                ptr, nbytes = comms[q].scratch()
+                words = _d2h(ptr, nbytes).view(np.float32)
+                arr, nops, _, _ = H.build_schedule(op_type, algo, n, q, count, O.FP32, root, 0)
+                recv_offs = sorted({int(arr[i].dstOff) for i in range(nops)
+                                    if arr[i].kind == H.IrKind.RECV and arr[i].dstBuf == 2})
+                e = int(bad[0])
+                starts = [int(bad[0])] + [int(bad[i]) for i in range(1, len(bad)) if bad[i] != bad[i - 1] + 1]
+                runs = []
+                for st in starts[:24]:
+                    ln = 1
+                    while st + ln in set(bad.tolist()):
+                        ln += 1
+                    # the operands whose float32 sum (rank order) is what the run's first element got
+                    ops_ = [np.float32(x[q * count + st] if op_type == RS else x[st]) for x in xs]
+                    fits = [list(c) for k in range(1, n + 1) for c in itertools.combinations(range(n), k)
+                            if np.float32(sum(np.float32(ops_[i]) for i in c)) == outs[q][st]]
+                    runs.append((st, ln, fits[:3]))
+                diag.setdefault("bad_runs", {})[q] = runs
+                diag["staging_now"][q] = {"at_bad": [float(words[int(b)]) for b in bad[:3]],
+                                          "recv_offsets": recv_offs,
+                                          "at_recv_plus_bad": {o: float(words[o + e]) for o in recv_offs
+                                                               if o + e < len(words)},
+                                          "operands_at_bad": [float(x[e]) for x in xs]}
         for r in range(n):
             if op_type == RED and r != root:
                 assert not outs[r].any(), "non-root recvBuf written"
                 continue
-            assert O.equal_bits(O.FP32, outs[r], want[r]), r
+            bad = np.nonzero(outs[r].view(np.uint32) != want[r].view(np.uint32))[0]
+            assert not len(bad), (f"rank {r}: {len(bad)} bad, per rank {per_rank}, first {bad[:6].tolist()} last "
+                                  f"{bad[-3:].tolist()}; got {outs[r][bad[:3]]!r} want {want[r][bad[:3]]!r}; "
+                                  f"diagnosis {diag}")
     finally:
         torch.cuda.synchronize()
         for c in comms:

@@ -14,7 +14,8 @@ import torch
 import hccl_amd as H
 from oracle import oracle as O
 from tests import sched_ref as R
-from tests.test_gpu_collectives import AR, collective, ipc_status, oracle_replay
+from tests.test_gpu_collectives import AR, collective, ipc_status, oracle_replay, run_ranks
+from tests._util import to_device, to_host
 
 pytestmark = pytest.mark.gpu
 
@@ -123,10 +124,12 @@ def test_config_round_trip_and_ranges():
         assert c.get_config(H.Config.SMALL_IPC_BYTES) == 0  # the suite's environment (conftest)
         assert c.get_config(H.Config.GRAPH_CACHE) == 16
         assert c.get_config(H.Config.IPC_THREADS) == 256
+        assert c.get_config(H.Config.IPC_LL_BYTES) == 65536  # the LL form's default
         c.set_config(H.Config.IPC_THREADS, 512)
         assert c.get_config(H.Config.IPC_THREADS) == 512
         for key, bad in ((H.Config.IPC_THREADS, 300), (H.Config.IPC_LIGHT_FENCE, 2), (H.Config.IPC_STAGING_MIB, 8),
-                         (H.Config.AIV_CORE_LIMIT, 0), (99, 1)):
+                         (H.Config.AIV_CORE_LIMIT, 0), (H.Config.IPC_LL_BYTES, 65537), (H.Config.IPC_LL_BYTES, -1),
+                         (99, 1)):
             with pytest.raises(H.HcclError) as e:
                 c.set_config(key, bad)
             assert e.value.code == H.HcclResult.HCCL_E_PARA
@@ -177,6 +180,156 @@ def test_random_small_allreduce_matches_the_schedule(small_worlds, case):
     xs = [O.random_operands(dtype, count, seed=12000 + 17 * case[0] + r) for r in range(n)]
     used, outs = collective(comms, AR, algo, dtype, op, xs, count, inplace=inplace)
     assert used == (H.Algo.IPC_RHD if algo == H.Algo.RHD else H.Algo.IPC), H.Algo(used).name
+    want = oracle_replay(AR, algo, n, count, dtype, op, xs, 0, 0)
+    for r in range(n):
+        assert O.equal_bits(dtype, outs[r], want[r]), (case, r)
+
+
+# ---------------------------------------------------------------------------------------------- the LL form (r05)
+
+LL = 64 << 10
+
+
+def ll_world(n, ll=LL):
+    comms = world(n)
+    for c in comms:
+        c.set_config(H.Config.IPC_LL_BYTES, ll)
+    return comms
+
+
+def _itemsize(dtype):
+    return np.dtype(O.NP_STORAGE[dtype]).itemsize
+
+
+@pytest.mark.parametrize("dtype,op,count", [
+    (O.FP16, O.SUM, 512),           # 1 KiB, C5's smallest point
+    (O.INT8, O.MIN, 1),             # one byte: a partial LL word
+    (O.INT8, O.SUM, 3),
+    (O.INT8, O.MAX, 4101),          # windows whose last word is partial
+    (O.FP16, O.SUM, 32767),         # odd fp16 count, just under 64 KiB
+    (O.BFP16, O.MAX, 4097),
+    (O.FP32, O.SUM, 16384),         # exactly 64 KiB: the largest LL call
+    (O.FP32, O.SUM, 16385),         # 4 B over: the staged one-shot
+    (O.FP64, O.SUM, 8191),          # 8-byte elements span two LL words
+    (O.INT64, O.MAX, 3),
+    (O.UINT64, O.SUM, 5),
+    (O.INT32, O.PROD, 999),
+], ids=lambda v: str(v))
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_ll_allreduce_has_the_schedule_bits(n, dtype, op, count):
+    """HCCL_AMD_IPC_LL_BYTES: a one-shot AllReduce of at most that many bytes runs in the LL form (data and flag in
+    one 8-byte store, no barrier; ipc_kernel_body.h LlOneShot) and gives the auto schedule's bits; one byte over, the
+    staged one-shot runs. HcclAmdCommIpcLlLaunches counts the LL launches."""
+    comms = ll_world(n)
+    try:
+        xs = [O.random_operands(dtype, count, seed=5200 + 7 * n + r) for r in range(n)]
+        used, outs = collective(comms, AR, H.Algo.AUTO, dtype, op, xs, count)
+        assert used == H.Algo.IPC, H.Algo(used).name
+        assert comms[0].ipc_ll_launches() == (1 if count * _itemsize(dtype) <= LL else 0)
+        assert ipc_status(comms[0]) & 1 == 0
+        want = oracle_replay(AR, H.Algo.AUTO, n, count, dtype, op, xs, 0, 0)
+        for r in range(n):
+            assert O.equal_bits(dtype, outs[r], want[r]), r
+    finally:
+        destroy(comms)
+
+
+@pytest.mark.parametrize("count", [1, 512, 4099, 32768])
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_ll_rhd_allreduce_has_rhd_bits(n, count):
+    """RHD's order from the LL form (IPC_RHD, random fp16 where the order decides the bits)."""
+    comms = ll_world(n)
+    try:
+        xs = [O.random_operands(O.FP16, count, seed=5300 + 7 * n + r, edge=False) for r in range(n)]
+        used, outs = collective(comms, AR, H.Algo.RHD, O.FP16, O.SUM, xs, count)
+        assert used == H.Algo.IPC_RHD, H.Algo(used).name
+        assert comms[0].ipc_ll_launches() == 1
+        want = oracle_replay(AR, H.Algo.RHD, n, count, O.FP16, O.SUM, xs, 0, 0)
+        for r in range(n):
+            assert O.equal_bits(O.FP16, outs[r], want[r]), r
+    finally:
+        destroy(comms)
+
+
+def test_ll_calls_back_to_back_with_staged_calls_between():
+    """40 AllReduces per rank issued without a host wait: LL calls (both parities, many times over) with a staged
+    one-shot (256 KiB) and a two-shot-sized call (4 MiB, the auto family's two-shot) every few calls, fresh random
+    inputs per call, each into its own output. Every result has its schedule's bits: the LL flags and parities and
+    the staged barrier epochs advance independently and never confuse one call with another."""
+    n = 4
+    comms = ll_world(n)
+    try:
+        sizes = []
+        for k in range(40):
+            sizes.append((4 << 20) // 4 if k % 13 == 12 else (256 << 10) // 4 if k % 5 == 4 else 1 + 97 * k)
+        xs = [[O.random_operands(O.FP32, cnt, seed=5400 + 31 * k + r, edge=False) for r in range(n)]
+              for k, cnt in enumerate(sizes)]
+        sends = [[to_device(O.FP32, xs[k][r]) for r in range(n)] for k in range(len(sizes))]
+        recvs = [[torch.empty_like(sends[k][r]) for r in range(n)] for k in range(len(sizes))]
+        streams = [torch.cuda.Stream() for _ in range(n)]
+        for c in comms:
+            c.set_algo(H.Algo.AUTO)
+        torch.cuda.synchronize()
+
+        def body(r):
+            for k in range(len(sizes)):
+                comms[r].all_reduce(sends[k][r], recvs[k][r], O.SUM, streams[r])
+
+        run_ranks(n, body)
+        torch.cuda.synchronize()
+        assert ipc_status(comms[0]) & 1 == 0
+        n_ll = sum(1 for cnt in sizes if cnt * 4 <= LL)
+        assert comms[0].ipc_ll_launches() == n_ll
+        for k, cnt in enumerate(sizes):
+            want = oracle_replay(AR, H.Algo.AUTO, n, cnt, O.FP32, O.SUM, xs[k], 0, 0)
+            for r in range(n):
+                assert O.equal_bits(O.FP32, to_host(O.FP32, recvs[k][r]), want[r]), (k, cnt, r)
+    finally:
+        destroy(comms)
+
+
+def _random_ll_cases(k):
+    rng = np.random.default_rng(20261019)
+    dts = [O.INT8, O.INT16, O.INT32, O.INT64, O.UINT64, O.FP16, O.BFP16, O.FP32, O.FP64]
+    out = []
+    for i in range(k):
+        n = int(rng.choice([2, 3, 4, 5, 6, 8]))
+        algo = int(rng.choice([H.Algo.AUTO, H.Algo.RHD])) if n in (2, 4, 8) else int(H.Algo.AUTO)
+        dtype = int(rng.choice(dts))
+        op = int(rng.choice(O.OPS))
+        if op == O.PROD and dtype in (O.INT16, O.BFP16):
+            op = O.MAX
+        count = int(rng.integers(1, LL // _itemsize(dtype) + 1))
+        out.append((i, n, algo, dtype, op, count, bool(rng.integers(2))))
+    return out
+
+
+@pytest.fixture(scope="module")
+def ll_worlds():
+    cache = {}
+
+    def get(n):
+        if n not in cache:
+            cache[n] = ll_world(n)
+        return cache[n]
+
+    yield get
+    torch.cuda.synchronize()
+    for comms in cache.values():
+        for c in comms:
+            c.destroy()
+
+
+@pytest.mark.parametrize("case", _random_ll_cases(120), ids=lambda c: f"ll{c[0]}")
+def test_random_ll_allreduce_matches_the_schedule(ll_worlds, case):
+    """Seeded draws over ranks x family x dtype x op x count (1 .. 64 KiB) x in-place, all in the LL form."""
+    _, n, algo, dtype, op, count, inplace = case
+    comms = ll_worlds(n)
+    before = comms[0].ipc_ll_launches()
+    xs = [O.random_operands(dtype, count, seed=13000 + 17 * case[0] + r) for r in range(n)]
+    used, outs = collective(comms, AR, algo, dtype, op, xs, count, inplace=inplace)
+    assert used == (H.Algo.IPC_RHD if algo == H.Algo.RHD else H.Algo.IPC), H.Algo(used).name
+    assert comms[0].ipc_ll_launches() == before + 1
     want = oracle_replay(AR, algo, n, count, dtype, op, xs, 0, 0)
     for r in range(n):
         assert O.equal_bits(dtype, outs[r], want[r]), (case, r)

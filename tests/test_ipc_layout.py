@@ -205,7 +205,7 @@ def check_allgather(n, count, es, vec, blocks):
 
 def default_blocks(nbytes):
     """ipc.cc DefaultIpcBlocks: workgroups per launch by the call's bytes."""
-    for limit, b in ((512 << 10, 16), (2 << 20, 32), (32 << 20, 64), (64 << 20, 128)):
+    for limit, b in ((64 << 10, 4), (512 << 10, 16), (2 << 20, 32), (32 << 20, 64), (64 << 20, 128)):
         if nbytes <= limit:
             return b
     return 256

@@ -3,7 +3,8 @@ the one-GPU box: n processes share the GPU over the IPC-only communicator (HcclA
 an xGMI measurement; it shows the launch/barrier cost per block count at small sizes and the HBM-side effect at large
 ones. Run as:
   python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 \
-      tools/sweep_ipc_blocks.py > gpurun_out/sweep_ipc_blocks.jsonl
+      tools/probes/sweep_ipc_blocks.py > gpurun_out/sweep_ipc_blocks.jsonl
+(SWEEP_BLOCKS / SWEEP_SIZES: comma lists overriding the block counts and byte sizes.)
 """
 import json
 import os
@@ -16,7 +17,7 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import hccl_amd as H  # noqa: E402
 
-BLOCKS = (16, 32, 64, 128, 256)
+BLOCKS = tuple(int(x) for x in os.environ.get("SWEEP_BLOCKS", "").split(",") if x) or (16, 32, 64, 128, 256)
 SIZES = tuple(int(x) for x in os.environ.get("SWEEP_SIZES", "").split(",") if x) or (
     1 << 10, 1 << 16, 1 << 20, 1 << 24, 1 << 28)
 
