@@ -159,7 +159,7 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     if (p.algo == HCCL_AMD_ALGO_AUTO && NeedStrictOrder(c, opType, dt, op)) {
         p.algo = HCCL_AMD_ALGO_ORDER_PRESERVED;
     }
-    // Small AllReduces take the one-sided kernel (HCCL_AMD_SMALL_IPC_BYTES, default 1 MiB per rank): one launch with
+    // Small collectives take the one-sided kernel (HCCL_AMD_SMALL_IPC_BYTES, default 1 MiB per rank): one launch with
     // one or two cross-rank barriers instead of the transport groups of a schedule, each of which costs a group launch
     // (1 KiB one-shot over RCCL: 29-32 us, an 8-rank RHD: 81.5 us; profiles/r03_host_cost_rccl_selfloop.jsonl,
     // r02_rccl_selfloop_latency.jsonl). The reference runs small data on its vector cores the same way
@@ -167,8 +167,13 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
     // auto family runs in the auto family's order (HCCL_AMD_ALGO_IPC), RHD in RHD's (HCCL_AMD_ALGO_IPC_RHD). Every rank
     // decides alike (count, dtype and the (=) config are equal on every rank); a call the kernel cannot take (no peer
     // mappings, a capture before the set-up) runs the schedule.
-    if (opType == HCCL_AMD_OP_ALLREDUCE && c.transport->HasSendRecv() && !c.ipc.unavailable &&
-        count * es <= c.cfg.smallIpcBytes && (p.algo == HCCL_AMD_ALGO_AUTO || p.algo == HCCL_AMD_ALGO_RHD)) {
+    // ReduceScatter and Reduce take the rule too (r05), in the auto family's order only (the one-sided kernel has no
+    // RHD form of them); the threshold applies to the rank's input (ReduceScatter: n blocks).
+    const bool reducing = opType == HCCL_AMD_OP_ALLREDUCE || opType == HCCL_AMD_OP_REDUCE_SCATTER ||
+                          opType == HCCL_AMD_OP_REDUCE;
+    const uint64_t inBytes = count * es * (opType == HCCL_AMD_OP_REDUCE_SCATTER ? c.nRanks : 1);
+    if (reducing && c.transport->HasSendRecv() && !c.ipc.unavailable && inBytes <= c.cfg.smallIpcBytes &&
+        (p.algo == HCCL_AMD_ALGO_AUTO || (opType == HCCL_AMD_OP_ALLREDUCE && p.algo == HCCL_AMD_ALGO_RHD))) {
         IpcPlan plan{};
         HcclResult r = HCCL_E_NOT_SUPPORT;
         int32_t ran = HCCL_AMD_ALGO_IPC;

@@ -203,9 +203,9 @@ extern HcclResult HcclAmdCommSetIpcBlocks(HcclComm comm, uint32_t blocks);
 /* Pipelining granule (bytes per piece) for subsequent collectives on comm; 0 restores the default. */
 extern HcclResult HcclAmdCommSetPieceBytes(HcclComm comm, uint64_t pieceBytes);
 
-/* Algorithm the last collective on comm executed (HcclAmdAlgo), or -1. An AllReduce that the small-call rule
- * (HCCL_AMD_CFG_SMALL_IPC_BYTES) put on the one-sided kernel reports HCCL_AMD_ALGO_IPC (the auto family's order) or
- * HCCL_AMD_ALGO_IPC_RHD (RHD's order). */
+/* Algorithm the last collective on comm executed (HcclAmdAlgo), or -1. A collective that the small-call rule
+ * (HCCL_AMD_CFG_SMALL_IPC_BYTES) put on the one-sided kernel reports HCCL_AMD_ALGO_IPC (the auto family's order) or,
+ * for an AllReduce asked for RHD, HCCL_AMD_ALGO_IPC_RHD (RHD's order). */
 extern int32_t HcclAmdCommLastAlgo(HcclComm comm);
 
 /* Configuration. A communicator reads the environment once, when it is created (the reference parses its environment
@@ -218,9 +218,10 @@ typedef enum {
     HCCL_AMD_CFG_AIV_CORE_LIMIT = 2,       /* (=) HCCL_AMD_AIV_CORE_LIMIT, 1..4096 (default 48) */
     HCCL_AMD_CFG_SINGLE_STREAM_BYTES = 3,  /* HCCL_AMD_SINGLE_STREAM_BYTES: programs up to this per-rank payload run
                                               on the caller's stream alone (default 1 MiB) */
-    HCCL_AMD_CFG_SMALL_IPC_BYTES = 4,      /* (=) HCCL_AMD_SMALL_IPC_BYTES: an AllReduce of auto or RHD family up to this
-                                              many bytes per rank runs on the one-sided kernel, same bits (default
-                                              1 MiB; 0 = never) */
+    HCCL_AMD_CFG_SMALL_IPC_BYTES = 4,      /* (=) HCCL_AMD_SMALL_IPC_BYTES: an AllReduce of auto or RHD family, or a
+                                              ReduceScatter or Reduce of auto family, with at most this many input
+                                              bytes per rank runs on the one-sided kernel, same bits (default 1 MiB;
+                                              0 = never) */
     HCCL_AMD_CFG_PLAN_CACHE = 5,           /* HCCL_AMD_PLAN_CACHE: compiled-collective cache on (1, default) / off (0) */
     HCCL_AMD_CFG_GRAPH_CACHE = 6,          /* HCCL_AMD_GRAPH_CACHE: executor graphs kept, 0..1024 (default 16) */
     HCCL_AMD_CFG_IPC_LIGHT_FENCE = 7,      /* (=) HCCL_AMD_IPC_LIGHT_FENCE: -1 per mode (default), 0 system, 1 light */

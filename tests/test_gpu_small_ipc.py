@@ -14,7 +14,7 @@ import torch
 import hccl_amd as H
 from oracle import oracle as O
 from tests import sched_ref as R
-from tests.test_gpu_collectives import AR, collective, ipc_status, oracle_replay, run_ranks
+from tests.test_gpu_collectives import AR, RED, RS, collective, ipc_status, oracle_replay, run_ranks
 from tests._util import to_device, to_host
 
 pytestmark = pytest.mark.gpu
@@ -79,7 +79,8 @@ def test_small_rhd_allreduce_runs_ipc_rhd_with_rhd_bits(n, count):
 
 
 def test_threshold_and_switch():
-    """Above the threshold, with the rule off, and for other operations the schedules run as before."""
+    """Above the threshold (a ReduceScatter's whole input counted), with the rule off, and for an explicit family the
+    schedules run as before."""
     n = 4
     comms = world(n, small=64 << 10)
     try:
@@ -88,8 +89,10 @@ def test_threshold_and_switch():
         assert used == R.ALGO_ONESHOT, H.Algo(used).name
         used, _ = collective(comms, AR, H.Algo.AUTO, O.FP32, O.SUM, [x[:1000] for x in xs], 1000)
         assert used == H.Algo.IPC
-        # ReduceScatter is not covered by the rule
+        # ReduceScatter: 4 blocks of 1000 fp32 (16 KB of input) take the rule, 4 of 5000 (80 KB) the schedule
         used, _ = collective(comms, 1, H.Algo.AUTO, O.FP32, O.SUM, [x[:4000] for x in xs], 1000)
+        assert used == H.Algo.IPC, H.Algo(used).name
+        used, _ = collective(comms, 1, H.Algo.AUTO, O.FP32, O.SUM, xs, 5000)
         assert used == R.ALGO_ONESHOT, H.Algo(used).name
         # an explicit family is never rerouted
         used, _ = collective(comms, AR, H.Algo.MESH_TWOSHOT, O.FP32, O.SUM, [x[:1000] for x in xs], 1000)
@@ -333,3 +336,55 @@ def test_random_ll_allreduce_matches_the_schedule(ll_worlds, case):
     want = oracle_replay(AR, algo, n, count, dtype, op, xs, 0, 0)
     for r in range(n):
         assert O.equal_bits(dtype, outs[r], want[r]), (case, r)
+
+
+# ------------------------------------------------------------------ ReduceScatter and Reduce under the rule (r05)
+
+@pytest.mark.parametrize("op_type,n,count,dtype,op", [
+    (RS, 2, 5, O.FP32, O.SUM),
+    (RS, 4, 4099, O.FP16, O.SUM),
+    (RS, 8, 1000, O.BFP16, O.MAX),
+    (RS, 3, 8191, O.INT32, O.PROD),
+    (RS, 4, (1 << 20) // 16, O.FP32, O.SUM),   # exactly 1 MiB of input per rank: the rule's largest call
+    (RED, 2, 5, O.FP32, O.SUM),
+    (RED, 4, 40961, O.FP32, O.SUM),
+    (RED, 8, 3001, O.FP64, O.MIN),
+    (RED, 3, 65537, O.FP16, O.SUM),
+], ids=lambda v: str(v))
+def test_small_reduce_scatter_and_reduce_run_one_sided(op_type, n, count, dtype, op):
+    """The rule takes ReduceScatter and Reduce of the auto family as well (input bytes per rank at most
+    HCCL_AMD_SMALL_IPC_BYTES): one launch of the one-sided kernel in the auto family's order, the auto schedule's bits,
+    and a Reduce leaves the non-root outputs untouched."""
+    comms = world(n)
+    try:
+        root = n - 1
+        in_count = count * n if op_type == RS else count
+        xs = [O.random_operands(dtype, in_count, seed=5600 + 7 * n + r) for r in range(n)]
+        used, outs = collective(comms, op_type, H.Algo.AUTO, dtype, op, xs, count, root=root)
+        assert used == H.Algo.IPC, H.Algo(used).name
+        assert ipc_status(comms[0]) & 1 == 0
+        want = oracle_replay(op_type, H.Algo.AUTO, n, count, dtype, op, xs, root, 0)
+        for r in range(n):
+            if op_type == RED and r != root:
+                assert not outs[r].any(), "non-root recvBuf written"
+                continue
+            assert O.equal_bits(dtype, outs[r], want[r]), r
+    finally:
+        destroy(comms)
+
+
+def test_small_reduce_scatter_threshold_counts_the_whole_input():
+    """A ReduceScatter's input is n blocks: 4 ranks x 65,537 fp32 is 1 MiB + 16 B per rank, over the rule, so the
+    schedule runs; one element fewer per block fits."""
+    n = 4
+    comms = world(n)
+    try:
+        for count, over in (((1 << 20) // 16 + 1, True), ((1 << 20) // 16, False)):
+            xs = [O.random_operands(O.FP32, count * n, seed=5700 + r, edge=False) for r in range(n)]
+            used, outs = collective(comms, RS, H.Algo.AUTO, O.FP32, O.SUM, xs, count)
+            assert (used != H.Algo.IPC) == over, (count, H.Algo(used).name)
+            want = oracle_replay(RS, H.Algo.AUTO, n, count, O.FP32, O.SUM, xs, 0, 0)
+            for r in range(n):
+                assert O.equal_bits(O.FP32, outs[r], want[r]), (count, r)
+    finally:
+        destroy(comms)
