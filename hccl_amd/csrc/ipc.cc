@@ -555,12 +555,16 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
     // The LL form (HCCL_AMD_IPC_LL_BYTES; LlOneShot): a one-shot AllReduce of at most that many bytes per rank (and
     // kIpcLlMaxBytes), one launch of one round. The decision depends only on the call's arguments and the
     // configuration, which every rank shares, so every rank takes the same form.
+    // The ReduceScatter takes it too (equal blocks of `count`, each at most that many bytes): like the one-shot, every
+    // rank receives from every peer in every launch.
     IpcArgs a{};
-    a.ll = (kind == kIpcAllReduceOneShot && opType == HCCL_AMD_OP_ALLREDUCE && plan.geom == kIpcGeomWhole &&
-            loopElems == 0 && count * es <= std::min<uint64_t>(c.cfg.ipcLlBytes, kIpcLlMaxBytes))
+    const bool llKind = (kind == kIpcAllReduceOneShot && opType == HCCL_AMD_OP_ALLREDUCE && plan.geom == kIpcGeomWhole) ||
+                        (kind == kIpcReduceScatter && opType == HCCL_AMD_OP_REDUCE_SCATTER && plan.geom == kIpcGeomBlock);
+    a.ll = (llKind && (loopElems == 0 || count <= loopElems) &&
+            count * es <= std::min<uint64_t>(c.cfg.ipcLlBytes, kIpcLlMaxBytes))
                ? 1u
                : 0u;
-    s.blocks = c.ipcBlocks != 0 ? c.ipcBlocks : a.ll != 0 ? LlIpcBlocks(n, callBytes) : DefaultIpcBlocks(callBytes);
+    s.blocks = c.ipcBlocks != 0 ? c.ipcBlocks : a.ll != 0 ? LlIpcBlocks(n, count * es) : DefaultIpcBlocks(callBytes);
     if (c.transport->SharedDevice() && c.ipcBlocks == 0) s.blocks = std::min(s.blocks, kIpcBlocks);
     // Co-residency: every block waits at barriers for its peers' blocks, so all blocks on this device must be resident
     // at once (a loopback world puts every rank's blocks on it; in rank mode, the ranks whose processes share this

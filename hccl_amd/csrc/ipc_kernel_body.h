@@ -527,8 +527,10 @@ __device__ __forceinline__ uint32_t LoadWord(const uint8_t* b, uint64_t bytes, u
     return v;
 }
 
-// The one-shot AllReduce (kIpcAllReduceOneShot, its own order or kIpcRhd) in the LL form (IpcArgs::ll; calls of at most
-// kIpcLlMaxBytes, one round, windows of BlockWindow). Each block pushes its window of this rank's input to every peer's
+// The one-shot AllReduce (kIpcAllReduceOneShot, its own order or kIpcRhd) and the ReduceScatter (kIpcReduceScatter over
+// equal blocks) in the LL form (IpcArgs::ll; pieces of at most kIpcLlMaxBytes, one round, windows of BlockWindow).
+// Both receive from every peer in every launch, which the reuse argument below needs (a one-shot Reduce's non-roots
+// receive nothing, so it stays staged). Each block pushes its window of this rank's input to every peer's
 // LL slot `me` as 8-byte words {4 data bytes, flag}, one atomic store each, so a word's data is visible exactly when its
 // flag is: no drain, release or separate flag store, and no barrier. It then polls its window of every peer's slot
 // in its own LL area until the flags equal this launch's, unpacks the data into its own cached unpack area (the fold's
@@ -547,29 +549,37 @@ __device__ __forceinline__ void LlOneShot(const IpcArgs& a, uint32_t me)
     const uint32_t seq = __hip_atomic_load(a.status + kIpcLlSeqWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t arrivedBefore = Arrive(a, seq);
     const uint32_t par = seq & 1u, flag = seq + 1u;
-    const Range r = BlockWindow(a, a.total);
-    const uint64_t bytes = a.total * sizeof(S);
+    // Every destination's piece has the same length: the whole input (one-shot AllReduce) or one block of the
+    // ReduceScatter's equal blocks (peer c receives block c, this rank folds block me).
+    const bool perDest = a.kind == kIpcReduceScatter;
+    const uint64_t len = PieceLen(a, me, 0);
+    const Range r = BlockWindow(a, len);
+    const uint64_t bytes = len * sizeof(S);
     // words [wlo, whi) of the window; an empty window (a block past the end) has none, so the partial last word is
     // the last non-empty window's alone
     const uint64_t wlo = r.lo * sizeof(S) / 4, whi = r.hi > r.lo ? (r.hi * sizeof(S) + 3) / 4 : wlo, nw = whi - wlo;
     const uint8_t* in = static_cast<const uint8_t*>(a.in[me]);
+    auto src = [&](uint32_t c) { return in + ChunkStart(a, c) * sizeof(S); };
     // kLlBatch words per thread in flight at once: the first look at a batch costs one memory latency, not one per word
     constexpr uint32_t kLlBatch = 8;
-    // push: each word of the window, loaded once, to every peer's slot `me`
+    // push: each word of the window to every peer's slot `me` (the one-shot's word loaded once for all peers, a
+    // ReduceScatter's from each peer's block)
     for (uint64_t base = wlo + threadIdx.x; base < whi; base += uint64_t(kLlBatch) * blockDim.x) {
         uint32_t d[kLlBatch];
 #pragma unroll
         for (uint32_t k = 0; k < kLlBatch; ++k) {
             const uint64_t w = base + uint64_t(k) * blockDim.x;
-            if (w < whi) d[k] = LoadWord(in, bytes, w);
+            if (w < whi && !perDest) d[k] = LoadWord(src(me), bytes, w);
         }
 #pragma unroll
         for (uint32_t k = 0; k < kLlBatch; ++k) {
             const uint64_t w = base + uint64_t(k) * blockDim.x;
             if (w >= whi) continue;
-            const uint64_t v = uint64_t(d[k]) | (uint64_t(flag) << 32);
             for (uint32_t j = 1; j < n; ++j) {
-                __hip_atomic_store(LlWord(a, (me + j) % n, par, me, w), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                const uint32_t c = (me + j) % n;
+                const uint32_t data = perDest ? LoadWord(src(c), bytes, w) : d[k];
+                __hip_atomic_store(LlWord(a, c, par, me, w), uint64_t(data) | (uint64_t(flag) << 32),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
     }
@@ -636,8 +646,8 @@ __device__ __forceinline__ void LlOneShot(const IpcArgs& a, uint32_t me)
     __syncthreads();  // the unpacked words are the block's own stores: visible to its waves after the barrier
     Stamp(a, me, kTrBarrier1);
     if (failed == 0) {
-        const S* own = static_cast<const S*>(a.in[me]);
-        S* out = static_cast<S*>(a.out[me]);
+        const S* own = static_cast<const S*>(a.in[me]) + ChunkStart(a, me);
+        S* out = static_cast<S*>(a.out[me]) + (perDest ? 0 : ChunkStart(a, me));
         FoldRange<E, OP, kRhd>(a, me, 0, own, reinterpret_cast<const S*>(unpack), [out](uint32_t) { return out; },
                                1u, r, ChunkVec<S>(a, me));
     }

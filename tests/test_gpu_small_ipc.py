@@ -388,3 +388,65 @@ def test_small_reduce_scatter_threshold_counts_the_whole_input():
                 assert O.equal_bits(O.FP32, outs[r], want[r]), (count, r)
     finally:
         destroy(comms)
+
+
+@pytest.mark.parametrize("dtype,op,count", [
+    (O.FP32, O.SUM, 1),
+    (O.INT8, O.MAX, 5),             # blocks whose ends fall inside an LL word
+    (O.FP16, O.SUM, 4097),
+    (O.BFP16, O.MIN, 1023),
+    (O.FP32, O.SUM, 16384),         # 64 KiB blocks: the largest LL ReduceScatter
+    (O.FP32, O.SUM, 16385),         # 4 B over: staged
+    (O.FP64, O.PROD, 777),
+], ids=lambda v: str(v))
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_ll_reduce_scatter_has_the_schedule_bits(n, dtype, op, count):
+    """The ReduceScatter in the LL form (blocks of at most HCCL_AMD_IPC_LL_BYTES): each rank pushes block c to rank c as
+    LL words and folds its own block from every peer's, the auto schedule's bits; one block over, the staged kernel."""
+    comms = ll_world(n)
+    try:
+        xs = [O.random_operands(dtype, count * n, seed=5800 + 7 * n + r) for r in range(n)]
+        used, outs = collective(comms, RS, H.Algo.AUTO, dtype, op, xs, count)
+        assert used == H.Algo.IPC, H.Algo(used).name
+        assert comms[0].ipc_ll_launches() == (1 if count * _itemsize(dtype) <= LL else 0)
+        assert ipc_status(comms[0]) & 1 == 0
+        want = oracle_replay(RS, H.Algo.AUTO, n, count, dtype, op, xs, 0, 0)
+        for r in range(n):
+            assert O.equal_bits(dtype, outs[r], want[r]), r
+    finally:
+        destroy(comms)
+
+
+def test_ll_reduce_scatter_and_allreduce_back_to_back():
+    """30 calls per rank without a host wait, LL ReduceScatters and LL AllReduces in turn on one communicator (they
+    share the LL sequence and both parities), every result exact."""
+    n = 4
+    comms = ll_world(n)
+    try:
+        plan = [(RS if k % 2 else AR, 1 + 211 * k) for k in range(30)]
+        xs = [[O.random_operands(O.FP32, cnt * (n if kind == RS else 1), seed=5900 + 31 * k + r, edge=False)
+               for r in range(n)] for k, (kind, cnt) in enumerate(plan)]
+        sends = [[to_device(O.FP32, xs[k][r]) for r in range(n)] for k in range(len(plan))]
+        recvs = [[torch.empty(cnt, device="cuda") for _ in range(n)] for (_, cnt) in plan]
+        streams = [torch.cuda.Stream() for _ in range(n)]
+        for c in comms:
+            c.set_algo(H.Algo.AUTO)
+        torch.cuda.synchronize()
+
+        def body(r):
+            for k, (kind, _) in enumerate(plan):
+                if kind == RS:
+                    comms[r].reduce_scatter(sends[k][r], recvs[k][r], O.SUM, streams[r])
+                else:
+                    comms[r].all_reduce(sends[k][r], recvs[k][r], O.SUM, streams[r])
+
+        run_ranks(n, body)
+        torch.cuda.synchronize()
+        assert ipc_status(comms[0]) & 1 == 0
+        assert comms[0].ipc_ll_launches() == len(plan)
+        for k, (kind, cnt) in enumerate(plan):
+            want = oracle_replay(kind, H.Algo.AUTO, n, cnt, O.FP32, O.SUM, xs[k], 0, 0)
+            for r in range(n):
+                assert O.equal_bits(O.FP32, to_host(O.FP32, recvs[k][r]), want[r]), (k, kind, cnt, r)
+    finally:
+        destroy(comms)

@@ -28,6 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--algo", default="IPC")
     ap.add_argument("--sizes", default="1024,65536,1048576")
+    ap.add_argument("--op", default="ar", choices=["ar", "rs"], help="AllReduce, or ReduceScatter (size = input)")
     args = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     os.environ.setdefault("HCCL_AMD_IPC_TIMEOUT_MS", "10000")
@@ -46,10 +47,17 @@ def main():
     s = torch.cuda.Stream()
     for nbytes in [int(v) for v in args.sizes.split(",")]:
         x = torch.ones(nbytes // 2, dtype=torch.float16, device="cuda")
-        y = torch.empty_like(x)
+        y = torch.empty_like(x) if args.op == "ar" else torch.empty(nbytes // 2 // world, dtype=torch.float16,
+                                                                    device="cuda")
+
+        def call(st):
+            if args.op == "ar":
+                comm.all_reduce(x, y, H.HcclReduceOp.SUM, st)
+            else:
+                comm.reduce_scatter(x, y, H.HcclReduceOp.SUM, st)
         torch.cuda.synchronize()  # x is made on the current stream; the collectives run on s
         for i in range(10):
-            comm.all_reduce(x, y, H.HcclReduceOp.SUM, s)
+            call(s)
             if i == 0:
                 progress(rank, f"{nbytes} B: first call enqueued ({H.Algo(comm.last_algo).name})")
                 s.synchronize()
@@ -62,7 +70,7 @@ def main():
         H.host_profile(reset=True)
         h0 = time.perf_counter()
         for _ in range(K):
-            comm.all_reduce(x, y, H.HcclReduceOp.SUM, s)
+            call(s)
         enqueue = (time.perf_counter() - h0) / K * 1e3  # host ms per call (the calls return before the device work)
         # with HCCL_AMD_HOST_PROFILE=1: the library's own host time per call (the entry past its argument checks, and
         # the one-sided launch within it); the rest of `enqueue` is this script's Python and ctypes
@@ -76,7 +84,7 @@ def main():
         with torch.cuda.graph(g, stream=torch.cuda.Stream()):
             cs = torch.cuda.current_stream()
             for _ in range(K):
-                comm.all_reduce(x, y, H.HcclReduceOp.SUM, cs)
+                call(cs)
         torch.cuda.synchronize()
         progress(rank, f"{nbytes} B: captured")
         g.replay()
@@ -95,7 +103,7 @@ def main():
         t = torch.tensor([eager, graph, enqueue])
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         if rank == 0:
-            print(json.dumps({"algo": H.Algo(comm.last_algo).name, "n": world, "bytes": nbytes, "eager_us": round(float(t[0]) * 1e3, 2),
+            print(json.dumps({"op": args.op, "algo": H.Algo(comm.last_algo).name, "n": world, "bytes": nbytes, "eager_us": round(float(t[0]) * 1e3, 2),
                               "graph_us": round(float(t[1]) * 1e3, 2), "enqueue_us": round(float(t[2]) * 1e3, 2),
                               "library_host_us": lib_us,
                               "ok": ok,
