@@ -130,7 +130,8 @@ def _rank_main(rank, n, port, q, fence=None):
             results.append((i, status, comm.last_algo, ok))
             if max(all_gather(status & 1)) != 0:  # every rank stops together after a barrier timeout anywhere
                 break
-        # HIP graph: AllReduce (three sizes, so one-shot and two-shot), ReduceScatter and AllGather captured once,
+        # HIP graph: AllReduce (three sizes: the LL one-shot, a staged one-shot, two-shot), ReduceScatter (staged and
+        # LL) and AllGather captured once,
         # then replayed with fresh inputs. The barrier epochs live on the device, so each replay takes new ones as a
         # new call would. Small integers in fp32: every order gives the same bits.
         comm.set_algo(R.ALGO_IPC)
@@ -138,9 +139,11 @@ def _rank_main(rank, n, port, q, fence=None):
         sizes = (1000, 300001, (3 << 20) + 5)
         ar_in = [torch.zeros(c, device="cuda") for c in sizes]
         ar_out = [torch.zeros(c, device="cuda") for c in sizes]
-        rs_len, ag_len = 70001, 50003
+        rs_len, ag_len, rs_small = 70001, 50003, 1001  # rs_small: the LL ReduceScatter (blocks under 64 KiB)
         rs_in = torch.zeros(n * rs_len, device="cuda")
         rs_out = torch.zeros(rs_len, device="cuda")
+        rss_in = torch.zeros(n * rs_small, device="cuda")
+        rss_out = torch.zeros(rs_small, device="cuda")
         ag_in = torch.zeros(ag_len, device="cuda")
         ag_out = torch.zeros(n * ag_len, device="cuda")
         ramp = torch.arange(n * rs_len, device="cuda", dtype=torch.float32) % 97
@@ -151,6 +154,7 @@ def _rank_main(rank, n, port, q, fence=None):
             for x, y in zip(ar_in, ar_out):
                 comm.all_reduce(x, y, O.SUM, stream=cs)
             comm.reduce_scatter(rs_in, rs_out, O.SUM, stream=cs)
+            comm.reduce_scatter(rss_in, rss_out, O.SUM, stream=cs)
             comm.all_gather(ag_in, ag_out, stream=cs)
         graph_ok = []
         for rep in range(4):
@@ -158,6 +162,7 @@ def _rank_main(rank, n, port, q, fence=None):
             for x in ar_in:
                 x.fill_(v)
             rs_in.copy_(ramp + v)
+            rss_in.copy_(ramp[:n * rs_small] + v)
             ag_in.fill_(v)
             torch.cuda.synchronize()
             graph.replay()
@@ -165,6 +170,7 @@ def _rank_main(rank, n, port, q, fence=None):
             tot = float((rep + 1) * n * (n + 1) // 2)
             ok = all(bool(torch.all(y == tot).item()) for y in ar_out)
             ok = ok and bool(torch.all(rs_out == n * ramp[rank * rs_len:(rank + 1) * rs_len] + tot).item())
+            ok = ok and bool(torch.all(rss_out == n * ramp[rank * rs_small:(rank + 1) * rs_small] + tot).item())
             want = torch.cat([torch.full((ag_len,), float((q + 1) * (rep + 1)), device="cuda") for q in range(n)])
             ok = ok and bool(torch.equal(ag_out, want))
             graph_ok.append(ok)
