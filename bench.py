@@ -779,6 +779,7 @@ def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
                 a = send.view(torch.float16)[: nbytes // 2]
                 b = recv.view(torch.float16)[: nbytes // 2]
                 iters = 20 if nbytes <= (64 << 20) else 3
+                ll0 = comm.ipc_ll_launches()
                 try:
                     t = _timed(lambda: comm.all_reduce(a, b, H.HcclReduceOp.SUM, s), iters)
                 except H.HcclError as e:
@@ -801,6 +802,7 @@ def bench_c5(comm, send, recv, world, max_bytes: int = 4 << 30) -> dict:
                     row[f"{key}_matches_{tw}"] = bool(torch.equal(sample, digests[(tw, nbytes)])) if meaningful else None
                 if ran.startswith("IPC"):
                     row[f"{key}_barrier_timeouts"] = comm.ipc_status() & 1
+                    row[f"{key}_ll"] = comm.ipc_ll_launches() != ll0  # the LL form ran (HCCL_AMD_IPC_LL_BYTES)
         for nbytes in sizes:
             row = rows[nbytes]
             for key, algo, rule in (("ipc", H.Algo.IPC, 0), ("rhd_default", H.Algo.RHD, small)):
