@@ -223,7 +223,7 @@ def test_ipc_collectives_rank_mode(n, fence):
             assert ok, f"rank {r} case {CASES[i]} differs from the reference order"
 
 
-def _lost_peer_main(rank, port, q):
+def _lost_peer_main(rank, port, q, count=1 << 20):
     # the bound comes from the reference's own variable (AIV-mode rule: seconds, two decimals)
     os.environ.pop("HCCL_AMD_IPC_TIMEOUT_MS", None)
     os.environ["HCCL_EXEC_TIMEOUT"] = "1.5"
@@ -250,14 +250,16 @@ def _lost_peer_main(rank, port, q):
                 return e.code
 
         comm = H.comm_init_host_exchange(2, rank, all_gather)
+        comm.set_algo(H.Algo.IPC)  # the auto family's one-shot: the LL form at the small size
         stream = torch.cuda.Stream()
-        x = torch.full((1 << 20,), float(rank + 1), device="cuda")
+        x = torch.full((count,), float(rank + 1), device="cuda")
         y = torch.empty_like(x)
         torch.cuda.synchronize()
         comm.all_reduce(x, y, H.HcclReduceOp.SUM, stream=stream)  # both ranks: set-up + a good call
         stream.synchronize()
         res = {"first_status": comm.ipc_status(), "first_ok": bool(torch.all(y == 3.0).item()),
-               "first_async": comm.async_error(), "timeout_ms": H.lib.HcclAmdIpcTimeoutMs()}
+               "first_async": comm.async_error(), "timeout_ms": H.lib.HcclAmdIpcTimeoutMs(),
+               "ll_launches": comm.ipc_ll_launches()}
         progress.write(f"first {res}\n")
         dist.barrier()
         if rank == 0:  # rank 1 never joins this call
@@ -288,15 +290,17 @@ def _lost_peer_main(rank, port, q):
         time.sleep(10)
 
 
-def test_ipc_lost_peer_fails_the_communicator():
-    """A peer that never joins: the barrier gives up after HCCL_EXEC_TIMEOUT (no hang); the next collective returns
+@pytest.mark.parametrize("count", [1 << 20, 256], ids=["staged", "ll"])
+def test_ipc_lost_peer_fails_the_communicator(count):
+    """A peer that never joins: the wait (staged: the barrier; LL: the flag poll) gives up after HCCL_EXEC_TIMEOUT (no
+    hang); the next collective returns
     HCCL_E_TIMEOUT, every later one HCCL_E_SUSPENDING (the reference's status gate, op_common.cc:89-97), and
     HcclGetCommAsyncError reports HCCL_E_TIMEOUT without a device synchronisation; teardown still completes."""
     import hccl_amd as H
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_lost_peer_main, args=(r, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_lost_peer_main, args=(r, port, q, count)) for r in range(2)]
     for p in procs:
         p.start()
     try:
@@ -314,6 +318,7 @@ def test_ipc_lost_peer_fails_the_communicator():
         res = got[r][1]
         assert res["first_ok"] and res["first_status"] & 1 == 0 and res["first_async"] == 0, res
         assert res["timeout_ms"] == 1500, res
+        assert res["ll_launches"] == (1 if count * 4 <= (64 << 10) else 0), res
     r0 = got[0][1]
     assert r0["lost_rc"] == 0  # stream-ordered: the call that enqueued the lost barrier had already returned
     assert r0["lost_status"] & 1 == 1
