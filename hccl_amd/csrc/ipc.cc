@@ -309,10 +309,13 @@ void IpcRelease(Comm& c)
 // block's pull, unpack and fold are serial latencies, so the LL form wants many small blocks where the staged kernel
 // wants few: rank mode, n = 2 and 4 on one GPU (tools/probes/sweep_ipc_blocks.py with HCCL_AMD_IPC_LL_BYTES,
 // profiles/r05_ll_sweep_blocks.jsonl): 1 KiB best at 1-2 blocks (7.4 us), 64 KiB at 32 (9.4 us; 55.5 us with 1).
-uint32_t LlIpcBlocks(uint32_t n, uint64_t bytes)
+// RHD's order folds a tree per part and chunk, so its blocks want about one word per thread, and never fewer than two
+// blocks (n = 2, eager: 1 KiB 14.5 us on one block, 13.4 on two; 4 KiB 13.2 on four; profiles/r05_ll_rhd_blocks.jsonl).
+uint32_t LlIpcBlocks(uint32_t n, uint64_t bytes, bool rhd)
 {
     const uint64_t items = uint64_t(n > 1 ? n - 1 : 1) * ((bytes + 3) / 4);
-    return static_cast<uint32_t>(std::min<uint64_t>(128, std::max<uint64_t>(1, (items + 511) / 512)));
+    const uint64_t per = rhd ? 256 : 512;
+    return static_cast<uint32_t>(std::min<uint64_t>(128, std::max<uint64_t>(2, (items + per - 1) / per)));
 }
 
 uint32_t DefaultIpcBlocks(uint64_t bytes)
@@ -564,7 +567,9 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
             count * es <= std::min<uint64_t>(c.cfg.ipcLlBytes, kIpcLlMaxBytes))
                ? 1u
                : 0u;
-    s.blocks = c.ipcBlocks != 0 ? c.ipcBlocks : a.ll != 0 ? LlIpcBlocks(n, count * es) : DefaultIpcBlocks(callBytes);
+    s.blocks = c.ipcBlocks != 0               ? c.ipcBlocks
+               : a.ll != 0                    ? LlIpcBlocks(n, count * es, plan.order == kIpcRhd)
+                                              : DefaultIpcBlocks(callBytes);
     if (c.transport->SharedDevice() && c.ipcBlocks == 0) s.blocks = std::min(s.blocks, kIpcBlocks);
     // Co-residency: every block waits at barriers for its peers' blocks, so all blocks on this device must be resident
     // at once (a loopback world puts every rank's blocks on it; in rank mode, the ranks whose processes share this

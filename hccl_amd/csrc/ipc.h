@@ -217,7 +217,7 @@ struct IpcState {
 constexpr uint32_t kIpcBlocks = 128;     // workgroups per rank and launch in a loopback world (cap)
 constexpr uint32_t kIpcMaxBlocks = 512;  // flags are sized for this many (HcclAmdCommSetIpcBlocks)
 uint32_t DefaultIpcBlocks(uint64_t bytes);  // workgroups per launch when the communicator sets none (ipc.cc)
-uint32_t LlIpcBlocks(uint32_t n, uint64_t bytes);  // the same for a launch in the LL form (ipc.cc)
+uint32_t LlIpcBlocks(uint32_t n, uint64_t bytes, bool rhd);  // the same for a launch in the LL form (ipc.cc)
 constexpr size_t kIpcStatusBytes = 32;  // status words (IpcArgs::status)
 constexpr int kIpcEpochWord = 4;
 constexpr int kIpcDoneWord = 5;

@@ -12,10 +12,11 @@ UNPACK_BYTES = MAX_RANKS * (LL_MAX + 256)  # kIpcLlUnpackBytes
 LOOPBACK_BLOCK_CAP = 128          # kIpcBlocks
 
 
-def ll_blocks(n, nbytes):
+def ll_blocks(n, nbytes, rhd=False):
     """ipc.cc LlIpcBlocks."""
     items = max(n - 1, 1) * ((nbytes + 3) // 4)
-    return min(128, max(1, (items + 511) // 512))
+    per = 256 if rhd else 512
+    return min(128, max(2, (items + per - 1) // per))
 
 
 def windows(count, es, blocks):
@@ -67,15 +68,16 @@ def test_ll_windows_words_and_areas(n, es, nbytes):
     if count * es > LL_MAX:
         return
     computed = ll_blocks(n, count * es)
-    for blocks in sorted({computed, min(computed, LOOPBACK_BLOCK_CAP), 1, 3, 128}):
+    for blocks in sorted({computed, ll_blocks(n, count * es, rhd=True), 1, 3, 128}):
         check(n, es, count, blocks)
 
 
 def test_ll_block_rule():
-    """About two polled words per thread of 256: 1 KiB at n = 2 is one block, 64 KiB at n = 2 thirty-two, and the
-    count never leaves [1, 128]."""
-    assert ll_blocks(2, 1024) == 1
-    assert ll_blocks(2, 4096) == 2
-    assert ll_blocks(2, 65536) == 32
+    """About two polled words per thread of 256 (RHD's order: one), never fewer than two blocks nor more than 128:
+    1 KiB at n = 2 is two blocks, 64 KiB at n = 2 thirty-two (RHD sixty-four)."""
+    assert ll_blocks(2, 1024) == 2
+    assert ll_blocks(2, 4096) == 2 and ll_blocks(2, 4096, rhd=True) == 4
+    assert ll_blocks(2, 65536) == 32 and ll_blocks(2, 65536, rhd=True) == 64
     assert ll_blocks(8, 65536) == 128
-    assert all(1 <= ll_blocks(n, b) <= 128 for n in range(2, 17) for b in range(1, LL_MAX + 1, 511))
+    assert all(2 <= ll_blocks(n, b, r) <= 128 for n in range(2, 17) for b in range(1, LL_MAX + 1, 511)
+               for r in (False, True))

@@ -4,7 +4,7 @@ an xGMI measurement; it shows the launch/barrier cost per block count at small s
 ones. Run as:
   python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 \
       tools/probes/sweep_ipc_blocks.py > gpurun_out/sweep_ipc_blocks.jsonl
-(SWEEP_BLOCKS / SWEEP_SIZES: comma lists overriding the block counts and byte sizes.)
+(SWEEP_BLOCKS / SWEEP_SIZES: comma lists overriding the block counts and byte sizes; SWEEP_ALGO: the family, IPC.)
 """
 import json
 import os
@@ -34,7 +34,7 @@ def main():
         return out
 
     comm = H.comm_init_host_exchange(world, rank, all_gather)
-    comm.set_algo(H.Algo.IPC)
+    comm.set_algo(H.Algo[os.environ.get("SWEEP_ALGO", "IPC")])
     stream = torch.cuda.Stream()  # a null stream is HCCL_E_PTR, as in the reference's entry checks
     dev = torch.device("cuda", 0)
     for size in SIZES:
