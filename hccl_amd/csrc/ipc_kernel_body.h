@@ -149,11 +149,18 @@ __device__ __forceinline__ uint32_t Arrive(const IpcArgs& a, uint32_t epoch)
 {
     if (threadIdx.x != 0) return 0;
     asm volatile("" ::"v"(epoch) : "memory");  // the counter read has returned before the arrival is issued
-    return __hip_atomic_fetch_add(a.status + kIpcDoneWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // The offset is zero, but the compiler cannot see it: an address it takes for uniform across the wave gets the
+    // wave-combined atomic, whose per-lane result is computed (and waited for) right here instead of at EndLaunch.
+    uint32_t zero = 0;
+    asm volatile("" : "+v"(zero));
+    return __hip_atomic_fetch_add(a.status + kIpcDoneWord + zero, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ void EndLaunch(const IpcArgs& a, uint32_t arrivedBefore)
 {
+    // opaque until here: otherwise the compiler folds the comparison's + 1 into Arrive's branch and waits for the
+    // arrival's round trip at the launch's start, before the first store
+    asm volatile("" : "+v"(arrivedBefore));
     if (threadIdx.x == 0 && arrivedBefore + 1 == gridDim.x * gridDim.y) {
         __hip_atomic_store(a.status + kIpcDoneWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // an LL launch has no barrier epochs; it advances the LL sequence instead (LlOneShot)
@@ -228,22 +235,22 @@ __device__ __forceinline__ void ForBlockShare(const IpcArgs& a, uint64_t len, F&
 constexpr int kIpcU = 4;  // vectors per lane in flight (r03 A/B of 2, 4, 8: profiles/r03_ipc_variant_ab_unroll.jsonl)
 
 template <int NT>
-__device__ __forceinline__ void CopyVecs(u32x4* d, const u32x4* s, uint64_t& v, uint64_t vhi)
+__device__ __forceinline__ void CopyVecs(u32x4* d, const u32x4* s, uint64_t& v, uint64_t vhi, uint32_t bt)
 {
-    for (; v + (kIpcU - 1) * blockDim.x < vhi; v += kIpcU * blockDim.x) {
+    for (; v + (kIpcU - 1) * bt < vhi; v += kIpcU * bt) {
         u32x4 x[kIpcU];
 #pragma unroll
-        for (int u = 0; u < kIpcU; ++u) x[u] = ld<NT>(s + v + u * blockDim.x);
+        for (int u = 0; u < kIpcU; ++u) x[u] = ld<NT>(s + v + u * bt);
 #pragma unroll
-        for (int u = 0; u < kIpcU; ++u) st<NT>(d + v + u * blockDim.x, x[u]);
+        for (int u = 0; u < kIpcU; ++u) st<NT>(d + v + u * bt, x[u]);
     }
-    for (; v < vhi; v += blockDim.x) st<NT>(d + v, ld<NT>(s + v));
+    for (; v < vhi; v += bt) st<NT>(d + v, ld<NT>(s + v));
 }
 
 // dst[e] = src[e] for e in r. vec = both pointers are 16-B aligned; otherwise every element goes through the scalar
 // loop. nt: non-temporal loads and stores (IpcArgs::nt).
 template <typename S>
-__device__ __forceinline__ void CopyRange(S* dst, const S* src, Range r, bool vec, bool nt)
+__device__ __forceinline__ void CopyRange(S* dst, const S* src, Range r, bool vec, bool nt, uint32_t bt)
 {
     constexpr uint64_t V = 16 / sizeof(S);
     // r.lo is vector aligned unless the window is empty at the end of a piece (lo = hi = len); r.hi may be anything
@@ -252,11 +259,11 @@ __device__ __forceinline__ void CopyRange(S* dst, const S* src, Range r, bool ve
     u32x4* d = reinterpret_cast<u32x4*>(dst);
     uint64_t v = vlo + threadIdx.x;
     if (nt) {
-        CopyVecs<3>(d, s, v, vhi);
+        CopyVecs<3>(d, s, v, vhi, bt);
     } else {
-        CopyVecs<0>(d, s, v, vhi);
+        CopyVecs<0>(d, s, v, vhi, bt);
     }
-    for (uint64_t e = max(vhi * V, r.lo) + threadIdx.x; e < r.hi; e += blockDim.x) dst[e] = src[e];
+    for (uint64_t e = max(vhi * V, r.lo) + threadIdx.x; e < r.hi; e += bt) dst[e] = src[e];
 }
 
 // Rank of operand i (0 .. n-1) of a fold of chunk t in the given order; j = the sub-slice (kIpcO6 only).
@@ -365,13 +372,13 @@ __device__ __forceinline__ auto TreeFoldN(uint32_t n, const Leaf& leaf)
 // coordinates). One vector (or element) per lane and step keeps the register stack small.
 template <class E, int OP, class Dst, class RankSrc, class RankOf>
 __device__ __forceinline__ void TreeSeg(uint32_t n, const RankSrc& rankSrc, const RankOf& rankOf, Dst dsts,
-                                        uint32_t ndst, Range r, bool vec)
+                                        uint32_t ndst, Range r, bool vec, uint32_t bt)
 {
     using S = typename E::S;
     constexpr uint64_t V = 16 / sizeof(S);
     const uint64_t vb = (r.lo + V - 1) / V, ve = r.hi / V;
     auto scalarTree = [&](uint64_t lo, uint64_t hi) {
-        for (uint64_t e = lo + threadIdx.x; e < hi; e += blockDim.x) {
+        for (uint64_t e = lo + threadIdx.x; e < hi; e += bt) {
             const S acc = TreeFoldN<E, OP>(n, [&](uint32_t q) { return rankSrc(rankOf(q))[e]; });
             for (uint32_t d = 0; d < ndst; ++d) dsts(d)[e] = acc;
         }
@@ -381,7 +388,7 @@ __device__ __forceinline__ void TreeSeg(uint32_t n, const RankSrc& rankSrc, cons
         return;
     }
     scalarTree(r.lo, vb * V);
-    for (uint64_t v = vb + threadIdx.x; v < ve; v += blockDim.x) {
+    for (uint64_t v = vb + threadIdx.x; v < ve; v += bt) {
         const u32x4 acc = TreeFoldN<E, OP>(
             n, [&](uint32_t q) { return reinterpret_cast<const u32x4*>(rankSrc(rankOf(q)))[v]; });
         for (uint32_t d = 0; d < ndst; ++d) reinterpret_cast<u32x4*>(dsts(d))[v] = acc;
@@ -403,12 +410,12 @@ __device__ __forceinline__ void FoldSeg(const IpcArgs& a, uint32_t me, uint32_t 
     auto rankSrc = [&](uint32_t q) { return q == me ? own : slots + uint64_t(q) * a.piece; };
     if (a.order == kIpcO4) {
         // rank-independent tree
-        TreeSeg<E, OP>(n, rankSrc, [](uint32_t q) { return q; }, dsts, ndst, r, vec);
+        TreeSeg<E, OP>(n, rankSrc, [](uint32_t q) { return q; }, dsts, ndst, r, vec, a.threads);
         return;
     }
     auto src = [&](uint32_t i) { return rankSrc(OperandRank(a.order, n, me, j, i)); };
     auto scalar = [&](uint64_t lo, uint64_t hi) {
-        for (uint64_t e = lo + threadIdx.x; e < hi; e += blockDim.x) {
+        for (uint64_t e = lo + threadIdx.x; e < hi; e += a.threads) {
             S acc = src(0)[e];
             for (uint32_t i = 1; i < n; ++i) acc = E::template ap<OP>(src(i)[e], acc);
             for (uint32_t d = 0; d < ndst; ++d) dsts(d)[e] = acc;
@@ -424,20 +431,20 @@ __device__ __forceinline__ void FoldSeg(const IpcArgs& a, uint32_t me, uint32_t 
     auto body = [&](auto ntTag) {
         constexpr int NT = decltype(ntTag)::value;
         constexpr int U = kIpcU;
-        for (; v + (U - 1) * blockDim.x < ve; v += U * blockDim.x) {
+        for (; v + (U - 1) * a.threads < ve; v += U * a.threads) {
             u32x4 acc[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) acc[u] = ld<NT>(reinterpret_cast<const u32x4*>(src(0)) + v + u * blockDim.x);
+            for (int u = 0; u < U; ++u) acc[u] = ld<NT>(reinterpret_cast<const u32x4*>(src(0)) + v + u * a.threads);
             for (uint32_t i = 1; i < n; ++i) {
                 u32x4 x[U];
 #pragma unroll
-                for (int u = 0; u < U; ++u) x[u] = ld<NT>(reinterpret_cast<const u32x4*>(src(i)) + v + u * blockDim.x);
+                for (int u = 0; u < U; ++u) x[u] = ld<NT>(reinterpret_cast<const u32x4*>(src(i)) + v + u * a.threads);
 #pragma unroll
                 for (int u = 0; u < U; ++u) acc[u] = combine<E, OP>(x[u], acc[u]);
             }
             for (uint32_t d = 0; d < ndst; ++d) {
 #pragma unroll
-                for (int u = 0; u < U; ++u) st<NT>(reinterpret_cast<u32x4*>(dsts(d)) + v + u * blockDim.x, acc[u]);
+                for (int u = 0; u < U; ++u) st<NT>(reinterpret_cast<u32x4*>(dsts(d)) + v + u * a.threads, acc[u]);
             }
         }
     };
@@ -446,7 +453,7 @@ __device__ __forceinline__ void FoldSeg(const IpcArgs& a, uint32_t me, uint32_t 
     } else {
         body(std::integral_constant<int, 0>{});
     }
-    for (; v < ve; v += blockDim.x) {
+    for (; v < ve; v += a.threads) {
         u32x4 acc = reinterpret_cast<const u32x4*>(src(0))[v];
         for (uint32_t i = 1; i < n; ++i) acc = combine<E, OP>(reinterpret_cast<const u32x4*>(src(i))[v], acc);
         for (uint32_t d = 0; d < ndst; ++d) reinterpret_cast<u32x4*>(dsts(d))[v] = acc;
@@ -481,7 +488,7 @@ __device__ __forceinline__ void RhdFold(const IpcArgs& a, uint32_t me, uint64_t 
         uint64_t packed = 0;
         for (uint32_t q = 0; q < n; ++q) packed |= uint64_t(a.rhdReal[j][v ^ q]) << (4 * q);
         TreeSeg<E, OP>(n, rankSrc, [packed](uint32_t q) { return uint32_t(packed >> (4 * q)) & 15u; }, dsts, ndst,
-                       Range{g - kP, end - kP}, vec);
+                       Range{g - kP, end - kP}, vec, a.threads);
         g = end;
     }
 }
@@ -507,6 +514,13 @@ __device__ __forceinline__ void FoldRange(const IpcArgs& a, uint32_t me, uint64_
         const uint64_t lo = max(r.lo, sb > kP ? sb - kP : 0), hi = min(r.hi, se > kP ? se - kP : 0);
         if (lo < hi) FoldSeg<E, OP>(a, me, j, own, slots, dsts, ndst, Range{lo, hi}, vec);
     }
+}
+
+// A generic pointer into device memory as a global-address-space one (global, not flat, loads and stores).
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* AsGlobal(T* p)
+{
+    return (__attribute__((address_space(1))) T*)p;
 }
 
 // The LL word w of source rank q in rank c's LL area for parity p: 8 bytes {data bytes 4w .. 4w+3, flag}.
@@ -546,9 +560,10 @@ __device__ __forceinline__ void LlOneShot(const IpcArgs& a, uint32_t me)
     using S = typename E::S;
     const uint32_t n = a.n;
     Stamp(a, me, kTrEntry);
-    const uint32_t seq = __hip_atomic_load(a.status + kIpcLlSeqWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t arrivedBefore = Arrive(a, seq);
-    const uint32_t par = seq & 1u, flag = seq + 1u;
+    // The sticky word, the LL sequence word and the first batch of input words are all loaded before any of them is
+    // waited for: one memory latency before the first store instead of three.
+    uint32_t sticky = __hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t seq = __hip_atomic_load(a.status + kIpcLlSeqWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // Every destination's piece has the same length: the whole input (one-shot AllReduce) or one block of the
     // ReduceScatter's equal blocks (peer c receives block c, this rank folds block me).
     const bool perDest = a.kind == kIpcReduceScatter;
@@ -559,27 +574,74 @@ __device__ __forceinline__ void LlOneShot(const IpcArgs& a, uint32_t me)
     // the last non-empty window's alone
     const uint64_t wlo = r.lo * sizeof(S) / 4, whi = r.hi > r.lo ? (r.hi * sizeof(S) + 3) / 4 : wlo, nw = whi - wlo;
     const uint8_t* in = static_cast<const uint8_t*>(a.in[me]);
-    auto src = [&](uint32_t c) { return in + ChunkStart(a, c) * sizeof(S); };
+    // ChunkStart for the LL geometries (Whole and Block: neither vgeom nor balanced), without ChunkStart's vStart
+    // table, which a per-lane peer index would read from the argument memory with a round trip per word
+    auto src = [&](uint32_t c) { return in + uint64_t(c) * a.chunkStride * sizeof(S); };
     // kLlBatch words per thread in flight at once: the first look at a batch costs one memory latency, not one per word
     constexpr uint32_t kLlBatch = 8;
-    // push: each word of the window to every peer's slot `me` (the one-shot's word loaded once for all peers, a
-    // ReduceScatter's from each peer's block)
-    for (uint64_t base = wlo + threadIdx.x; base < whi; base += uint64_t(kLlBatch) * blockDim.x) {
-        uint32_t d[kLlBatch];
+    // Push items: a one-shot's words (each loaded once, stored to every peer), a ReduceScatter's (peer, word) pairs,
+    // the word fastest (peer c's word w comes from c's block). Every batch is loaded before any of it is stored, and
+    // the stores wait for nothing but their data: a store loop holding a load makes the compiler wait for each store
+    // to complete before the next.
+    const uint32_t T = a.threads;
+    const uint32_t pushItems = static_cast<uint32_t>(perDest ? uint64_t(n - 1) * nw : nw);
+    auto itemAt = [&](uint32_t i, uint32_t& c, uint64_t& w) {
+        c = perDest ? (me + 1 + i / static_cast<uint32_t>(nw)) % n : me;
+        w = wlo + (perDest ? i % static_cast<uint32_t>(nw) : i);
+    };
+    uint32_t d[kLlBatch];
+    auto loadBatch = [&](uint32_t base) {
 #pragma unroll
         for (uint32_t k = 0; k < kLlBatch; ++k) {
-            const uint64_t w = base + uint64_t(k) * blockDim.x;
-            if (w < whi && !perDest) d[k] = LoadWord(src(me), bytes, w);
+            const uint32_t i = base + k * T;
+            if (i < pushItems) {
+                uint32_t c;
+                uint64_t w;
+                itemAt(i, c, w);
+                d[k] = LoadWord(src(c), bytes, w);
+            }
         }
+    };
+    // a ReduceScatter's lanes store to different peers: their LL areas from LDS, not by a per-lane index into the
+    // arguments (a memory round trip per store)
+    __shared__ char* llArea[kIpcMaxRanks];
+    if (perDest && threadIdx.x < n) llArea[threadIdx.x] = reinterpret_cast<char*>(a.flags[threadIdx.x]) + kIpcFlagBytes;
+    loadBatch(threadIdx.x);
+    // the status words are used only from here, so the loads above are all issued before the first wait
+    asm volatile("" : "+v"(sticky), "+v"(seq)::"memory");
+    // a communicator whose IPC wait ever timed out stays failed (sticky bit): never wait on its peers again
+    if ((sticky & 1u) != 0) return;
+    if (perDest) __syncthreads();
+    // issued before the stores (its result is consumed only at EndLaunch), so it waits for none of them
+    const uint32_t arrivedBefore = Arrive(a, seq);
+    const uint32_t par = seq & 1u, flag = seq + 1u;
+    for (uint32_t base = threadIdx.x; base < pushItems; base += kLlBatch * T) {
+        if (base != threadIdx.x) loadBatch(base);  // the first batch is loaded above
+        if (perDest) {
 #pragma unroll
-        for (uint32_t k = 0; k < kLlBatch; ++k) {
-            const uint64_t w = base + uint64_t(k) * blockDim.x;
-            if (w >= whi) continue;
+            for (uint32_t k = 0; k < kLlBatch; ++k) {
+                const uint32_t i = base + k * T;
+                if (i >= pushItems) continue;
+                uint32_t c;
+                uint64_t w;
+                itemAt(i, c, w);
+                // LlWord(a, c, par, me, w), as a global pointer: a generic one makes a flat store, which the compiler
+                // waits for before the next LDS read
+                char* slot = llArea[c] + par * kIpcLlParityBytes + me * kIpcLlSlotBytes;
+                __hip_atomic_store(AsGlobal(reinterpret_cast<uint64_t*>(slot) + w),
+                                   uint64_t(d[k]) | (uint64_t(flag) << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        } else {
+            // peer-major: the loop over peers holds stores only, so the batch's loads are waited for once, before it
             for (uint32_t j = 1; j < n; ++j) {
-                const uint32_t c = (me + j) % n;
-                const uint32_t data = perDest ? LoadWord(src(c), bytes, w) : d[k];
-                __hip_atomic_store(LlWord(a, c, par, me, w), uint64_t(data) | (uint64_t(flag) << 32),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                const auto slot = AsGlobal(LlWord(a, (me + j) % n, par, me, wlo));
+#pragma unroll
+                for (uint32_t k = 0; k < kLlBatch; ++k) {
+                    const uint32_t i = base + k * T;
+                    if (i >= pushItems) continue;
+                    __hip_atomic_store(slot + i, uint64_t(d[k]) | (uint64_t(flag) << 32), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                }
             }
         }
     }
@@ -591,14 +653,14 @@ __device__ __forceinline__ void LlOneShot(const IpcArgs& a, uint32_t me)
     bool cut = false;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     const uint64_t items = uint64_t(n - 1) * nw;
-    for (uint64_t base = threadIdx.x; base < items && !cut; base += uint64_t(kLlBatch) * blockDim.x) {
+    for (uint64_t base = threadIdx.x; base < items && !cut; base += uint64_t(kLlBatch) * a.threads) {
         uint64_t v[kLlBatch];
         const uint64_t* src[kLlBatch];
         uint32_t dst[kLlBatch];
         uint32_t pending = 0;
 #pragma unroll
         for (uint32_t k = 0; k < kLlBatch; ++k) {
-            const uint64_t i = base + uint64_t(k) * blockDim.x;
+            const uint64_t i = base + uint64_t(k) * a.threads;
             src[k] = nullptr;
             if (i < items) {
                 const uint32_t q = (me + 1 + static_cast<uint32_t>(i / nw)) % n;
@@ -666,9 +728,7 @@ template <class E, int OP, bool kRhd>
 __global__ __launch_bounds__(kIpcMaxThreads) void k_ipc_ll(IpcArgs a)
 {
     const uint32_t me = a.me >= 0 ? static_cast<uint32_t>(a.me) : blockIdx.y;
-    // a communicator whose IPC wait ever timed out stays failed (sticky bit): never wait on its peers again
-    if ((__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 1u) != 0) return;
-    LlOneShot<E, OP, kRhd>(a, me);
+    LlOneShot<E, OP, kRhd>(a, me);  // checks the sticky bit itself
 }
 
 // kRhd: the kIpcRhd instantiation (one-shot AllReduce only, kind and order fixed at compile time). It is a kernel of
@@ -685,8 +745,11 @@ __global__ __launch_bounds__(kIpcMaxThreads) void k_ipc_collective(IpcArgs a)
     S* out = static_cast<S*>(a.out[me]);
     const bool oneShot = kind == kIpcAllReduceOneShot || kind == kIpcReduceOneShot;
     const bool reduceKind = kind == kIpcReduce || kind == kIpcReduceOneShot;
-    // a communicator whose IPC barrier ever timed out stays failed (sticky bit): never wait on its peers again
-    if ((__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 1u) != 0) return;
+    // a communicator whose IPC barrier ever timed out stays failed (sticky bit): never wait on its peers again. The
+    // epoch counter (below) is loaded together with it: one memory latency for both.
+    const uint32_t sticky = __hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t epoch = __hip_atomic_load(a.status + kIpcEpochWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((sticky & 1u) != 0) return;
     // Slots: the two-barrier kinds use stgIn. The single-barrier kinds alternate between two areas by the parity of
     // the round's barrier epoch e, and fold after the barrier with no second one, so rank i may store round k+2
     // (parity of k) while a peer still folds round k. That is safe because block b of rank i passed barrier k+1
@@ -706,9 +769,8 @@ __global__ __launch_bounds__(kIpcMaxThreads) void k_ipc_collective(IpcArgs a)
     // Epochs come from the device counter (Arrive / EndLaunch), so the next launch in stream order, a call or a graph
     // replay alike, starts where this one ended. Every rank runs the same launch sequence, so the counters agree.
     Stamp(a, me, kTrEntry);
-    uint32_t epoch = __hip_atomic_load(a.status + kIpcEpochWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const FlagLane fl = LaneFlags(a, me);
     const uint32_t arrivedBefore = Arrive(a, epoch);
+    const FlagLane fl = LaneFlags(a, me);  // after the arrival, whose issue would otherwise wait for this lane's load
     uint32_t waitMax = 0;
     for (uint32_t k = 0; k < a.rounds; ++k) {
         const uint64_t kP = uint64_t(k) * a.piece;
@@ -721,7 +783,7 @@ __global__ __launch_bounds__(kIpcMaxThreads) void k_ipc_collective(IpcArgs a)
             if (kind == kIpcReduceOneShot && c != a.root) continue;
             S* slot = reinterpret_cast<S*>(slotArea(c, epoch + 1)) + uint64_t(me) * a.piece;
             ForBlockShare(a, PieceLen(a, c, kP), [&](Range r) {
-                CopyRange<S>(slot, in + ChunkStart(a, c) + kP, r, ChunkVec<S>(a, c), a.nt != 0);
+                CopyRange<S>(slot, in + ChunkStart(a, c) + kP, r, ChunkVec<S>(a, c), a.nt != 0, a.threads);
             });
         }
         Stamp(a, me, kTrPhase0);
@@ -736,7 +798,8 @@ __global__ __launch_bounds__(kIpcMaxThreads) void k_ipc_collective(IpcArgs a)
                     const S* src = q == me ? in + kP : slots + uint64_t(q) * a.piece;
                     S* dst = out + uint64_t(q) * a.outStride + kP;
                     if (src != dst) {
-                        CopyRange<S>(dst, src, r, a.aligned && (uint64_t(q) * a.outStride) % V == 0, a.nt != 0);
+                        CopyRange<S>(dst, src, r, a.aligned && (uint64_t(q) * a.outStride) % V == 0, a.nt != 0,
+                                     a.threads);
                     }
                 }
             });
@@ -772,7 +835,7 @@ __global__ __launch_bounds__(kIpcMaxThreads) void k_ipc_collective(IpcArgs a)
                 ForBlockShare(a, PieceLen(a, c, kP), [&](Range r) {
                     CopyRange<S>(out + ChunkStart(a, c) + kP,
                                  static_cast<const S*>(a.stgRes[me]) + uint64_t(c) * a.piece, r, ChunkVec<S>(a, c),
-                                 a.nt != 0);
+                                 a.nt != 0, a.threads);
                 });
             }
         }
