@@ -81,3 +81,36 @@ def test_ll_block_rule():
     assert ll_blocks(8, 65536) == 128
     assert all(2 <= ll_blocks(n, b, r) <= 128 for n in range(2, 17) for b in range(1, LL_MAX + 1, 511)
                for r in (False, True))
+
+
+@pytest.mark.parametrize("n", [2, 3, 8, 16])
+@pytest.mark.parametrize("nw", [0, 1, 5, 64, 257, 16384])
+@pytest.mark.parametrize("threads", [256, 512])
+def test_push_items_cover_every_peer_word_once(n, nw, threads):
+    """LlOneShot's push (ipc_kernel_body.h): a ReduceScatter's items are (peer, word) pairs, the word fastest, dealt to
+    the block's threads in batches of kLlBatch x threads; every peer's every word of the window is stored exactly once,
+    and the item index stays inside 32 bits. A one-shot's items are its words, each stored to every peer."""
+    K = 8  # kLlBatch
+    me, wlo = n - 1, 1000
+    for per_dest in (True, False):
+        items = (n - 1) * nw if per_dest else nw
+        assert items < 2 ** 32 - K * threads
+        stored = []
+        for t in range(threads):
+            base = t
+            while base < items:
+                for k in range(K):
+                    i = base + k * threads
+                    if i >= items:
+                        continue
+                    c = (me + 1 + i // nw) % n if per_dest else me
+                    w = wlo + (i % nw if per_dest else i)
+                    if per_dest:
+                        stored.append((c, w))
+                    else:
+                        stored.extend(((me + j) % n, w) for j in range(1, n))
+                base += K * threads
+        want = [((me + j) % n, wlo + x) for j in range(1, n) for x in range(nw)]
+        assert sorted(stored) == sorted(want)
+        assert all(c != me for c, _ in stored)
+
