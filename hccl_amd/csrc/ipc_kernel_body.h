@@ -55,7 +55,7 @@ namespace {
 // longest wait (in polls) stays in the lane's `waitMax` and is published once per launch (PublishWait), off the
 // barrier's critical path.
 // The flag words lane t (< n) of block b uses in every barrier: the one it stores into on peer t, and the one peer t
-// stores into here. Computed once per launch (the pointer table is in kernel-argument memory, indexed per lane).
+// stores into here (the pointer table is in kernel-argument memory, indexed per lane).
 struct FlagLane {
     uint32_t* remote;
     uint32_t* mine;
@@ -770,7 +770,6 @@ __global__ __launch_bounds__(kIpcMaxThreads) void k_ipc_collective(IpcArgs a)
     // replay alike, starts where this one ended. Every rank runs the same launch sequence, so the counters agree.
     Stamp(a, me, kTrEntry);
     const uint32_t arrivedBefore = Arrive(a, epoch);
-    const FlagLane fl = LaneFlags(a, me);  // after the arrival, whose issue would otherwise wait for this lane's load
     uint32_t waitMax = 0;
     for (uint32_t k = 0; k < a.rounds; ++k) {
         const uint64_t kP = uint64_t(k) * a.piece;
@@ -787,6 +786,9 @@ __global__ __launch_bounds__(kIpcMaxThreads) void k_ipc_collective(IpcArgs a)
             });
         }
         Stamp(a, me, kTrPhase0);
+        // this lane's flag words, loaded behind the phase's stores: the barrier's drain waits for both at once
+        // (computed before the push, the per-lane pointer load held up the first store by a memory round trip)
+        const FlagLane fl = LaneFlags(a, me);
         if (!Barrier(a, fl, ++epoch, waitMax)) break;
         Stamp(a, me, kTrBarrier1);
         if (kind == kIpcAllGather) {
