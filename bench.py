@@ -319,8 +319,13 @@ def ipc_two_shot_roofline(dev, n: int = 2, mib: int = 512, reps: int = 10) -> di
 
     # phase stamps on (read at the world's IPC set-up): each launch's own span, first block in to last block out, is
     # the kernel's duration; the HIP events between calls also hold the loopback world's cross-stream hand-offs
-    prev_trace = os.environ.get("HCCL_AMD_IPC_TRACE")
+    prev = {k: os.environ.get(k) for k in ("HCCL_AMD_IPC_TRACE", "HCCL_BUFFSIZE", "HCCL_AMD_IPC_STAGING_MIB")}
     os.environ["HCCL_AMD_IPC_TRACE"] = "1"
+    # the large staging tier's areas are HCCL_BUFFSIZE / 2 (the reference's 2 x HCCL_BUFFSIZE for the four): a caller
+    # that moves 512 MiB per call sets HCCL_BUFFSIZE to 1024, as on the reference, and each call is one staging round
+    # (the rows before r06 ran with 512 MiB areas, the default then)
+    os.environ["HCCL_BUFFSIZE"] = "1024"
+    os.environ.pop("HCCL_AMD_IPC_STAGING_MIB", None)
     comms = H.loopback_world(n)
     count = (mib << 20) // 4
     g = torch.Generator(device=dev).manual_seed(0x5EED0009)
@@ -338,10 +343,11 @@ def ipc_two_shot_roofline(dev, n: int = 2, mib: int = 512, reps: int = 10) -> di
 
         call()  # set-up (staging, peer pointers) on the first call
         torch.cuda.synchronize()
-        if prev_trace is None:
-            os.environ.pop("HCCL_AMD_IPC_TRACE")
-        else:
-            os.environ["HCCL_AMD_IPC_TRACE"] = prev_trace
+        for k, v in prev.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
         evs[0].record(streams[0])
         for k in range(reps):
@@ -369,6 +375,7 @@ def ipc_two_shot_roofline(dev, n: int = 2, mib: int = 512, reps: int = 10) -> di
     traffic, source = pmc_traffic("ipc_two_shot")
     return {"kernel": "k_ipc_collective<EFp<float>, SUM> (two-shot AllReduce, loopback world)", "ranks": n,
             "bytes_per_rank": count * 4, "ran": ran, "algorithmic_bytes_per_launch": nbytes,
+            "staging": "HCCL_BUFFSIZE=1024: large-tier areas of 512 MiB, one staging round per call",
             "kernel_avg_us": round(kavg * 1e6, 1), "kernel_median_us": round(float(np.median(per)) * 1e6, 1),
             "kernel_timing": "each launch's span from its blocks' s_memrealtime stamps (first entry to last exit; "
                              "HCCL_AMD_IPC_TRACE), one launch per call",
@@ -607,6 +614,9 @@ def rccl_allreduce_reference(send, recv, world, args):
             for req in dist.batch_isend_irecv(ops) if ops else ():
                 req.wait()
 
+        if dist.get_world_size() < 2:
+            out["link_probe"] = {"skipped": "one rank (the self-loop stand-in): no link to probe"}
+            return out
         try:
             t = _timed(lambda: p2p(False), 3)
             out["link_probe"] = {"pair": [0, 1], "bytes": nbytes, "one_way_GBps": round(nbytes / t / 1e9, 2)}
@@ -841,9 +851,11 @@ def bench_fold_piece(comm, send, recv, world) -> dict:
     out = {"note": "per rank: the second of two calls, eager; fold durations are HIP-event brackets of each fold launch"}
     comm.set_config(H.Config.FOLD_TIMING, 1)
     try:
-        for name, call in (("c3_mesh_chunk", lambda: comm.all_reduce(send, recv, H.HcclReduceOp.SUM, s)),
-                           ("c4_rs_mesh_chunk", lambda: comm.reduce_scatter(x, shard, H.HcclReduceOp.SUM, s))):
-            comm.set_algo(H.Algo.MESH_CHUNK)
+        for name, algo, call in (
+                ("c3_mesh_chunk", H.Algo.MESH_CHUNK, lambda: comm.all_reduce(send, recv, H.HcclReduceOp.SUM, s)),
+                ("c3_ring", H.Algo.RING, lambda: comm.all_reduce(send, recv, H.HcclReduceOp.SUM, s)),
+                ("c4_rs_mesh_chunk", H.Algo.MESH_CHUNK, lambda: comm.reduce_scatter(x, shard, H.HcclReduceOp.SUM, s))):
+            comm.set_algo(algo)
             try:
                 call()
                 torch.cuda.synchronize()
@@ -867,6 +879,37 @@ def bench_fold_piece(comm, send, recv, world) -> dict:
     finally:
         comm.set_config(H.Config.FOLD_TIMING, 0)
         comm.set_algo(H.Algo.AUTO)
+    return out
+
+
+def recommend_data_paths(c3: dict, c5: dict) -> dict:
+    """Which data path each size range should default to, from the rows of one N > 1 line: the
+    two paths give the same bits within an order family, so the choice is free for parity. At C3's 4 GiB: the RCCL
+    schedule of each order family against its one-sided twin (MESH_CHUNK vs IPC, MESH_TWOSHOT vs IPC_TWOSHOT). Over
+    C5's sweep: per size, the faster of the auto schedule over RCCL (`auto`) and the one-sided kernel (`auto_default`
+    up to the small-call threshold, `ipc` above it), then maximal runs of sizes with the same winner. Rows that errored,
+    or whose path did not run what it names, are left out."""
+    out = {"c3": {}, "c5_ranges": [], "note": "faster path per order family / size range; same bits either way"}
+    for rccl, ipc in (("MESH_CHUNK", "IPC"), ("MESH_TWOSHOT", "IPC_TWOSHOT")):
+        a, b = (c3 or {}).get(rccl, {}), (c3 or {}).get(ipc, {})
+        if "ms" in a and "ms" in b and a.get("ran") == rccl and str(b.get("ran", "")).startswith("IPC"):
+            out["c3"][rccl.lower()] = {"rccl_ms": a["ms"], "one_sided_ms": b["ms"],
+                                       "choose": "one_sided" if b["ms"] < a["ms"] else "rccl"}
+    runs = []
+    for row in (c5 or {}).get("points", []):
+        rccl_us = row.get("auto_us") if not str(row.get("auto_ran", "IPC")).startswith("IPC") else None
+        ipc_us = None
+        for key in ("auto_default", "ipc"):
+            if str(row.get(f"{key}_ran", "")).startswith("IPC") and f"{key}_us" in row:
+                ipc_us = row[f"{key}_us"] if ipc_us is None else min(ipc_us, row[f"{key}_us"])
+        if rccl_us is None or ipc_us is None:
+            continue
+        choose = "one_sided" if ipc_us < rccl_us else "rccl"
+        if runs and runs[-1]["choose"] == choose:
+            runs[-1]["to_bytes"] = row["bytes"]
+        else:
+            runs.append({"from_bytes": row["bytes"], "to_bytes": row["bytes"], "choose": choose})
+    out["c5_ranges"] = runs
     return out
 
 
@@ -1099,6 +1142,13 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     # communicator is the IPC-only one (HcclAmdCommInitHostExchange, bootstrapped over the gloo group), so the N > 1
     # code path runs end to end; the RCCL-dependent rows then report HCCL_E_NOT_SUPPORT. Never used for results.
     harness = os.environ.get("HCCL_AMD_BENCH_HOST_EXCHANGE") == "1"
+    # HCCL_AMD_BENCH_SELFLOOP=1 is the RCCL stand-in on a one-GPU box: one process runs rank 0 of
+    # a `world`-rank run on a self-loop communicator (HcclAmdCommInitSelfLoop: rank 0's schedules through a one-rank
+    # RCCL communicator, every peer mapped onto itself), so every RCCL-path row of the N > 1 line (the ring headline,
+    # c3_schedules, fold_piece, c4, c5, the e2e bucket, RCCL's own all_reduce) runs its code path through RCCL's
+    # kernels before any 8-GPU node does. The data no longer means the collective: no result check, never a result.
+    selfloop = os.environ.get("HCCL_AMD_BENCH_SELFLOOP") == "1"
+    dist_world, dist_rank = (1, 0) if selfloop else (world, rank)
     if harness:
         local_rank = local_rank % max(1, torch.cuda.device_count())
         args.no_rccl_ref = True
@@ -1106,16 +1156,19 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     dev = torch.device("cuda", local_rank)
     with _stdout_to_stderr():  # gloo announces its connections on stdout, which carries only the JSON line
         # a rank lost on the host ends the others' gloo waits after 10 minutes, not gloo's default 30
-        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=600))
+        dist.init_process_group("gloo", rank=dist_rank, world_size=dist_world,
+                                timeout=datetime.timedelta(seconds=600))
 
     def _all_gather(b):
-        out = [None] * world
+        out = [None] * dist_world
         dist.all_gather_object(out, b)
         return out
 
     def new_comm():
         if harness:
             return H.comm_init_host_exchange(world, rank, _all_gather)
+        if selfloop:
+            return H.comm_init_selfloop(world, 0)
         # root info out of band, exactly as the reference's callers do (examples/.../01_allreduce/main.cc:122-136)
         obj = [H.get_root_info() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
@@ -1165,7 +1218,7 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
         warm(comm, headline)
     dist.barrier()
     torch.cuda.synchronize()
-    comm_mem = torch.tensor([_device_memory_outside_torch() - mem0], dtype=torch.float64)
+    comm_mem = torch.tensor([_device_memory_outside_torch() - mem0, comm.device_bytes()], dtype=torch.float64)
     dist.all_reduce(comm_mem, op=dist.ReduceOp.MAX)
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     e0, e1 = evs[0], evs[-1]
@@ -1212,7 +1265,7 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     torch.cuda.synchronize()
     ok = torch.tensor([1 if torch.equal(recv, (check * world + world * (world - 1) // 2).to(recv.dtype)) else 0])
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-    result_ok = bool(ok.item())
+    result_ok = None if selfloop else bool(ok.item())  # a self loop's data does not mean the AllReduce
     del check
     graph_launches, graph_captures = comm.graph_stats()
     comm.destroy()
@@ -1231,7 +1284,9 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic (uniform [-1,1) fp32, device-generated)" + (
-            "; HARNESS MODE (all ranks on one GPU, IPC-only communicator): not a result" if harness else ""),
+            "; HARNESS MODE (all ranks on one GPU, IPC-only communicator): not a result" if harness else "") + (
+            f"; STAND-IN MODE (one GPU: rank 0's {world}-rank programs over a one-rank RCCL self loop): not a result"
+            if selfloop else ""),
         "config": {
             "workload": "C3: HcclAllReduce fp32 SUM, 4 GiB per rank, RCCL send/recv over xGMI + HIP reduce kernels",
             "bytes_per_rank": C3_BYTES,
@@ -1245,16 +1300,19 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
                     "p90": round(float(np.percentile(steps_ms.numpy(), 90)), 3),
                     "note": "per-step HIP-event durations on the launch stream, max over ranks per step"},
         "transport": dict(_transport_info(), device_memory={
-            "communicator_GiB": round(float(comm_mem.item()) / GIB, 3),
-            "note": "device memory in use outside torch's caching allocator after the headline warm-up minus before "
-                    "the communicator (RCCL's per-peer channel buffers + this library's staging and scratch), max over "
-                    "ranks"}),
+            "library_GiB": round(float(comm_mem[1]) / GIB, 3),
+            # ranks sharing one GPU (the harness) see each other's tensors in the device-wide figure: none then
+            "device_outside_torch_GiB": None if harness else round(float(comm_mem[0]) / GIB, 3),
+            "note": "library_GiB: the bytes this library holds for the headline communicator after its warm-up "
+                    "(HcclAmdCommDeviceBytes: executor staging + the one-sided kernel's allocations), max over ranks; "
+                    "device_outside_torch_GiB: device memory in use outside torch's caching allocator after the warm-up "
+                    "minus before the communicator (adds RCCL's per-peer channel buffers), max over ranks"}),
         "executor_graphs": {"launches": graph_launches, "captures": graph_captures,
                             "note": "rank 0's calls served by one hipGraphLaunch of the captured executor program "
                                     "(HCCL_AMD_GRAPH_CACHE); the first call of a shape runs eagerly"},
         "per_gpu": {"workload": "C3", "bytes_per_gpu_per_step": C3_BYTES, "algbw_GBps": round(algbw, 2),
                     "busbw_GBps": round(busbw, 2), "bound": "xgmi", "roofline_peak_GBps": round(xgmi_peak, 1),
-                    "frac": None if harness else round(busbw / xgmi_peak, 4)},
+                    "frac": None if (harness or selfloop) else round(busbw / xgmi_peak, 4)},
         "result_ok": result_ok,
         "result_ok_algorithm": verified_algo,
         "headline_fallback": fallback,
@@ -1265,12 +1323,19 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
             "achieved": round(busbw, 2),
             "peak": round(xgmi_peak, 1),
             "unit": "GB/s",
-            "frac": None if harness else round(busbw / xgmi_peak, 4),  # one shared GPU has no xGMI in the path
+            # one shared GPU has no xGMI in the path
+            "frac": None if (harness or selfloop) else round(busbw / xgmi_peak, 4),
             "traffic": None,
             "note": f"busbw = algbw*2(n-1)/n against the {world - 1} direct xGMI links a rank has to its peers "
                     "x 76.8 GB/s per direction (fully connected node: one link per peer)",
         },
     }
+    if selfloop:
+        res["n_gpus"] = 1
+        res["config"]["parallelism"] = f"self loop standing in for rank 0 of {world}"
+        res["stand_in"] = {"virtual_ranks": world, "physical_gpus": 1,
+                           "note": "HCCL_AMD_BENCH_SELFLOOP=1: every RCCL-path row of the N > 1 line runs its code "
+                                   "through RCCL's kernels on one GPU; times and data are the self loop's, not xGMI's"}
     # Secondary configs and the RCCL reference run under a watchdog: a collective that never returns there (a first
     # run of some schedule on real hardware) must not cost the headline line. At the deadline every rank stops, rank
     # 0 printing the result with what finished so far.
@@ -1298,6 +1363,10 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
                         cm.destroy()
                     except Exception as e:  # noqa: BLE001
                         extra.setdefault(name, {})["destroy_error"] = f"{type(e).__name__}: {e}"
+    try:
+        extra["data_path_choice"] = recommend_data_paths(extra.get("c3_schedules"), extra.get("c5"))
+    except Exception as e:  # noqa: BLE001
+        extra["data_path_choice"] = {"error": f"{type(e).__name__}: {e}"}
     if not args.no_rccl_ref:
         wd.stage("rccl_allreduce_reference")
         res["rccl_allreduce_reference"] = rccl_allreduce_reference(send, recv, world, args)
@@ -1324,7 +1393,9 @@ _PRINT_LOCK = threading.Lock()
 EXIT_FAILED = 3
 EXIT_WATCHDOG = 4
 EXIT_WRONG_RESULT = 5
+EXIT_REFUSED = 6  # the run's shape does not match the machine or the launch (_refuse); nothing was measured
 _EXIT_CODE = 0
+METRIC = "device-resident reduce GiB/s (fp32 sum) vs HBM peak; ring all-reduce bus GB/s"
 
 
 def emit(res: dict) -> None:
@@ -1366,6 +1437,94 @@ class _Watchdog:
         os._exit(EXIT_WATCHDOG)
 
 
+def _refuse(args, why: str, world=None) -> None:
+    """Prints the refusal line (value null: nothing was measured) and exits with EXIT_REFUSED."""
+    print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": args.gpus, "steps": args.steps,
+                      "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "weak",
+                      "vs_baseline": None, "dtype": "fp32", "data": "none (refused before any measurement)",
+                      "config": {"workload": "C3" if args.gpus > 1 else "C2"},
+                      "error": {"refused": why, "world_size_env": world,
+                                "device_count": _device_count()}}), flush=True)
+    sys.exit(EXIT_REFUSED)
+
+
+def _device_count() -> int:
+    # counting devices does not initialise the GPU on this stack (torch reads the count without creating a context),
+    # so the launcher may call it before it starts the ranks
+    try:
+        return int(torch.cuda.device_count())
+    except Exception:  # noqa: BLE001
+        return 0
+
+
+def _harness() -> bool:
+    return os.environ.get("HCCL_AMD_BENCH_HOST_EXCHANGE") == "1"
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_command(gpus: int, argv, port: int):
+    """The command the launcher starts for `bench.py --gpus N` without WORLD_SIZE: one rank per GPU under
+    torch.distributed.run on this node, rendezvous on 127.0.0.1, the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def launch_ranks(args, argv) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: the parent makes no GPU call, starts N rank processes
+    (torch.distributed.run) as a child, relays rank 0's JSON line to stdout and everything else to stderr, and exits
+    with the child's code. The reference's callers run one rank per device the same way (examples/02_collectives/
+    01_allreduce/main.cc:113-136)."""
+    import subprocess
+
+    cmd = launch_command(args.gpus, argv, _free_port())
+    log("[bench] launching", " ".join(cmd))
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
+    for line in proc.stdout:
+        (sys.stdout if line.startswith("{") else sys.stderr).write(line)
+        sys.stdout.flush()
+    return proc.wait()
+
+
+def check_launch(args):
+    """The run's shape against the launch and the machine. Returns "launch" when this process
+    must start the ranks, "local" for the N = 1 line, "rank" for one rank of an N > 1 run; refuses (exit EXIT_REFUSED,
+    one JSON line from rank 0) when --gpus disagrees with WORLD_SIZE, or when the node has fewer GPUs than ranks
+    (unless HCCL_AMD_BENCH_HOST_EXCHANGE=1 puts every rank on one GPU, the harness that is never a result)."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus < 1:
+        _refuse(args, f"--gpus {args.gpus}: at least one GPU")
+    if env_world is None:
+        if args.gpus == 1:
+            return "local"
+        if os.environ.get("HCCL_AMD_BENCH_SELFLOOP") == "1":
+            # the RCCL stand-in: this one process runs rank 0 of the --gpus N line over a self loop (never a result)
+            if _device_count() < 1:
+                _refuse(args, "the self-loop stand-in needs one GPU; this node has none")
+            return "selfloop"
+        if not _harness() and _device_count() < args.gpus:
+            _refuse(args, f"--gpus {args.gpus} but this node has {_device_count()} GPU(s)")
+        return "launch"
+    world = int(env_world)
+    rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        if rank == 0:
+            _refuse(args, f"WORLD_SIZE={world} but --gpus {args.gpus}: one rank per GPU", world)
+        sys.exit(EXIT_REFUSED)
+    need = 1 if _harness() else world
+    if _device_count() < need:
+        if rank == 0:
+            _refuse(args, f"{world} rank(s) but this node has {_device_count()} GPU(s)", world)
+        sys.exit(EXIT_REFUSED)
+    return "local" if world == 1 else "rank"
+
+
 def main():
     import faulthandler
 
@@ -1387,9 +1546,17 @@ def main():
     p.add_argument("--cpu-budget", type=float, default=12.0)
     p.add_argument("--algo", default="", help="N>1: the headline AllReduce schedule (default ring; mesh_chunk is the "
                                               "reference's own selection at 4 GiB, auto, rhd, ipc ...)")
-    args = p.parse_args()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1:
+    argv = sys.argv[1:]
+    args = p.parse_args(argv)
+    mode = check_launch(args)
+    if mode == "launch":
+        sys.exit(launch_ranks(args, argv))
+    if mode == "selfloop":
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        res = bench_allreduce(args, 0, args.gpus, 0)
+    elif mode == "rank":
+        world = int(os.environ["WORLD_SIZE"])
         rank = int(os.environ["RANK"])
         res = bench_allreduce(args, rank, world, int(os.environ.get("LOCAL_RANK", rank)))
     else:

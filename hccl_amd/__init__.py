@@ -99,12 +99,6 @@ def set_reduce_launch(blocks_per_cu: int = 0, unroll: int = 0, cache_policy: int
     check("HcclAmdSetReduceLaunch", lib.HcclAmdSetReduceLaunch(blocks_per_cu, unroll, cache_policy))
 
 
-def set_device_copy_kernel(on: bool = True) -> None:
-    """Process-wide: device copies by the library's copy kernel (True, the default) or hipMemcpyAsync (False;
-    diagnostics). HcclAmdSetDeviceCopyKernel."""
-    check("HcclAmdSetDeviceCopyKernel", lib.HcclAmdSetDeviceCopyKernel(1 if on else 0))
-
-
 def set_fold_mode(mode: int = 0) -> None:
     """Operand pipelining of the n-ary fold (0 default, 1 serial, 2 prefetch, 3 all operands first);
     see HcclAmdSetFoldMode in include/hccl_amd.h."""
@@ -287,6 +281,12 @@ class Comm:
         check("HcclAmdCommScratch", lib.HcclAmdCommScratch(self.handle, ctypes.byref(p), ctypes.byref(b)))
         return p.value or 0, b.value
 
+    def device_bytes(self) -> int:
+        """Device bytes the library holds for this communicator now (HcclAmdCommDeviceBytes)."""
+        b = ctypes.c_uint64(0)
+        check("HcclAmdCommDeviceBytes", lib.HcclAmdCommDeviceBytes(self.handle, ctypes.byref(b)))
+        return b.value
+
     def compile_stats(self) -> tuple:
         """(hits, misses) of the communicator's compiled-collective cache (HcclAmdCommCompileStats)."""
         h, m = ctypes.c_uint64(0), ctypes.c_uint64(0)
@@ -372,6 +372,15 @@ def comm_init_root_info(n_ranks: int, root_info: bytes, rank: int) -> Comm:
     ctypes.memmove(ctypes.addressof(ri), root_info, HCCL_ROOT_INFO_BYTES)
     h = ctypes.c_void_p(0)
     check("HcclCommInitRootInfo", lib.HcclCommInitRootInfo(n_ranks, ctypes.byref(ri), rank, ctypes.byref(h)))
+    return Comm(h.value)
+
+
+def comm_init_selfloop(n_ranks: int, rank: int = 0) -> Comm:
+    """A one-GPU stand-in for rank `rank` of an n_ranks world: its schedules run through a one-rank RCCL communicator
+    with every peer mapped onto itself (HcclAmdCommInitSelfLoop; harnesses only: the data no longer means the
+    collective)."""
+    h = ctypes.c_void_p(0)
+    check("HcclAmdCommInitSelfLoop", lib.HcclAmdCommInitSelfLoop(n_ranks, rank, ctypes.byref(h)))
     return Comm(h.value)
 
 

@@ -102,7 +102,6 @@ class Config(enum.IntEnum):
     IPC_TILE_KIB = 10
     IPC_TIMEOUT_MS = 11
     IPC_STAGING_MIB = 12
-    IPC_STAGING_CACHED = 13
     IPC_TRACE = 14
     IPC_L2_SCRUB = 15
     FOLD_TIMING = 16
@@ -215,7 +214,6 @@ SIGNATURES = {
     "HcclAmdCommSetConfig": (_res, [_vp, _i32, ctypes.c_int64]),
     "HcclAmdCommGetConfig": (_res, [_vp, _i32, ctypes.POINTER(ctypes.c_int64)]),
     "HcclAmdCommReloadConfig": (_res, [_vp]),
-    "HcclAmdSetDeviceCopyKernel": (_res, [_i32]),
     "HcclAmdCommFoldTiming": (_res, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64), ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_double)]),
     "HcclAmdCommCompileStats": (_res, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
@@ -233,6 +231,8 @@ SIGNATURES = {
     "HcclAmdBootstrapExchangeId": (_res, [ctypes.c_char_p, _u32, _vp]),
     "HcclAmdCommPendingDestroys": (_u32, []),
     "HcclAmdCommScratch": (_res, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_u64)]),
+    "HcclAmdCommDeviceBytes": (_res, [_vp, ctypes.POINTER(_u64)]),
+    "HcclAmdCommInitSelfLoop": (_res, [_u32, _u32, ctypes.POINTER(_vp)]),
     "HcclAmdL2Maintain": (_res, [_vp]),
     "HcclAmdRcclP2pChannels": (_res, [ctypes.POINTER(_u32), ctypes.POINTER(_u32)]),
     "HcclAmdDiagReadByXcc": (_res, [_vp, _vp, _u64, _i32, _vp, _vp]),

@@ -93,12 +93,6 @@ using namespace hccl_amd;
 
 extern "C" {
 
-HcclResult HcclAmdSetDeviceCopyKernel(int32_t on)
-{
-    SetDeviceCopyByKernel(on != 0);
-    return HCCL_SUCCESS;
-}
-
 HcclResult HcclAmdLocalReduce(void* dst, const void* src, uint64_t count, HcclDataType dataType, HcclReduceOp op,
                               aclrtStream stream)
 {

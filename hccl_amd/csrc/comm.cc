@@ -48,33 +48,43 @@ HcclResult Comm::Init(int dev)
     // the link stream gets the higher priority: its kernels are short and gate every peer
     HIP_CHK(hipStreamCreateWithPriority(&commStream, hipStreamNonBlocking, hi));
     HIP_CHK(hipStreamCreateWithPriority(&reduceStream, hipStreamNonBlocking, lo));
-    if (nRanks > 1) {
-        cclBytes = CclBytesDefault();
-        scratchBytes = 2 * cclBytes;
-        HIP_CHK(hipMalloc(&scratch, scratchBytes));
+    // the executor's staging is allocated by the first program that needs it (EnsureScratch)
+    cclBytes = CclBytesDefault();
+    scratchBytes = 2 * cclBytes;
+    return HCCL_SUCCESS;
+}
+
+HcclResult Comm::EnsureScratch()
+{
+    if (scratch != nullptr) return HCCL_SUCCESS;
+    HIP_CHK(hipSetDevice(device));
+    // A first program may be issued under the caller's stream capture: an allocation is not a stream operation, and
+    // the relaxed mode lets this thread make it whatever capture mode the caller chose (as a library's lazily made
+    // workspace must).
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    HIP_CHK(hipThreadExchangeStreamCaptureMode(&mode));
+    const hipError_t e = hipMalloc(&scratch, scratchBytes);
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+    if (e != hipSuccess) {
+        scratch = nullptr;
+        HCCL_AMD_ERR("rank %u: executor staging of %llu B: %s", rank, (unsigned long long)scratchBytes,
+                     hipGetErrorString(e));
+        return HCCL_E_MEMORY;
     }
     return HCCL_SUCCESS;
 }
 
+uint64_t Comm::DeviceBytes() const { return (scratch != nullptr ? scratchBytes : 0) + IpcDeviceBytes(*this); }
+
 // The executor's ordering events (a program's start, its cross-stream unit events and stream joins) keep the runtime's
 // default system-scope fence: unlike the communicator's tail (EntryScope), they order data one stream's kernel or
-// transport group wrote before another stream's kernel reads it. HCCL_AMD_EXECUTOR_EVENT_FENCE=0 (read once; a
-// diagnostic) creates them with hipEventDisableSystemFence, to measure what the fences cost a program.
-static unsigned ExecutorEventFlags()
-{
-    static const unsigned flags = [] {
-        const char* e = std::getenv("HCCL_AMD_EXECUTOR_EVENT_FENCE");
-        const bool off = e != nullptr && std::strcmp(e, "0") == 0;
-        return off ? unsigned(hipEventDisableTiming | hipEventDisableSystemFence) : unsigned(hipEventDisableTiming);
-    }();
-    return flags;
-}
-
+// transport group wrote before another stream's kernel reads it (r05 measured them fence-free within 1 % behind RCCL
+// groups and kept them).
 HcclResult Comm::NextEvent(hipEvent_t* e)
 {
     if (nextEvent == events.size()) {
         hipEvent_t ev;
-        HIP_CHK(hipEventCreateWithFlags(&ev, ExecutorEventFlags()));
+        HIP_CHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         events.push_back(ev);
     }
     *e = events[nextEvent++];
@@ -162,6 +172,7 @@ Comm::~Comm()
     if (reduceStream != nullptr) (void)hipStreamDestroy(reduceStream);
     if (stallHost != nullptr) (void)hipHostFree(stallHost);
     if (tail != nullptr) (void)hipEventDestroy(tail);
+    XSentinelCheck("destroy");
     TeardownTrace(rank, "done", false);
 }
 
@@ -180,16 +191,6 @@ HcclResult FromNccl(ncclResult_t r, const char* what)
         case ncclRemoteError: return HCCL_E_REMOTE;
         default: return HCCL_E_INTERNAL;
     }
-}
-
-// HCCL_AMD_RCCL_BLOCKING=1 creates blocking RCCL communicators (the pre-r03 behaviour; diagnostics). By default they
-// are non-blocking (ncclConfig_t::blocking = 0): a call that must wait for a peer (communicator set-up, the first
-// message to a peer, finalize) returns ncclInProgress and the wait is ours to bound, where a blocking call would hang
-// the host on a lost peer.
-bool RcclBlocking()
-{
-    const char* e = std::getenv("HCCL_AMD_RCCL_BLOCKING");
-    return e != nullptr && std::strcmp(e, "1") == 0;
 }
 
 // Polls a non-blocking communicator until the call that returned `r` has finished, at most boundMs (0 = no bound).
@@ -214,7 +215,8 @@ ncclResult_t WaitSettled(ncclComm_t comm, ncclResult_t r, uint64_t boundMs)
 
 class RcclTransport : public Transport {
 public:
-    explicit RcclTransport(ncclComm_t comm) : comm_(comm) {}
+    // selfLoop: a one-rank RCCL communicator standing in for every peer (HcclAmdCommInitSelfLoop)
+    explicit RcclTransport(ncclComm_t comm, bool selfLoop = false) : comm_(comm), selfLoop_(selfLoop) {}
     ~RcclTransport() override
     {
         std::lock_guard<std::mutex> lk(mu_);
@@ -238,9 +240,29 @@ public:
     {
         std::lock_guard<std::mutex> lk(mu_);
         if (comm_ == nullptr) return HCCL_E_SUSPENDING;  // aborted by the watchdog
+        std::vector<P2pOp> paired;
+        const std::vector<P2pOp>* post = &ops;
+        if (selfLoop_) {
+            // every peer is this rank: each send is posted beside a receive of the same size, since RCCL pairs
+            // messages to itself in posting order
+            std::vector<P2pOp> recvs;
+            for (const P2pOp& o : ops) {
+                if (!o.isSend) recvs.push_back(o);
+            }
+            for (const P2pOp& o : ops) {
+                if (!o.isSend) continue;
+                auto it = std::find_if(recvs.begin(), recvs.end(), [&](const P2pOp& q) { return q.bytes == o.bytes; });
+                if (it == recvs.end()) return HCCL_E_NOT_SUPPORT;
+                paired.push_back({true, 0, o.ptr, o.bytes});
+                paired.push_back({false, 0, it->ptr, it->bytes});
+                recvs.erase(it);
+            }
+            if (!recvs.empty()) return HCCL_E_NOT_SUPPORT;
+            post = &paired;
+        }
         ncclResult_t r = ncclGroupStart();
         if (r != ncclSuccess) return FromNccl(r, "ncclGroupStart");
-        for (const P2pOp& o : ops) {
+        for (const P2pOp& o : *post) {
             r = o.isSend ? ncclSend(o.ptr, o.bytes, ncclUint8, static_cast<int>(o.peer), comm_, stream)
                          : ncclRecv(o.ptr, o.bytes, ncclUint8, static_cast<int>(o.peer), comm_, stream);
             if (r != ncclSuccess && r != ncclInProgress) {
@@ -256,6 +278,14 @@ public:
     {
         std::lock_guard<std::mutex> lk(mu_);
         localTeardown_ = on;
+    }
+    // hands the RCCL communicator over (to a transport of another kind around it)
+    ncclComm_t Release()
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        ncclComm_t c = comm_;
+        comm_ = nullptr;
+        return c;
     }
     // From the watchdog thread. The communicator is taken out under the lock and aborted outside it: RCCL's abort
     // raises the kernels' abort flag at once but then waits for the graphs holding its plans (the executor graph cache,
@@ -282,6 +312,7 @@ public:
     }
     HcclResult AllGatherHost(const void* mine, size_t bytes, void* all) override
     {
+        if (selfLoop_) return HCCL_E_NOT_SUPPORT;  // no peers to exchange with (the one-sided kernel is unavailable)
         std::lock_guard<std::mutex> lk(mu_);
         if (comm_ == nullptr) return HCCL_E_SUSPENDING;
         int n = 0;
@@ -344,6 +375,7 @@ private:
     }
     std::mutex mu_;
     ncclComm_t comm_;
+    bool selfLoop_ = false;
     bool localTeardown_ = false;
 };
 
@@ -418,12 +450,23 @@ void RcclP2pChannels(uint32_t* perPeer, uint32_t* minP2p)
     *minP2p = g_p2pMin;
 }
 
+std::unique_ptr<Transport> MakeRcclSelfLoopTransport(HcclResult* err)
+{
+    ncclUniqueId id;
+    *err = FromNccl(ncclGetUniqueId(&id), "ncclGetUniqueId");
+    if (*err != HCCL_SUCCESS) return nullptr;
+    std::unique_ptr<Transport> t = MakeRcclTransport(&id, 1, 0, err);
+    if (t == nullptr) return nullptr;
+    auto* rc = static_cast<RcclTransport*>(t.get());
+    return std::make_unique<RcclTransport>(rc->Release(), true);
+}
+
 std::unique_ptr<Transport> MakeRcclTransport(void* uniqueId, uint32_t nRanks, uint32_t rank, HcclResult* err)
 {
     ncclUniqueId id;
     std::memcpy(&id, uniqueId, sizeof id);
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-    cfg.blocking = RcclBlocking() ? 1 : 0;
+    cfg.blocking = 0;  // non-blocking: every wait on a peer returns ncclInProgress and is ours to bound
     ncclComm_t comm = nullptr;
     ncclResult_t r = ncclCommInitRankConfig(&comm, static_cast<int>(nRanks), id, static_cast<int>(rank), &cfg);
     if (comm != nullptr) r = WaitSettled(comm, r, ConnectTimeoutMs());
@@ -449,7 +492,7 @@ HcclResult MakeRcclTransportsAll(uint32_t ndev, const int32_t* devices, std::vec
     ncclUniqueId id;
     HCCL_CHK(FromNccl(ncclGetUniqueId(&id), "ncclGetUniqueId"));
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-    cfg.blocking = RcclBlocking() ? 1 : 0;
+    cfg.blocking = 0;  // non-blocking: every wait on a peer returns ncclInProgress and is ours to bound
     std::vector<ncclComm_t> comms(ndev, nullptr);
     int dev0 = 0;
     HIP_CHK(hipGetDevice(&dev0));
@@ -495,11 +538,7 @@ public:
         bool consumed = false;
         bool failed = false;
     };
-    explicit LoopbackWorld(uint32_t n) : n_(n), boxes_(size_t(n) * n), slots_(n)
-    {
-        const char* e = std::getenv("HCCL_AMD_LOOPBACK_EVENT_DESTROY");  // diagnostics, read once per world
-        immediateDestroy_ = e != nullptr && std::strcmp(e, "immediate") == 0;
-    }
+    explicit LoopbackWorld(uint32_t n) : n_(n), boxes_(size_t(n) * n), slots_(n) {}
     ~LoopbackWorld()
     {
         // every rank's communicator has drained its streams before it released the world (~Comm)
@@ -527,19 +566,15 @@ public:
     // Events of the links, retired once both sides have enqueued their waits on them. They were destroyed at once
     // before r05, right after another thread's stream had been told to wait on them: HIP may hand a
     // destroyed event's completion signal to a new event while a wait on it is still queued. They now live until the
-    // world is torn down; past kRetiredMax the oldest completed ones go, far behind any wait still queued.
-    // HCCL_AMD_LOOPBACK_EVENT_DESTROY=immediate restores the old lifetime (the r05 experiment).
+    // world is torn down; past kRetiredMax the oldest completed ones go, far behind any wait still queued (r05 showed
+    // the old lifetime was not the cause of the r03 stale operands, DESIGN.md §5b, but this is the lifetime HIP's
+    // contract wants).
     static constexpr size_t kRetiredMax = 16384;
-    bool immediateDestroy_ = false;
     std::deque<hipEvent_t> retired_;
 
     void Retire(hipEvent_t e)  // mu_ not held
     {
         if (e == nullptr) return;
-        if (immediateDestroy_) {
-            (void)hipEventDestroy(e);
-            return;
-        }
         std::lock_guard<std::mutex> lk(mu_);
         retired_.push_back(e);
         while (retired_.size() > kRetiredMax && hipEventQuery(retired_.front()) == hipSuccess) {

@@ -63,6 +63,9 @@ public:
 };
 
 std::unique_ptr<Transport> MakeRcclTransport(void* uniqueId, uint32_t nRanks, uint32_t rank, HcclResult* err);
+// A one-rank RCCL communicator standing in for every peer of a larger world (HcclAmdCommInitSelfLoop): each group's
+// sends are posted beside receives of the same size.
+std::unique_ptr<Transport> MakeRcclSelfLoopTransport(HcclResult* err);
 // One RCCL communicator per listed device, all in this process (ncclCommInitAll); (*out)[r] is rank r.
 HcclResult MakeRcclTransportsAll(uint32_t ndev, const int32_t* devices, std::vector<std::unique_ptr<Transport>>* out);
 HcclResult RcclGetUniqueId(void* id128);
@@ -204,9 +207,9 @@ struct Comm {
     std::unique_ptr<Transport> transport;
     hipStream_t commStream = nullptr;
     hipStream_t reduceStream = nullptr;
-    void* scratch = nullptr;
+    void* scratch = nullptr;    // executor staging, nullptr until EnsureScratch
     uint64_t cclBytes = 0;      // HCCL_BUFFSIZE: sizes the executor loops (ScheduleParams::cclBytes)
-    uint64_t scratchBytes = 0;  // 2 x cclBytes
+    uint64_t scratchBytes = 0;  // 2 x cclBytes (the staging's size once allocated)
     int32_t algoOverride = HCCL_AMD_ALGO_AUTO;
     uint64_t pieceBytes = 0;
     int32_t lastAlgo = -1;
@@ -279,6 +282,12 @@ struct Comm {
     hipStream_t tailStream = nullptr;
 
     HcclResult Init(int dev);
+    // The executor's staging (2 x HCCL_BUFFSIZE), allocated by the first schedule program that runs: a communicator
+    // whose calls all go to the one-sided kernel never holds it.
+    HcclResult EnsureScratch();
+    // Device bytes the library holds for this communicator now (executor staging + the IPC path's allocations; RCCL's
+    // own buffers are not counted). HcclAmdCommDeviceBytes.
+    uint64_t DeviceBytes() const;
     // After the transport is set: the watchdog for an Abortable transport and the fault-injection hook.
     HcclResult StartWatchdog();
     HcclResult NextEvent(hipEvent_t* e);
@@ -313,6 +322,10 @@ int32_t SelectAivPlan(int32_t opType, uint32_t n, uint64_t count, HcclDataType d
 // Collective: every rank's IPC kernels have finished before any rank unmaps or frees (called by ~Comm).
 void IpcQuiesce(Comm& c);
 void IpcRelease(Comm& c);
+// The area sizes of staging tier t (kIpcTierSmall / kIpcTierLarge) for c: a function of the rank count and the (=)
+// configuration, so equal on every rank. IpcDeviceBytes: the device bytes c's IPC path holds now.
+IpcTier IpcTierSizes(const Comm& c, int t);
+uint64_t IpcDeviceBytes(const Comm& c);
 
 Comm* AsComm(HcclComm c);
 

@@ -72,9 +72,8 @@ CommConfig ReadCommConfig()
     c.ipcThreads = EnvIs("HCCL_AMD_IPC_THREADS", "512", false) ? 512u : 256u;
     if (EnvU64("HCCL_AMD_IPC_TILE_KIB", &v) && v <= (1u << 20)) c.ipcTileBytes = v << 10;  // the setter's range
     c.ipcTimeoutMs = IpcTimeoutMsFromEnv();
-    // the staging allocation stays below 2 GiB (ipc.cc IpcSetup): areas of 16 .. 1000 MiB
+    // the staging allocation stays below 2 GiB (ipc.cc IpcSetupTier): areas of 16 .. 1000 MiB
     if (EnvU64("HCCL_AMD_IPC_STAGING_MIB", &v) && v >= 16 && v <= 1000) c.ipcStagingBytes = v << 20;
-    c.ipcStagingCached = EnvIs("HCCL_AMD_IPC_STAGING_CACHED", "1", false);
     c.ipcTrace = EnvIs("HCCL_AMD_IPC_TRACE", "1", false);
     c.ipcL2Scrub = !EnvIs("HCCL_AMD_IPC_L2_SCRUB", "0", false);
     c.foldTiming = EnvIs("HCCL_AMD_FOLD_TIMING", "1", false);
@@ -124,10 +123,9 @@ HcclResult SetConfigEntry(CommConfig& c, int32_t key, int64_t value)
             c.ipcTimeoutMs = static_cast<uint64_t>(value);
             break;
         case HCCL_AMD_CFG_IPC_STAGING_MIB:
-            if (!in(16, 1000)) return HCCL_E_PARA;
+            if (value != 0 && !in(16, 1000)) return HCCL_E_PARA;
             c.ipcStagingBytes = static_cast<uint64_t>(value) << 20;
             break;
-        case HCCL_AMD_CFG_IPC_STAGING_CACHED: if (!flag()) return HCCL_E_PARA; c.ipcStagingCached = value != 0; break;
         case HCCL_AMD_CFG_IPC_TRACE: if (!flag()) return HCCL_E_PARA; c.ipcTrace = value != 0; break;
         case HCCL_AMD_CFG_IPC_L2_SCRUB: if (!flag()) return HCCL_E_PARA; c.ipcL2Scrub = value != 0; break;
         case HCCL_AMD_CFG_FOLD_TIMING: if (!flag()) return HCCL_E_PARA; c.foldTiming = value != 0; break;
@@ -156,7 +154,6 @@ HcclResult GetConfigEntry(const CommConfig& c, int32_t key, int64_t* value)
         case HCCL_AMD_CFG_IPC_TILE_KIB: *value = static_cast<int64_t>(c.ipcTileBytes >> 10); break;
         case HCCL_AMD_CFG_IPC_TIMEOUT_MS: *value = static_cast<int64_t>(c.ipcTimeoutMs); break;
         case HCCL_AMD_CFG_IPC_STAGING_MIB: *value = static_cast<int64_t>(c.ipcStagingBytes >> 20); break;
-        case HCCL_AMD_CFG_IPC_STAGING_CACHED: *value = c.ipcStagingCached; break;
         case HCCL_AMD_CFG_IPC_TRACE: *value = c.ipcTrace; break;
         case HCCL_AMD_CFG_IPC_L2_SCRUB: *value = c.ipcL2Scrub; break;
         case HCCL_AMD_CFG_FOLD_TIMING: *value = c.foldTiming; break;

@@ -25,12 +25,13 @@ struct CommConfig {
     uint32_t ipcThreads = 256;                    // HCCL_AMD_IPC_THREADS (256 or 512)
     uint64_t ipcTileBytes = 0;                    // HCCL_AMD_IPC_TILE_KIB (0 = one window per block)
     uint64_t ipcTimeoutMs = 1091000;              // HCCL_AMD_IPC_TIMEOUT_MS, else HCCL_EXEC_TIMEOUT (AIV rule)
-    // HCCL_AMD_IPC_STAGING_MIB (read at the IPC set-up): the slot area per rank; the result area is as large, and so is
-    // each alternate slot area, so 2 GiB of uncached HBM per rank once a communicator makes its first IPC call. 512 MiB
-    // areas run the C3-sized calls in one staging round where 128 MiB areas took 2-4, 5-12 % faster at n = 2 and 4
-    // (profiles/r03_ipc_variant_ab_shapes.jsonl): each round costs two barriers and three phase fills and drains.
-    uint64_t ipcStagingBytes = 512ull << 20;
-    bool ipcStagingCached = false;                // HCCL_AMD_IPC_STAGING_CACHED (diagnostics)
+    // HCCL_AMD_IPC_STAGING_MIB (read when the one-sided kernel's large staging tier is set up, ipc.h IpcTier): the
+    // area size of that tier (four areas per rank); 0 = HCCL_BUFFSIZE / 2, so that the tier holds 2 x HCCL_BUFFSIZE
+    // like the reference's CCL buffer pair. Larger areas run large calls in fewer staging rounds (each round costs
+    // two barriers and three phase fills and drains: 512 MiB areas were 5-12 % faster than 128 MiB at n = 2 and 4 on
+    // C3-sized calls, profiles/r03_ipc_variant_ab_shapes.jsonl); a caller that wants that sets HCCL_BUFFSIZE, as on
+    // the reference.
+    uint64_t ipcStagingBytes = 0;
     bool ipcTrace = false;                        // HCCL_AMD_IPC_TRACE (diagnostics)
     bool ipcL2Scrub = true;                       // HCCL_AMD_IPC_L2_SCRUB
     bool foldTiming = false;                      // HCCL_AMD_FOLD_TIMING: time the executor's folds (diagnostics)

@@ -70,11 +70,9 @@ struct FoldSeg {
 HcclResult LaunchReduceNBatch(const FoldSeg* segs, uint32_t nseg, uint32_t nsrc, HcclDataType dt, HcclReduceOp op,
                               hipStream_t stream);
 
-// dst = src over `bytes` bytes on `stream`: this library's copy kernel, or hipMemcpyAsync with
-// HCCL_AMD_DEVICE_COPY=memcpy / HcclAmdSetDeviceCopyKernel(0) (reduce_kernels.hip; DESIGN.md §5b, device copies).
+// dst = src over `bytes` bytes on `stream`: every device-to-device copy the library makes is this copy kernel, never
+// hipMemcpyAsync (r04: the runtime copy's writes showed up late in the r03 order; DESIGN.md §5b, device copies).
 HcclResult LaunchCopyBytes(void* dst, const void* src, uint64_t bytes, hipStream_t stream);
-bool DeviceCopyByKernel();
-void SetDeviceCopyByKernel(bool on);
 
 // HCCL_EXEC_TIMEOUT in the reference's format (ParseExecTimeout, alg_env_config.cc:75-110): false when unset or
 // malformed, else *seconds (>= 0, <= UINT32_MAX, at most two decimals).

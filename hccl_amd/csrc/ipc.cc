@@ -8,6 +8,7 @@
 // as one launch (all ranks' blocks must be resident together, which separate per-rank launches on 4 hardware queues
 // would not guarantee).
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -53,70 +54,236 @@ bool UncachedAlloc(int device, void** ptr, size_t bytes)
     return hipExtMallocWithFlags(ptr, bytes, hipDeviceMallocUncached) == hipSuccess;
 }
 
+// EXPERIMENT (r06; removed after the run): HCCL_AMD_X_RELEASE = pool (default) | free |
+// scrubfree | sentinel. free: hipFree at release (the pre-pool behaviour); scrubfree: system-scope L2 write-back +
+// invalidate on every XCD, then hipFree; sentinel: keep the block, fill it with 0xA5A5A5A5 and check it at every later
+// set-up and at XSentinelCheck (a late writer into a released block changes it).
+int XMode()
+{
+    static const int m = [] {
+        const char* e = std::getenv("HCCL_AMD_X_RELEASE");
+        if (e == nullptr) return 0;
+        if (std::strcmp(e, "free") == 0) return 1;
+        if (std::strcmp(e, "scrubfree") == 0) return 2;
+        if (std::strcmp(e, "sentinel") == 0) return 3;
+        return 0;
+    }();
+    return m;
+}
+
+struct XBlock {
+    int device;
+    void* ptr;
+    size_t bytes;
+};
+std::vector<XBlock>& XKept()
+{
+    static auto* v = new std::vector<XBlock>;
+    return *v;
+}
+
+void XSentinelCheckLocked(const char* where)
+{
+    // blocks up to 64 MiB in full, larger ones by their first and last 4 MiB (a full 2 GiB copy per check is too slow)
+    constexpr size_t kPart = 4ull << 20;
+    for (const XBlock& b : XKept()) {
+        const bool whole = b.bytes <= (64ull << 20);
+        size_t bad = 0, first = 0;
+        uint32_t firstVal = 0;
+        for (int part = 0; part < (whole ? 1 : 2); ++part) {
+            const size_t off = whole ? 0 : (part == 0 ? 0 : b.bytes - kPart);
+            const size_t len = whole ? b.bytes : kPart;
+            std::vector<uint32_t> h(len / 4);
+            if (hipMemcpy(h.data(), static_cast<char*>(b.ptr) + off, len, hipMemcpyDeviceToHost) != hipSuccess) {
+                std::fprintf(stderr, "X_SENTINEL %s block %p: copy failed\n", where, b.ptr);
+                break;
+            }
+            for (size_t i = 0; i < h.size(); ++i) {
+                if (h[i] != 0xA5A5A5A5u) {
+                    if (bad == 0) {
+                        first = off / 4 + i;
+                        firstVal = h[i];
+                    }
+                    ++bad;
+                }
+            }
+        }
+        std::fprintf(stderr, "X_SENTINEL %s block %p bytes %zu %s changed_words %zu first %zu val 0x%08x\n", where,
+                     b.ptr, b.bytes, whole ? "whole" : "ends", bad, first, firstVal);
+    }
+}
+
 void UncachedRelease(int device, void* ptr, size_t bytes)
 {
+    const int m = XMode();
+    if (m == 0) {
+        UncachedPool& pool = Pool();
+        std::lock_guard<std::mutex> lk(pool.mu);
+        pool.idle.insert({{device, bytes}, ptr});
+        return;
+    }
     UncachedPool& pool = Pool();
     std::lock_guard<std::mutex> lk(pool.mu);
-    pool.idle.insert({{device, bytes}, ptr});
+    (void)hipDeviceSynchronize();
+    if (m == 3) {
+        (void)hipMemsetD32(static_cast<hipDeviceptr_t>(ptr), 0xA5A5A5A5, bytes / 4);
+        (void)hipDeviceSynchronize();
+        XKept().push_back({device, ptr, bytes});
+        std::fprintf(stderr, "X_KEEP %p bytes %zu\n", ptr, bytes);
+        return;
+    }
+    if (m == 2) {
+        (void)ScrubL2(nullptr);
+        (void)hipDeviceSynchronize();
+    }
+    std::fprintf(stderr, "X_FREE %p bytes %zu end %p\n", ptr, bytes, static_cast<char*>(ptr) + bytes);
+    (void)hipFree(ptr);
 }
+
+}  // namespace
+
+void XSentinelCheck(const char* where)
+{
+    if (XMode() != 3) return;
+    std::lock_guard<std::mutex> lk(Pool().mu);
+    XSentinelCheckLocked(where);
+}
+
+namespace {
 
 size_t FlagAllocBytes() { return size_t(kIpcFlagBytes + 2 * kIpcLlParityBytes); }
 
-struct Exported {
-    hipIpcMemHandle_t stg;
-    hipIpcMemHandle_t flags;
-    char busId[32];  // the rank's device: ranks that share one count against its resident blocks together
-};
-
-struct RawPtrs {
-    void* stg;
-    uint32_t* flags;
-    uint8_t ok;
-};
+// Maps one allocation of every rank (collective: every rank takes part whatever its local outcome, and the outcome
+// is agreed: either every rank has every peer's allocation mapped, or none keeps a mapping and all report
+// HCCL_E_NOT_SUPPORT; a failed host exchange returns the transport's error). peers[r] receives rank r's allocation
+// as this rank addresses it (its own at [me]); opened[r] marks the ones opened with hipIpcOpenMemHandle. In a loopback
+// world the ranks share the device and exchange raw pointers. ranksOnDevice (rank mode, optional) receives the most
+// ranks any one device holds, from every rank's PCI bus id: the same number on every rank.
+HcclResult MapPeers(Comm& c, void* mine, bool localOk, void* peers[kIpcMaxRanks], bool opened[kIpcMaxRanks],
+                    uint32_t* ranksOnDevice)
+{
+    const uint32_t n = c.nRanks, me = c.rank;
+    if (c.transport->SharedDevice()) {
+        struct Raw {
+            void* p;
+            uint8_t ok;
+        };
+        const Raw m{mine, static_cast<uint8_t>(localOk ? 1 : 0)};
+        std::vector<Raw> all(n);
+        HCCL_CHK(c.transport->AllGatherHost(&m, sizeof m, all.data()));
+        for (uint32_t r = 0; r < n; ++r) {
+            if (all[r].ok == 0) return HCCL_E_NOT_SUPPORT;
+        }
+        for (uint32_t r = 0; r < n; ++r) peers[r] = all[r].p;
+        return HCCL_SUCCESS;
+    }
+    struct Exported {
+        hipIpcMemHandle_t h;
+        char busId[32];  // the rank's device: ranks that share one count against its resident blocks together
+        uint8_t ok;
+    };
+    Exported m{};
+    bool ok = localOk && hipIpcGetMemHandle(&m.h, mine) == hipSuccess &&
+              hipDeviceGetPCIBusId(m.busId, sizeof m.busId - 1, c.device) == hipSuccess;
+    m.ok = ok ? 1 : 0;
+    std::vector<Exported> all(n);
+    HCCL_CHK(c.transport->AllGatherHost(&m, sizeof m, all.data()));
+    for (uint32_t r = 0; r < n; ++r) ok = ok && all[r].ok != 0;  // nobody opens a handle some rank could not export
+    if (ranksOnDevice != nullptr) {
+        *ranksOnDevice = 1;
+        for (uint32_t r = 0; r < n; ++r) {
+            uint32_t k = 0;
+            for (uint32_t q = 0; q < n; ++q) k += std::strncmp(all[r].busId, all[q].busId, sizeof m.busId) == 0;
+            *ranksOnDevice = std::max(*ranksOnDevice, k);
+        }
+    }
+    for (uint32_t r = 0; r < n && ok; ++r) {
+        if (r == me) {
+            peers[r] = mine;
+            continue;
+        }
+        void* p = nullptr;
+        const hipError_t e = hipIpcOpenMemHandle(&p, all[r].h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) {
+            HCCL_AMD_ERR("rank %u: hipIpcOpenMemHandle of rank %u failed: %s", me, r, hipGetErrorString(e));
+            ok = false;
+            break;
+        }
+        peers[r] = p;
+        opened[r] = true;
+    }
+    const uint8_t mineOk = ok ? 1 : 0;
+    std::vector<uint8_t> allOk(n);
+    const HcclResult xr = c.transport->AllGatherHost(&mineOk, 1, allOk.data());
+    for (uint32_t r = 0; r < n && xr == HCCL_SUCCESS; ++r) ok = ok && allOk[r] != 0;
+    if (xr == HCCL_SUCCESS && ok) return HCCL_SUCCESS;
+    for (uint32_t r = 0; r < n; ++r) {
+        if (opened[r]) (void)hipIpcCloseMemHandle(peers[r]);
+        opened[r] = false;
+        peers[r] = nullptr;
+    }
+    return xr != HCCL_SUCCESS ? xr : HCCL_E_NOT_SUPPORT;
+}
 
 // The four areas inside one staging allocation at base (every rank has the same layout).
-void AreasOf(const IpcState& s, void* base, void* areas[kIpcAreas])
+void AreasOf(const IpcTier& t, void* base, void* areas[kIpcAreas])
 {
     char* b = static_cast<char*>(base);
     areas[kIpcAreaIn] = b;
-    areas[kIpcAreaRes] = b + s.stgInBytes;
-    areas[kIpcAreaAlt0] = b + s.stgInBytes + s.stgResBytes;
-    areas[kIpcAreaAlt1] = b + s.stgInBytes + s.stgResBytes + s.stgAltBytes;
+    areas[kIpcAreaRes] = b + t.inBytes;
+    areas[kIpcAreaAlt0] = b + t.inBytes + t.resBytes;
+    areas[kIpcAreaAlt1] = b + t.inBytes + t.resBytes + t.altBytes;
 }
 
-HcclResult IpcSetup(Comm& c)
+void ReleaseTier(Comm& c, IpcTier& t)
+{
+    for (uint32_t r = 0; r < kIpcMaxRanks; ++r) {
+        if (t.opened[r]) (void)hipIpcCloseMemHandle(t.peerArea[kIpcAreaIn][r]);  // the peer's one allocation
+    }
+    if (t.area[0] != nullptr) UncachedRelease(c.device, t.area[0], t.allocBytes());
+    const bool unavailable = t.unavailable;
+    t = IpcTier{};
+    t.unavailable = unavailable;
+}
+
+}  // namespace
+
+IpcTier IpcTierSizes(const Comm& c, int t)
+{
+    constexpr uint64_t kGranule = 64ull << 10;
+    const auto up = [](uint64_t b) { return (b + kGranule - 1) / kGranule * kGranule; };
+    // the large tier: HCCL_BUFFSIZE / 2 per area (2 x HCCL_BUFFSIZE for the four), or HCCL_AMD_IPC_STAGING_MIB
+    uint64_t large = c.cfg.ipcStagingBytes != 0 ? c.cfg.ipcStagingBytes : c.cclBytes / 2 / kGranule * kGranule;
+    large = std::min<uint64_t>(std::max<uint64_t>(large, 1ull << 20), kIpcStagingAreaMaxBytes);
+    uint64_t area = large;
+    if (t == kIpcTierSmall) {
+        area = std::min(large, up(uint64_t(std::max<uint32_t>(c.nRanks, 1)) *
+                                  std::max<uint64_t>(c.cfg.smallIpcBytes, 64ull << 10)));
+    }
+    IpcTier s{};
+    s.inBytes = area;
+    s.resBytes = area;  // results of a whole round, in round coordinates
+    // slots of the single-barrier kinds, two areas used alternately: as large as the others, within the one
+    // allocation's bound (1000 MiB areas leave them 23.5 MiB)
+    s.altBytes = std::min<uint64_t>(area, (kIpcStagingMaxBytes - 2 * area) / 2 / kGranule * kGranule);
+    return s;
+}
+
+namespace {
+
+// What every one-sided call needs (collective, at the communicator's first one-sided call): the flags and, behind
+// them, the LL area (one uncached allocation mapped by every peer, zeroed), the status words, the host-visible failure
+// word and the LL unpack area.
+HcclResult IpcSetupBase(Comm& c)
 {
     IpcState& s = c.ipc;
     if (s.ready) return HCCL_SUCCESS;
     if (s.unavailable) return HCCL_E_NOT_SUPPORT;
-    const uint32_t n = c.nRanks, me = c.rank;
     s.blocks = kIpcBlocks;
-    const uint64_t area = c.cfg.ipcStagingBytes;
-    s.stgInBytes = area;
-    s.stgResBytes = area;  // results of a whole round, in round coordinates
-    // slots of the single-barrier kinds, two areas used alternately: as large as the others, within the one
-    // allocation's bound below (the default 512 MiB areas leave them 511.5 MiB)
-    s.stgAltBytes = std::min<uint64_t>(area, (kIpcStagingMaxBytes - 2 * area) / 2 / (64ull << 10) * (64ull << 10));
-    // the flags and, behind them, the LL area (one allocation, one IPC handle; zeroed like the flags)
     const size_t flagBytes = FlagAllocBytes();
     // The fresh uncached pages may carry lines of a freed cached buffer in some XCD's L2: scrub the L2s before the
     // flags are zeroed (ScrubL2), so that no stale line is ever read or written back over them.
-    // HCCL_AMD_IPC_STAGING_CACHED=1 (diagnostics, one device only: the r03 A/B of what uncached staging costs) puts
-    // the slot and result areas in ordinary cached memory; the barriers' system-scope release and acquire then carry
-    // the hand-off through the L2s of that one device.
-    const bool cached = c.cfg.ipcStagingCached;
-    s.cachedStaging = cached;
-    // One allocation [in][results][alternate 0][alternate 1], below 2 GiB: hipIpcOpenMemHandle never returned for a
-    // 2 GiB allocation on this stack (the r03 512 MiB areas in one 2 GiB block hung the rank-mode set-up;
-    // tools/probe_ipc_open.py, profiles/r03_probe_ipc_open*.jsonl: up to 2047 MiB opens in < 1 ms and is written
-    // through whole, 2048 MiB does not return). (The stale lines r03 saw after changing this layout were the loopback
-    // link's hipMemcpyAsync, not the layout: DESIGN.md §5b, root cause.)
-    const uint64_t stgBytes = s.stgInBytes + s.stgResBytes + 2 * s.stgAltBytes;
-    void* base = nullptr;
-    bool ok = cached ? hipMalloc(&base, stgBytes) == hipSuccess : UncachedAlloc(c.device, &base, stgBytes);
-    if (ok) AreasOf(s, base, s.area);
-    ok = ok &&
-              UncachedAlloc(c.device, reinterpret_cast<void**>(&s.flags), flagBytes) &&
+    bool ok = UncachedAlloc(c.device, reinterpret_cast<void**>(&s.flags), flagBytes) &&
               hipMalloc(reinterpret_cast<void**>(&s.status), kIpcStatusBytes) == hipSuccess &&
               hipMalloc(&s.llUnpack, kIpcLlUnpackBytes) == hipSuccess &&
               hipHostMalloc(reinterpret_cast<void**>(&s.failHost), 64, hipHostMallocCoherent | hipHostMallocMapped) ==
@@ -126,7 +293,8 @@ HcclResult IpcSetup(Comm& c)
               hipMemset(s.flags, 0, flagBytes) == hipSuccess && hipMemset(s.status, 0, kIpcStatusBytes) == hipSuccess &&
               hipDeviceSynchronize() == hipSuccess;
     if (ok && c.cfg.ipcTrace) {
-        // phase stamps (diagnostics, HCCL_AMD_IPC_TRACE; HcclAmdCommIpcTrace reads them back): every rank's and block's row, so a loopback world's one launch fits too
+        // phase stamps (diagnostics, HCCL_AMD_IPC_TRACE; HcclAmdCommIpcTrace reads them back): every rank's and
+        // block's row, so a loopback world's one launch fits too
         const size_t tb = size_t(kIpcMaxRanks) * kIpcMaxBlocks * kIpcTraceSlots * sizeof(uint64_t);
         ok = hipMalloc(reinterpret_cast<void**>(&s.trace), tb) == hipSuccess && hipMemset(s.trace, 0, tb) == hipSuccess &&
              hipDeviceSynchronize() == hipSuccess;
@@ -134,98 +302,64 @@ HcclResult IpcSetup(Comm& c)
     if (ok) {
         *s.failHost = 0;
     } else {
-        HCCL_AMD_ERR("rank %u: IPC staging allocation failed", me);
+        HCCL_AMD_ERR("rank %u: IPC flag or status allocation failed", c.rank);
     }
     const volatile uint32_t* watch = s.failHost;
+    uint32_t* wdev = nullptr;
     if (c.transport->SharedDevice()) {
         // The world runs one launch for all ranks (issued by rank 0): its timeouts go to the world's word, which every
         // rank watches and which outlives each rank's communicator.
-        uint32_t* wdev = nullptr;
         uint32_t* word = ok ? c.transport->SharedFailWord(&wdev) : nullptr;
         ok = ok && word != nullptr;
-        // Every rank thread takes part in the exchange whatever its local outcome (a rank that returned early
-        // would leave the others blocked in the rendezvous), and they all agree on the result.
-        RawPtrs mine{s.area[0], s.flags, static_cast<uint8_t>(ok ? 1 : 0)};
-        std::vector<RawPtrs> all(n);
-        const HcclResult xr = c.transport->AllGatherHost(&mine, sizeof mine, all.data());
-        for (uint32_t r = 0; r < n && xr == HCCL_SUCCESS; ++r) ok = ok && all[r].ok != 0;
-        if (xr != HCCL_SUCCESS || !ok) {
-            IpcRelease(c);
-            s.unavailable = true;
-            return xr != HCCL_SUCCESS ? xr : HCCL_E_MEMORY;
-        }
-        for (uint32_t r = 0; r < n; ++r) {
-            void* areas[kIpcAreas];
-            AreasOf(s, all[r].stg, areas);
-            for (int k = 0; k < kIpcAreas; ++k) s.peerArea[k][r] = areas[k];
-            s.peerFlags[r] = all[r].flags;
-        }
-        s.failDev = wdev;
         watch = word;
-    } else {
-        // Every rank takes part in both exchanges whatever happens locally, and the outcome is agreed: either all
-        // ranks have every peer mapped or all release and report NOT_SUPPORT (the caller then runs the RCCL
-        // two-shot on every rank alike, never a mix of paths that would leave peers waiting).
-        Exported mine{};
-        ok = ok && hipIpcGetMemHandle(&mine.stg, s.area[0]) == hipSuccess &&
-             hipIpcGetMemHandle(&mine.flags, s.flags) == hipSuccess &&
-             hipDeviceGetPCIBusId(mine.busId, sizeof mine.busId - 1, c.device) == hipSuccess;
-        std::vector<Exported> all(n);
-        HcclResult xr = c.transport->AllGatherHost(&mine, sizeof mine, all.data());
-        if (xr != HCCL_SUCCESS) {
-            // the bootstrap failed under us: nothing was mapped; free the staging rather than leak it (a later call
-            // would otherwise allocate again) and report the transport's error
-            IpcRelease(c);
-            s.unavailable = true;
-            return xr;
-        }
-        // the most ranks any one device holds, from every rank's bus id: the same number on every rank, so the block
-        // counts (block b pairs with block b of each peer) stay equal whatever the placement
-        s.ranksOnDevice = 1;
-        for (uint32_t r = 0; r < n; ++r) {
-            uint32_t k = 0;
-            for (uint32_t q = 0; q < n; ++q) k += std::strncmp(all[r].busId, all[q].busId, sizeof mine.busId) == 0;
-            s.ranksOnDevice = std::max(s.ranksOnDevice, k);
-        }
-        for (uint32_t r = 0; r < n && ok; ++r) {
-            if (r == me) {
-                for (int k = 0; k < kIpcAreas; ++k) s.peerArea[k][r] = s.area[k];
-                s.peerFlags[r] = s.flags;
-                continue;
-            }
-            // the peer's staging, then its flags; the staging is closed again if the flags fail
-            void* f = nullptr;
-            void* peer = nullptr;
-            hipError_t e = hipIpcOpenMemHandle(&peer, all[r].stg, hipIpcMemLazyEnablePeerAccess);
-            if (e == hipSuccess) {
-                e = hipIpcOpenMemHandle(&f, all[r].flags, hipIpcMemLazyEnablePeerAccess);
-                if (e != hipSuccess) (void)hipIpcCloseMemHandle(peer);
-            }
-            if (e == hipSuccess) {
-                void* areas[kIpcAreas];
-                AreasOf(s, peer, areas);
-                for (int k = 0; k < kIpcAreas; ++k) s.peerArea[k][r] = areas[k];
-            }
-            if (e != hipSuccess) {
-                HCCL_AMD_ERR("rank %u: hipIpcOpenMemHandle of rank %u failed: %s", me, r, hipGetErrorString(e));
-                ok = false;
-                break;
-            }
-            s.peerFlags[r] = static_cast<uint32_t*>(f);
-            s.opened[r] = true;
-        }
-        const uint8_t mineOk = ok ? 1 : 0;
-        std::vector<uint8_t> allOk(n);
-        xr = c.transport->AllGatherHost(&mineOk, 1, allOk.data());
-        for (uint32_t r = 0; r < n && xr == HCCL_SUCCESS; ++r) ok = ok && allOk[r] != 0;
-        if (xr != HCCL_SUCCESS || !ok) {
-            IpcRelease(c);
-            s.unavailable = true;
-            return xr != HCCL_SUCCESS ? xr : HCCL_E_NOT_SUPPORT;
-        }
     }
+    void* peers[kIpcMaxRanks] = {};
+    const HcclResult r = MapPeers(c, s.flags, ok, peers, s.flagsOpened, &s.ranksOnDevice);
+    if (r != HCCL_SUCCESS) {
+        IpcRelease(c);
+        s.unavailable = true;
+        return r;
+    }
+    for (uint32_t q = 0; q < c.nRanks; ++q) s.peerFlags[q] = static_cast<uint32_t*>(peers[q]);
+    if (c.transport->SharedDevice()) s.failDev = wdev;
     c.failWord.store(watch, std::memory_order_release);
     s.ready = true;
+    return HCCL_SUCCESS;
+}
+
+// Staging tier t (collective, at the first call that needs it): one uncached allocation below 2 GiB holding
+// [in][results][alternate 0][alternate 1], mapped by every peer. hipIpcOpenMemHandle never returned for a 2 GiB
+// allocation on this stack (r03: the 512 MiB areas in one 2 GiB block hung the rank-mode set-up;
+// profiles/r03_probe_ipc_open*.jsonl: up to 2047 MiB opens in < 1 ms, 2048 MiB does not return).
+HcclResult IpcSetupTier(Comm& c, int t)
+{
+    IpcTier& tr = c.ipc.tier[t];
+    if (tr.ready) return HCCL_SUCCESS;
+    if (tr.unavailable) return HCCL_E_NOT_SUPPORT;
+    tr = IpcTierSizes(c, t);
+    void* base = nullptr;
+    bool ok = UncachedAlloc(c.device, &base, tr.allocBytes());
+    if (!ok) {
+        base = nullptr;
+        HCCL_AMD_ERR("rank %u: IPC staging allocation of %llu B failed", c.rank, (unsigned long long)tr.allocBytes());
+    }
+    // no stale line of a freed cached buffer may be written back over the new staging (as for the flags)
+    ok = ok && hipDeviceSynchronize() == hipSuccess && (!c.cfg.ipcL2Scrub || ScrubL2(c.reduceStream) == HCCL_SUCCESS);
+    void* peers[kIpcMaxRanks] = {};
+    const HcclResult r = MapPeers(c, base, ok, peers, tr.opened, nullptr);
+    if (r != HCCL_SUCCESS) {
+        if (base != nullptr) UncachedRelease(c.device, base, tr.allocBytes());
+        tr = IpcTier{};
+        tr.unavailable = true;
+        return r;
+    }
+    AreasOf(tr, base, tr.area);
+    for (uint32_t q = 0; q < c.nRanks; ++q) {
+        void* areas[kIpcAreas];
+        AreasOf(tr, peers[q], areas);
+        for (int k = 0; k < kIpcAreas; ++k) tr.peerArea[k][q] = areas[k];
+    }
+    tr.ready = true;
     return HCCL_SUCCESS;
 }
 
@@ -239,12 +373,12 @@ bool Aligned16(const void* p, const void* q)
 // (the CU's L1) suffices for the reader, whose loads go to memory. The user buffers are never handed over inside the
 // kernel (each element is read and written by the lane that owns it); across kernels they are ordered by the ordinary
 // kernel boundaries, which make plain and non-temporal stores visible to the next kernel on every XCD
-// (tools/coherence_probe.hip, profiles/r04_coherence_probe.jsonl). The light fences skip the system-scope release and
-// acquire, which write back and invalidate the whole XCD L2 for every block: 3-13 % per call in loopback worlds
-// (profiles/r03_ipc_variant_ab_fence.jsonl). Default (CommConfig::ipcLightFence = -1): light in a loopback world, where
-// every store goes through the owner's own uncached pointer; system scope in rank mode, whose stores reach the peers'
-// staging through hipIpcOpenMemHandle mappings, and an imported mapping need not keep the exporter's uncached memory
-// type (imported mappings). HCCL_AMD_IPC_LIGHT_FENCE=1 or 0 forces either. Equal on every rank.
+// (tools/probes/coherence_probe.hip, profiles/r04_coherence_probe.jsonl). The light fences skip the system-scope
+// release and acquire, which write back and invalidate the whole XCD L2 for every block: 3-13 % per call in loopback
+// worlds (profiles/r03_ipc_variant_ab_fence.jsonl). Default (CommConfig::ipcLightFence = -1): light in a loopback
+// world, where every store goes through the owner's own uncached pointer; system scope in rank mode, whose stores reach
+// the peers' staging through hipIpcOpenMemHandle mappings, and an imported mapping need not keep the exporter's uncached
+// memory type (imported mappings). HCCL_AMD_IPC_LIGHT_FENCE=1 or 0 forces either. Equal on every rank.
 bool IpcLightFence(const Comm& c)
 {
     return c.cfg.ipcLightFence < 0 ? c.transport->SharedDevice() : c.cfg.ipcLightFence != 0;
@@ -259,32 +393,25 @@ void IpcQuiesce(Comm& c)
     // Peers store into this rank's staging and flags: unmapping or freeing them while any peer's kernel may still
     // run would fault that peer. Wait for this device, then for every rank to get here (each has waited for its own).
     (void)hipDeviceSynchronize();
-    if (!c.transport->SharedDevice()) {
-        uint8_t mine = 1;
-        std::vector<uint8_t> all(c.nRanks);
-        if (c.transport->AllGatherHost(&mine, 1, all.data()) != HCCL_SUCCESS) {
-            HCCL_AMD_ERR("rank %u: IPC teardown rendezvous failed; peer mappings are left in place", c.rank);
-            c.ipc = IpcState{};  // leak rather than free memory a peer may still write
-        }
+    // A loopback world has no rendezvous here: its ranks are destroyed one after another from any thread (a host
+    // exchange would wait for ranks that are destroyed later on the same thread), and every one-sided launch of the
+    // world is a single launch on this device, which the device synchronisation above has drained; a world whose ranks
+    // are destroyed while others still issue collectives is outside the contract.
+    if (c.transport->SharedDevice()) return;
+    uint8_t mine = 1;
+    std::vector<uint8_t> all(c.nRanks);
+    if (c.transport->AllGatherHost(&mine, 1, all.data()) != HCCL_SUCCESS) {
+        HCCL_AMD_ERR("rank %u: IPC teardown rendezvous failed; peer mappings are left in place", c.rank);
+        c.ipc = IpcState{};  // leak rather than free memory a peer may still write
     }
 }
 
 void IpcRelease(Comm& c)
 {
     IpcState& s = c.ipc;
+    for (IpcTier& t : s.tier) ReleaseTier(c, t);
     for (uint32_t r = 0; r < kIpcMaxRanks; ++r) {
-        if (s.opened[r]) {
-            (void)hipIpcCloseMemHandle(s.peerArea[0][r]);  // the peer's one staging allocation
-            (void)hipIpcCloseMemHandle(s.peerFlags[r]);
-            s.opened[r] = false;
-        }
-    }
-    if (s.area[0] != nullptr) {  // the areas are parts of this one allocation
-        if (s.cachedStaging) {
-            (void)hipFree(s.area[0]);
-        } else {
-            UncachedRelease(c.device, s.area[0], s.stgInBytes + s.stgResBytes + 2 * s.stgAltBytes);
-        }
+        if (s.flagsOpened[r]) (void)hipIpcCloseMemHandle(s.peerFlags[r]);
     }
     if (s.flags != nullptr) UncachedRelease(c.device, s.flags, FlagAllocBytes());
     if (s.status != nullptr) (void)hipFree(s.status);
@@ -296,6 +423,20 @@ void IpcRelease(Comm& c)
     const bool unavailable = s.unavailable;
     s = IpcState{};
     s.unavailable = unavailable;
+}
+
+uint64_t IpcDeviceBytes(const Comm& c)
+{
+    const IpcState& s = c.ipc;
+    uint64_t b = 0;
+    if (s.flags != nullptr) b += FlagAllocBytes();
+    if (s.status != nullptr) b += kIpcStatusBytes;
+    if (s.llUnpack != nullptr) b += kIpcLlUnpackBytes;
+    if (s.trace != nullptr) b += uint64_t(kIpcMaxRanks) * kIpcMaxBlocks * kIpcTraceSlots * sizeof(uint64_t);
+    for (const IpcTier& t : s.tier) {
+        if (t.area[0] != nullptr) b += t.allocBytes();
+    }
+    return b;
 }
 
 // Default workgroups per launch by the bytes of one rank's input. Every block runs its own cross-rank barrier (a
@@ -543,7 +684,8 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
     if (capture != hipStreamCaptureStatusNone && (!c.ipc.ready || c.transport->SharedDevice())) {
         return HCCL_E_NOT_SUPPORT;
     }
-    HCCL_CHK(IpcSetup(c));
+    const bool capturing = capture != hipStreamCaptureStatusNone;
+    HCCL_CHK(IpcSetupBase(c));
     IpcState& s = c.ipc;
     const uint32_t n = c.nRanks;
     // workgroups per rank (equal on every rank: block b pairs with block b of each peer, and the default is a function
@@ -582,13 +724,7 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
     }
     const uint64_t V = 16 / es;
 
-    for (uint32_t r = 0; r < n; ++r) {
-        a.stgIn[r] = s.peerArea[kIpcAreaIn][r];
-        a.stgRes[r] = s.peerArea[kIpcAreaRes][r];
-        a.stgAlt[0][r] = s.peerArea[kIpcAreaAlt0][r];
-        a.stgAlt[1][r] = s.peerArea[kIpcAreaAlt1][r];
-        a.flags[r] = s.peerFlags[r];
-    }
+    for (uint32_t r = 0; r < n; ++r) a.flags[r] = s.peerFlags[r];
     a.n = n;
     a.kind = kind;
     a.order = plan.order;
@@ -614,8 +750,9 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
         }
     }
     const bool single = SingleBarrierKind(kind);
-    const uint64_t slotCap = ((single ? s.stgAltBytes : s.stgInBytes) / es / n) / V * V;
-
+    // slot capacity of a tier in elements (a round's piece of every chunk must fit n slots)
+    const auto capOf = [&](const IpcTier& t) { return ((single ? t.altBytes : t.inBytes) / es / n) / V * V; };
+    uint64_t slotCap = capOf(IpcTierSizes(c, kIpcTierSmall));
 
     // One launch per executor loop [off, off + cnt) of the reference template whose order the fold follows: its
     // slicing is per loop (schedule.cc RefLoopElems and the MeshChunk loops). A ReduceScatter loop takes elements
@@ -687,7 +824,7 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
         g.blockElems = ((g.piece + s.blocks - 1) / s.blocks + V - 1) / V * V;
         g.tileElems = c.cfg.ipcTileBytes / es / V * V;  // 0: contiguous windows (HCCL_AMD_IPC_TILE_KIB)
         g.nt = c.cfg.ipcNt ? 1u : 0u;                     // non-temporal loads and stores (HCCL_AMD_IPC_NT)
-        g.fence = (IpcLightFence(c) && !s.cachedStaging) ? 1u : 0u;
+        g.fence = IpcLightFence(c) ? 1u : 0u;
         g.threads = c.cfg.ipcThreads;                    // HCCL_AMD_IPC_THREADS
         g.rounds = static_cast<uint32_t>((widest + g.piece - 1) / g.piece);
         g.epochSpan = (single ? 1 : 2) * g.rounds;
@@ -699,6 +836,36 @@ HcclResult RunIpcPlan(Comm& c, int32_t opType, const IpcPlan& plan, const void* 
         }
     };
     auto at = [es](const void* p, uint64_t off) { return static_cast<char*>(const_cast<void*>(p)) + off * es; };
+
+    // The staging tier (IpcTier): the small one when every launch of the call fits one round there, else the large
+    // one (also when the small tier's set-up failed). The choice depends on the call's arguments and the configuration
+    // at the set-up, equal on every rank, and each tier's availability is agreed, so every rank takes the same tier.
+    // The LL form uses no staging area (its words travel through the flags allocation's LL area).
+    bool fitsSmall = true;
+    for (const Launch& l : launches) {
+        IpcArgs g = a;
+        geometry(g, l.cnt);
+        fitsSmall = fitsSmall && g.rounds == 1;
+    }
+    if (a.ll == 0) {
+        int t = fitsSmall && !s.tier[kIpcTierSmall].unavailable ? kIpcTierSmall : kIpcTierLarge;
+        if (capturing && !s.tier[t].ready) return HCCL_E_NOT_SUPPORT;  // no collective set-up under capture
+        HcclResult r = IpcSetupTier(c, t);
+        if (r == HCCL_E_NOT_SUPPORT && t == kIpcTierSmall) {
+            t = kIpcTierLarge;
+            if (capturing && !s.tier[t].ready) return HCCL_E_NOT_SUPPORT;
+            r = IpcSetupTier(c, t);
+        }
+        HCCL_CHK(r);
+        const IpcTier& tr = s.tier[t];
+        slotCap = capOf(tr);
+        for (uint32_t q = 0; q < n; ++q) {
+            a.stgIn[q] = tr.peerArea[kIpcAreaIn][q];
+            a.stgRes[q] = tr.peerArea[kIpcAreaRes][q];
+            a.stgAlt[0][q] = tr.peerArea[kIpcAreaAlt0][q];
+            a.stgAlt[1][q] = tr.peerArea[kIpcAreaAlt1][q];
+        }
+    }
 
     if (!c.transport->SharedDevice()) {
         a.me = static_cast<int32_t>(c.rank);

@@ -188,28 +188,48 @@ uint32_t IpcResidentBlocks(HcclDataType dt, HcclReduceOp op, bool rhd, bool ll, 
 
 // Writes back and invalidates every XCD's L2 at system scope (one maintenance block per CU); synchronous on `stream`.
 HcclResult ScrubL2(hipStream_t stream);
+void XSentinelCheck(const char* where);  // EXPERIMENT (r06)
 
-// Per-communicator state of the IPC path.
+// Staging of the one-sided kernel comes in two tiers, each one uncached allocation per rank holding the four areas
+// (kIpcAreaIn, kIpcAreaRes, kIpcAreaAlt0, kIpcAreaAlt1), mapped by every peer, and each set up collectively by the
+// first call that needs it:
+//   kIpcTierSmall — areas of n x HCCL_AMD_SMALL_IPC_BYTES (at least n x 64 KiB): every call whose staging fits one
+//                   round there (the small-call rule's calls and any other small one-sided call);
+//   kIpcTierLarge — areas of HCCL_BUFFSIZE / 2, so the four hold 2 x HCCL_BUFFSIZE, the reference's CCL buffer pair
+//                   (HCCL_BUFFSIZE.md; aiv_defines.h:44), unless HCCL_AMD_IPC_STAGING_MIB sets the area size.
+// A communicator that only makes small calls therefore holds MiBs, not the large tier.
+constexpr int kIpcTierSmall = 0;
+constexpr int kIpcTierLarge = 1;
+constexpr int kIpcTiers = 2;
+
+struct IpcTier {
+    bool ready = false;
+    bool unavailable = false;  // its set-up failed on some rank: calls that need it report NOT_SUPPORT
+    void* area[kIpcAreas] = {};  // own areas, parts of one uncached allocation at area[0]
+    void* peerArea[kIpcAreas][kIpcMaxRanks] = {};
+    bool opened[kIpcMaxRanks] = {};  // rank mode: the peer's allocation was opened with hipIpcOpenMemHandle
+    uint64_t inBytes = 0;
+    uint64_t resBytes = 0;
+    uint64_t altBytes = 0;  // each of the two alternate slot areas of the single-barrier kinds
+    uint64_t allocBytes() const { return inBytes + resBytes + 2 * altBytes; }
+};
+
+// Per-communicator state of the IPC path. `ready` covers what every call needs: the flags and LL area (one uncached
+// allocation mapped by every peer), the status words, the failure word and the LL unpack area.
 struct IpcState {
     bool ready = false;
     bool unavailable = false;      // set-up failed on some rank: every later call reports NOT_SUPPORT
-    void* area[kIpcAreas] = {};    // own staging areas, uncached, in one allocation at area[0] (kIpcAreaIn, kIpcAreaRes,
-                                   // kIpcAreaAlt0, kIpcAreaAlt1)
     uint32_t* flags = nullptr;     // own flags, uncached, zeroed
     uint32_t* status = nullptr;    // device words: [0] bit 0 = barrier timeout, [2..3] = tagged longest wait (IpcArgs)
     uint32_t callSeq = 0;          // IPC calls issued on the communicator (tags the wait diagnostic)
     uint32_t* failHost = nullptr;  // pinned host word the kernel sets on a barrier timeout (hipHostMalloc, coherent)
     uint32_t* failDev = nullptr;   // the device address the launches write (IpcArgs::failHost): of failHost, or in a
                                    // loopback world of the world's word (Transport::SharedFailWord)
-    void* peerArea[kIpcAreas][kIpcMaxRanks] = {};
     uint32_t* peerFlags[kIpcMaxRanks] = {};
-    bool opened[kIpcMaxRanks] = {};
-    uint64_t stgInBytes = 0;
-    uint64_t stgResBytes = 0;
-    uint64_t stgAltBytes = 0;      // each of the two alternate slot areas of the single-barrier kinds
+    bool flagsOpened[kIpcMaxRanks] = {};
+    IpcTier tier[kIpcTiers];
     uint32_t blocks = 0;
     uint32_t ranksOnDevice = 1;    // rank mode: the most ranks that share one device (by PCI bus id), same on all ranks
-    bool cachedStaging = false;    // HCCL_AMD_IPC_STAGING_CACHED=1 at set-up (diagnostics): barriers keep full fences
     uint64_t* trace = nullptr;     // HCCL_AMD_IPC_TRACE=1 at set-up: [kIpcMaxRanks][kIpcMaxBlocks][kIpcTraceSlots]
     void* llUnpack = nullptr;      // own unpack area of the LL path (cached, kIpcLlUnpackBytes)
 };
@@ -234,5 +254,8 @@ constexpr uint64_t kIpcLlUnpackBytes = uint64_t(kIpcMaxRanks) * (kIpcLlMaxBytes 
 // The staging allocation of a rank (slot, result and two alternate areas) stays below 2 GiB: hipIpcOpenMemHandle never
 // returned for a 2 GiB allocation on this stack (IpcSetup). The area size is CommConfig::ipcStagingBytes.
 constexpr uint64_t kIpcStagingMaxBytes = 2047ull << 20;
+// One staging area (HCCL_AMD_IPC_STAGING_MIB's range, and the cap of HCCL_BUFFSIZE / 2): two such areas leave the
+// alternate areas 23.5 MiB each within kIpcStagingMaxBytes.
+constexpr uint64_t kIpcStagingAreaMaxBytes = 1000ull << 20;
 
 }  // namespace hccl_amd

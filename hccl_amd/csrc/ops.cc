@@ -86,8 +86,10 @@ bool DeviceAccessible(const void* p)
         (void)hipGetLastError();  // an unregistered host pointer reports an error: clear it
         return false;
     }
+    // registered host memory counts only where the device addresses it at the host pointer itself (the copy kernel is
+    // handed that pointer); a registration mapped elsewhere goes to hipMemcpyAsync
     return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged ||
-           (a.type == hipMemoryTypeHost && a.devicePointer != nullptr);
+           (a.type == hipMemoryTypeHost && a.devicePointer == p);
 }
 
 // The one-rank collective's copy (SingleRankProc). The library's copy kernel when both buffers are device-accessible;
@@ -209,6 +211,7 @@ HcclResult RunCollective(Comm& c, int32_t opType, void* sendBuf, void* recvBuf, 
         if (!c.transport->HasSendRecv()) return HCCL_E_NOT_SUPPORT;
         p.algo = opType == HCCL_AMD_OP_ALLGATHER ? HCCL_AMD_ALGO_MESH_ONESHOT : family;
     }
+    HCCL_CHK(c.EnsureScratch());
     p.nRanks = c.nRanks;
     p.rank = c.rank;
     p.count = count;
@@ -269,6 +272,7 @@ HcclResult RunReduceScatterV(Comm& c, void* sendBuf, const uint64_t* counts, con
         if (ipcOnly) return HCCL_E_NOT_SUPPORT;
     }
     const uint32_t es = DataTypeSize(dt);
+    HCCL_CHK(c.EnsureScratch());
     ScheduleParams p;
     p.opType = HCCL_AMD_OP_REDUCE_SCATTER_V;
     p.nRanks = c.nRanks;
@@ -502,6 +506,25 @@ HcclResult HcclAmdCommInitHostExchange(uint32_t nRanks, uint32_t rank, HcclAmdHo
     return HCCL_SUCCESS;
 }
 
+HcclResult HcclAmdCommInitSelfLoop(uint32_t nRanks, uint32_t rank, HcclComm* comm)
+{
+    if (comm == nullptr) return HCCL_E_PTR;
+    if (nRanks == 0 || rank >= nRanks || nRanks > HCCL_AMD_IR_MAX_SRC) return HCCL_E_PARA;
+    int dev = 0;
+    HIP_CHK(hipGetDevice(&dev));
+    auto c = std::make_unique<Comm>();
+    c->rank = rank;
+    c->nRanks = nRanks;
+    HCCL_CHK(c->Init(dev));
+    HcclResult err = HCCL_SUCCESS;
+    c->transport = MakeRcclSelfLoopTransport(&err);
+    if (c->transport == nullptr) return err == HCCL_SUCCESS ? HCCL_E_INTERNAL : err;
+    c->ipc.unavailable = true;  // no peers to map: the one-sided kernel answers NOT_SUPPORT
+    HCCL_CHK(c->StartWatchdog());
+    *comm = c.release();
+    return HCCL_SUCCESS;
+}
+
 HcclResult HcclAmdCommSetAlgo(HcclComm comm, int32_t algo)
 {
     Comm* c = AsComm(comm);
@@ -559,6 +582,15 @@ HcclResult HcclAmdCommGetConfig(HcclComm comm, int32_t key, int64_t* value)
     return GetConfigEntry(c->cfg, key, value);
 }
 
+HcclResult HcclAmdCommDeviceBytes(HcclComm comm, uint64_t* bytes)
+{
+    Comm* c = AsComm(comm);
+    if (c == nullptr || bytes == nullptr) return HCCL_E_PTR;
+    std::lock_guard<std::mutex> lk(c->mu);
+    *bytes = c->DeviceBytes();
+    return HCCL_SUCCESS;
+}
+
 HcclResult HcclAmdCommScratch(HcclComm comm, void** ptr, uint64_t* bytes)
 {
     Comm* c = AsComm(comm);
@@ -588,17 +620,14 @@ HcclResult HcclAmdCommExecute(HcclComm comm,const HcclAmdIrOp* ops, uint64_t num
     const uint64_t es = DataTypeSize(dataType);
     std::lock_guard<std::mutex> lk(c->mu);
     if (c->scratch == nullptr) {
-        // a one-rank communicator has no staging until a program asks for it
+        // no staging until a program asks for it
         for (uint64_t i = 0; i < numOps; ++i) {
             bool uses = ops[i].kind != HCCL_AMD_IR_SEND && ops[i].dstBuf == HCCL_AMD_BUF_SCRATCH;
             for (int j = 0; j < ops[i].nsrc && j < HCCL_AMD_IR_MAX_SRC; ++j) {
                 uses = uses || ops[i].srcBuf[j] == HCCL_AMD_BUF_SCRATCH;
             }
             if (uses) {
-                HIP_CHK(hipSetDevice(c->device));
-                c->cclBytes = CclBytesDefault();
-                HIP_CHK(hipMalloc(&c->scratch, 2 * c->cclBytes));
-                c->scratchBytes = 2 * c->cclBytes;
+                HCCL_CHK(c->EnsureScratch());
                 break;
             }
         }

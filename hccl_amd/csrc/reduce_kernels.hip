@@ -911,24 +911,9 @@ hipError_t RunCopy(unsigned char* dst, const unsigned char* src, uint64_t bytes,
 
 }  // namespace
 
-// HCCL_AMD_DEVICE_COPY=memcpy (read once, at library load) or HcclAmdSetDeviceCopyKernel(0): hipMemcpyAsync instead of
-// the copy kernel (diagnostics of the r03 stale-operand failure).
-std::atomic<bool> g_copyByKernel{[] {
-    const char* e = std::getenv("HCCL_AMD_DEVICE_COPY");
-    return e == nullptr || std::strcmp(e, "memcpy") != 0;
-}()};
-
-bool DeviceCopyByKernel() { return g_copyByKernel.load(std::memory_order_relaxed); }
-
-void SetDeviceCopyByKernel(bool on) { g_copyByKernel.store(on, std::memory_order_relaxed); }
-
 HcclResult LaunchCopyBytes(void* dst, const void* src, uint64_t bytes, hipStream_t stream)
 {
     if (bytes == 0 || dst == src) return HCCL_SUCCESS;
-    if (!DeviceCopyByKernel()) {
-        HIP_CHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream));
-        return HCCL_SUCCESS;
-    }
     auto* d = static_cast<unsigned char*>(dst);
     const auto* sp = static_cast<const unsigned char*>(src);
     const uintptr_t x = reinterpret_cast<uintptr_t>(dst) ^ reinterpret_cast<uintptr_t>(src);  // phase difference

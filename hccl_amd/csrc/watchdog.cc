@@ -337,7 +337,6 @@ void WaitForReaperAtExit()
 
 bool DeferDestroy(Comm* c)
 {
-    if (!EnvFlag("HCCL_AMD_DEFER_DESTROY", true)) return false;  // diagnostics: tear down at once, as before r03
     if (c->graphRefs.load(std::memory_order_acquire) == 0) return false;
     // The collective steps of the teardown run now, on this rank's destroy, as on every peer's: the IPC
     // rendezvous (after it no peer stores into this rank's staging, nor this rank into theirs), and the transport is

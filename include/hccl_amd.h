@@ -229,8 +229,11 @@ typedef enum {
     HCCL_AMD_CFG_IPC_THREADS = 9,          /* (=) HCCL_AMD_IPC_THREADS: 256 (default) or 512 */
     HCCL_AMD_CFG_IPC_TILE_KIB = 10,        /* (=) HCCL_AMD_IPC_TILE_KIB: 0 = one window per block (default) */
     HCCL_AMD_CFG_IPC_TIMEOUT_MS = 11,      /* HCCL_AMD_IPC_TIMEOUT_MS, else HCCL_EXEC_TIMEOUT's AIV rule (HcclAmdIpcTimeoutMs) */
-    HCCL_AMD_CFG_IPC_STAGING_MIB = 12,     /* (=) HCCL_AMD_IPC_STAGING_MIB, 16..1000 (default 512); at the IPC set-up */
-    HCCL_AMD_CFG_IPC_STAGING_CACHED = 13,  /* (=) HCCL_AMD_IPC_STAGING_CACHED (diagnostics); at the IPC set-up */
+    HCCL_AMD_CFG_IPC_STAGING_MIB = 12,     /* (=) HCCL_AMD_IPC_STAGING_MIB: the one-sided kernel's large staging tier,
+                                              MiB per area (four areas per rank), 16..1000, or 0 (default) for
+                                              HCCL_BUFFSIZE / 2, so that the tier holds 2 x HCCL_BUFFSIZE; read when
+                                              the tier is set up (HcclAmdCommDeviceBytes) */
+    /* 13 is retired (HCCL_AMD_IPC_STAGING_CACHED, an r03 diagnostic): HCCL_E_PARA */
     HCCL_AMD_CFG_IPC_TRACE = 14,           /* HCCL_AMD_IPC_TRACE: phase stamps (diagnostics); at the IPC set-up */
     HCCL_AMD_CFG_IPC_L2_SCRUB = 15,        /* HCCL_AMD_IPC_L2_SCRUB: L2 maintenance at the IPC set-up (default 1) */
     HCCL_AMD_CFG_FOLD_TIMING = 16,         /* HCCL_AMD_FOLD_TIMING: time the executor's folds (diagnostics; calls run
@@ -255,10 +258,6 @@ extern HcclResult HcclAmdCommReloadConfig(HcclComm comm);
 extern HcclResult HcclAmdCommFoldTiming(HcclComm comm, uint64_t* folds, uint64_t* foldBytes, double* foldUs,
                                         double* spanUs);
 
-/* Process-wide: the device-to-device copies the library makes (loopback links, COPY records, one-operand folds, a
- * one-rank collective) run as its copy kernel (on != 0, the default) or as hipMemcpyAsync (0; diagnostics).
- * Initialised at library load from HCCL_AMD_DEVICE_COPY (=memcpy: 0). */
-extern HcclResult HcclAmdSetDeviceCopyKernel(int32_t on);
 
 /* Runs one rank's IR program on comm's executor: what every collective runs after it has built its schedule (SEND/RECV
  * groups on the transport, folds and copies on the reduce stream, the cross-stream waits derived from the records'
@@ -352,6 +351,12 @@ extern HcclResult HcclAmdRcclP2pChannels(uint32_t* perPeer, uint32_t* minP2pChan
 /* The executor staging of comm (diagnostics): *ptr = its device address (NULL until allocated), *bytes = its size. */
 extern HcclResult HcclAmdCommScratch(HcclComm comm, void** ptr, uint64_t* bytes);
 
+/* The device memory the library holds for comm now, in bytes: the executor staging (2 x HCCL_BUFFSIZE, allocated by
+ * the first collective that runs a schedule) plus the one-sided kernel's allocations (flags and LL area, status words
+ * and unpack area at its first call; the small staging tier, n x HCCL_AMD_SMALL_IPC_BYTES per area, and the large
+ * one, 2 x HCCL_BUFFSIZE, each at the first call that needs it). RCCL's own buffers are not included. */
+extern HcclResult HcclAmdCommDeviceBytes(HcclComm comm, uint64_t* bytes);
+
 /* Enqueues on `stream` a system-scope write-back and invalidate of every XCD's L2 of the current device (one
  * workgroup per CU runs buffer_wbl2 sc0 sc1 / buffer_inv sc0 sc1) and waits for it. Diagnostics: a kernel launched
  * after it reads every line from memory. */
@@ -377,6 +382,15 @@ typedef int32_t (*HcclAmdHostAllGatherFn)(void* ctx, const void* mine, uint64_t 
  * `fn` and `ctx` must stay valid for the communicator's lifetime. */
 extern HcclResult HcclAmdCommInitHostExchange(uint32_t nRanks, uint32_t rank, HcclAmdHostAllGatherFn fn, void* ctx,
                                               HcclComm* comm);
+
+/* A stand-in for one rank of an nRanks-rank communicator on one GPU (benchmark and test harnesses; never a data
+ * path): rank `rank`'s schedules run through a one-rank RCCL communicator with every peer mapped onto itself. Each
+ * transport group's sends are paired with its receives of the same size (RCCL pairs messages to itself in posting
+ * order), so every program keeps the schedule's shape (groups, pieces, staging, folds, waits, graph capture) and runs
+ * through RCCL's kernels, while the data no longer means the collective. A group whose send and receive sizes differ
+ * returns HCCL_E_NOT_SUPPORT. The one-sided kernel is unavailable (HCCL_E_NOT_SUPPORT; the small-call rule falls back
+ * to the schedule). */
+extern HcclResult HcclAmdCommInitSelfLoop(uint32_t nRanks, uint32_t rank, HcclComm* comm);
 
 #ifdef __cplusplus
 }

@@ -333,10 +333,13 @@ def test_ipc_lost_peer_fails_the_communicator(count):
     assert r0["after_s"] < 1.0, r0  # the gate enqueues nothing
 
 
-# Calls of the default-staging test (no HCCL_AMD_IPC_STAGING_MIB: 512 MiB slot and result areas, 511.5 MiB alternate
-# areas): (collective, elements per rank's input, in place). At n = 2 a two-shot owner's slot holds 64 Mi int32 per
-# staging round, so the 600 MiB AllReduces (chunks of 75 Mi elements) cross one round boundary, in place and out of
-# place; the 640 MiB ReduceScatter input (blocks of 80 Mi elements) crosses the alternate areas' boundary.
+# Calls of the default-staging test: (collective, elements per rank's input, in place). The large staging tier's areas
+# are HCCL_BUFFSIZE / 2 (100 MiB at the default 200 MB, the reference's 2 x HCCL_BUFFSIZE for the four) or, with
+# HCCL_AMD_IPC_STAGING_MIB=1000, the largest allocation the set-up makes (2 x 1000 MiB + 2 x 23.5 MiB, below the 2 GiB
+# that hipIpcOpenMemHandle never returned for in r03). At n = 2 and 100 MiB areas a two-shot owner's slot holds
+# 12.5 Mi int32 per staging round, so the 300 and 600 MiB AllReduces cross several round boundaries, in place and out
+# of place; the 640 MiB ReduceScatter input crosses the alternate areas' boundaries (at 1000 MiB areas: one boundary
+# for the 600 MiB AllReduces, several of the 23.5 MiB alternate areas for the ReduceScatter).
 DEFAULT_STAGING_CALLS = [
     (AR, 1025, False),
     (AR, (300 << 20) // 4 + 3, False),  # the r03 call that once returned a wrong result on rank 0
@@ -347,7 +350,7 @@ DEFAULT_STAGING_CALLS = [
 ]
 
 
-def _mismatch_detail(torch, y, want, xs_fn, prev, count, n, k):
+def _mismatch_detail(torch, y, want, xs_fn, prev, count, n, k, area_bytes):
     """Everything a wrong result can say about its cause: how many elements, where (owner chunk and
     staging round of the first, owners of all), the values at the first, and what the wrong value equals: the fold
     with one rank's operand missing, the previous call's result, zero, or none of these."""
@@ -355,7 +358,7 @@ def _mismatch_detail(torch, y, want, xs_fn, prev, count, n, k):
     i = int(bad[0])
     es, align = 4, 32  # int32; chunks rounded up to 128 B (HCCL_MIN_SLICE_ALIGN)
     chunk = ((count + n - 1) // n + align - 1) // align * align
-    slot = (512 << 20) // es // n // 4 * 4  # elements of one owner's slot per staging round
+    slot = area_bytes // es // n // 4 * 4  # elements of one owner's slot per staging round
     owners = torch.bincount(torch.div(bad, chunk, rounding_mode="floor"), minlength=n).tolist()
     got_i, want_i = int(y[i]), int(want[i])
     missing = [q for q in range(n) if got_i == want_i - int(xs_fn(q, i))]
@@ -366,10 +369,13 @@ def _mismatch_detail(torch, y, want, xs_fn, prev, count, n, k):
             "is_zero": got_i == 0}
 
 
-def _default_staging_main(rank, n, port, q):
-    # the default staging: one allocation of 2047 MiB per rank (a 2 GiB one, r03's first layout, never opened with
-    # hipIpcOpenMemHandle, so the rank-mode set-up hung)
+def _default_staging_main(rank, n, port, q, area_mib):
+    # area_mib None: the default large tier (HCCL_BUFFSIZE / 2 per area); 1000: one allocation of 2047 MiB per rank
+    # (a 2 GiB one, r03's first layout, was never opened with hipIpcOpenMemHandle, so the rank-mode set-up hung)
     os.environ.pop("HCCL_AMD_IPC_STAGING_MIB", None)
+    os.environ.pop("HCCL_BUFFSIZE", None)
+    if area_mib is not None:
+        os.environ["HCCL_AMD_IPC_STAGING_MIB"] = str(area_mib)
     os.environ["HCCL_AMD_IPC_TIMEOUT_MS"] = "20000"
     try:
         import torch
@@ -410,7 +416,8 @@ def _default_staging_main(rank, n, port, q):
             ok = bool(torch.equal(y, want))
             res.append((H.Algo(comm.last_algo).name, ok, comm.ipc_status() & 1))
             if not ok:
-                res.append(("mismatch", _mismatch_detail(torch, y, want, xs_fn, prev, out_len, n, k)))
+                res.append(("mismatch", _mismatch_detail(torch, y, want, xs_fn, prev, out_len, n, k,
+                                                         (area_mib or 100) << 20)))
             prev = y.clone() if kind == AR else None
             del x, y, want, base
         dist.barrier()
@@ -423,16 +430,18 @@ def _default_staging_main(rank, n, port, q):
 
 
 @pytest.mark.timeout(240)
-def test_ipc_rank_mode_default_staging():
-    """Rank mode with the default staging (no HCCL_AMD_IPC_STAGING_MIB; one allocation below 2 GiB per rank, opened by
-    every peer): two-shot AllReduces and a ReduceScatter exact without a barrier timeout, including calls that cross
-    the default areas' round boundary in place and out of place. A wrong result reports everything it can say about its
-    cause (_mismatch_detail) in the assertion message, in full."""
+@pytest.mark.parametrize("area_mib", [None, 1000])
+def test_ipc_rank_mode_default_staging(area_mib):
+    """Rank mode with the default large staging tier (HCCL_BUFFSIZE / 2 per area) and with the largest one (1000 MiB
+    areas: one allocation just below 2 GiB per rank, opened by every peer): two-shot AllReduces and a ReduceScatter
+    exact without a barrier timeout, including calls that cross the areas' round boundaries in place and out of place.
+    A wrong result reports everything it can say about its cause (_mismatch_detail) in the assertion message, in
+    full."""
     n = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_default_staging_main, args=(r, n, port, q)) for r in range(n)]
+    procs = [ctx.Process(target=_default_staging_main, args=(r, n, port, q, area_mib)) for r in range(n)]
     for p in procs:
         p.start()
     try:
@@ -447,7 +456,7 @@ def test_ipc_rank_mode_default_staging():
                 p.kill()
     import json
     os.makedirs("gpurun_out", exist_ok=True)
-    with open("gpurun_out/ipc_default_staging.json", "w") as f:
+    with open(f"gpurun_out/ipc_default_staging_{area_mib or 'default'}.json", "w") as f:
         json.dump({str(r): got[r] for r in got}, f, indent=1)
     for r in range(n):
         assert got[r][0] == "ok", f"rank {r}:\n{got[r][0]}"

@@ -14,7 +14,6 @@ import os
 import subprocess
 import sys
 
-import numpy as np
 import pytest
 import torch
 
@@ -31,7 +30,6 @@ def test_r03_failing_order_passes_with_kernel_copies(fence):
     process so the allocation history is the one that reproduced the failure."""
     ids = open(os.path.join(ROOT, "tests", "r03_failing_selection.txt")).read().split()
     env = dict(os.environ, HCCL_AMD_IPC_STAGING_MIB="64", HCCL_AMD_IPC_LIGHT_FENCE=fence)
-    env.pop("HCCL_AMD_DEVICE_COPY", None)  # the default: the library's copy kernel
     r = subprocess.run([sys.executable, "-u", "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", "--timeout", "120",
                         "--timeout-method", "thread", *ids], cwd=ROOT, env=env, capture_output=True, text=True,
                        timeout=300)
@@ -47,7 +45,6 @@ def test_user_copy_at_the_end_of_the_r03_failing_order():
     ids = open(os.path.join(ROOT, "tests", "r03_failing_selection.txt")).read().split()
     ids.append("tests/test_gpu_user_copy.py::test_user_copy_then_allreduce")
     env = dict(os.environ, HCCL_AMD_IPC_STAGING_MIB="64")
-    env.pop("HCCL_AMD_DEVICE_COPY", None)
     r = subprocess.run([sys.executable, "-u", "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", "--timeout", "120",
                         "--timeout-method", "thread", *ids], cwd=ROOT, env=env, capture_output=True, text=True,
                        timeout=400)
@@ -74,18 +71,3 @@ def test_device_copy_kernel_bytes(nbytes, shift):
     assert torch.equal(d, s)
     host = dst.cpu().numpy()
     assert (host[:do] == 0xA5).all() and (host[do + nbytes:] == 0xA5).all()
-
-
-def test_device_copy_memcpy_mode():
-    """HcclAmdSetDeviceCopyKernel(0) (HCCL_AMD_DEVICE_COPY=memcpy at load; diagnostics) still copies, through
-    hipMemcpyAsync."""
-    H.set_device_copy_kernel(False)
-    try:
-        x = torch.arange(1000, dtype=torch.float32, device="cuda")
-        y = torch.zeros_like(x)
-        H.local_reduce_n(y, [x])
-        torch.cuda.synchronize()
-        assert torch.equal(x, y)
-        assert np.array_equal(y.cpu().numpy(), np.arange(1000, dtype=np.float32))
-    finally:
-        H.set_device_copy_kernel(True)

@@ -5,10 +5,11 @@
 #   bench        bench.py default line (N = 1) -> gpurun_out/bench.json
 #   profile      tools/profile_round.sh $TAG (rocprofv3 trace + FETCH_SIZE + WRITE_SIZE of the N = 1 line)
 #   harness      bench.py's N > 1 path with $HARNESS_N ranks sharing the GPU (IPC-only communicators; a crash check)
-#   latency      small-call latency: rank mode (tools/graph_latency.py, n = 2 and 4, RHD and auto) and loopback worlds
-#                (tools/small_call_latency.py)
-#   hostcost     tools/host_cost_probe.py over a one-rank RCCL self loop, graph cache on and off
-#   rankprobe    tools/probes/ipc_rank_probe.py at 300 MiB without and with the input synchronisation (r03 record)
+#   xrel         the r06 release experiment (tools/probes/release_experiment.sh; DESIGN.md §5b, correctness record 5)
+#   launcher     bench.py's N > 1 entry on a one-GPU box: a plain --gpus 8 (the refusal, exit 6) and the harness through
+#                the launcher (HCCL_AMD_BENCH_HOST_EXCHANGE=1 python3 bench.py --gpus 2: n_gpus 2)
+#   selfloop     the RCCL stand-in of the N > 1 line (HCCL_AMD_BENCH_SELFLOOP=1 bench.py --gpus 8: rank 0's programs
+#                over a one-rank RCCL self loop, every RCCL-path row)
 # Every step runs under its own time limit; a limit, abort or crash ends the call there.
 set -o pipefail
 REPO=$(pwd)
@@ -47,7 +48,7 @@ step_bench() {
 }
 
 step_profile() {
-  run profile 1000 bash tools/profile_round.sh "${TAG:-r05}"
+  run profile 1000 bash tools/profile_round.sh "${TAG:-r06}"
 }
 
 step_harness() {
@@ -61,35 +62,35 @@ step_harness() {
   case $rc in 124|137|134|139) exit $rc ;; esac
 }
 
-step_latency() {
-  : > "$OUT/small_call_latency_rank_mode.jsonl"
-  local n algo port=29631
-  for n in 2 4; do
-    for algo in RHD AUTO; do
-      port=$((port + 1))
-      run "graph_latency_${algo}_n$n" 240 env HCCL_AMD_HOST_PROFILE=1 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" \
-        --master-addr 127.0.0.1 --master-port $port tools/graph_latency.py --algo "$algo" \
-        --sizes 1024,16384,131072,1048576
-      grep -h '^{' "$OUT/graph_latency_${algo}_n$n.log" >> "$OUT/small_call_latency_rank_mode.jsonl" || true
-    done
-  done
-  run small_call_latency 400 python3 -u tools/small_call_latency.py
-  grep -h '^{' "$OUT/small_call_latency.log" > "$OUT/small_call_latency_loopback.jsonl" || true
+step_xrel() {
+  echo "== release experiment"
+  bash tools/probes/release_experiment.sh
+  local rc=$?
+  echo "   rc=$rc"
+  case $rc in 124|137|134|139) exit $rc ;; esac
 }
 
-step_hostcost() {
-  run hostcost 300 env HCCL_AMD_HOST_PROFILE=1 python3 -u tools/host_cost_probe.py
-  run hostcost_nograph 300 env HCCL_AMD_HOST_PROFILE=1 HCCL_AMD_GRAPH_CACHE=0 python3 -u tools/host_cost_probe.py
-  grep -h '^{' "$OUT/hostcost.log" "$OUT/hostcost_nograph.log" > "$OUT/host_cost_selfloop.jsonl" || true
+step_launcher() {
+  echo "== launcher: plain --gpus 8 on a one-GPU box"
+  timeout -k 10 120 python3 bench.py --gpus 8 > "$OUT/bench_refuse_n8.json" 2> "$OUT/bench_refuse_n8.err"
+  local rc=$?
+  echo "   rc=$rc (6 = refused)"; cat "$OUT/bench_refuse_n8.json"
+  case $rc in 124|137|134|139) exit $rc ;; esac
+  echo "== harness through the launcher: python3 bench.py --gpus 2"
+  HCCL_AMD_BENCH_HOST_EXCHANGE=1 timeout -k 10 "${HARNESS_LIMIT:-500}" python3 bench.py --gpus 2 --steps 3 --warmup 1 \
+    > "$OUT/bench_harness_launcher_n2.json" 2> "$OUT/bench_harness_launcher_n2.err"
+  rc=$?
+  echo "   rc=$rc"; cut -c1-400 "$OUT/bench_harness_launcher_n2.json"
+  case $rc in 124|137|134|139) exit $rc ;; esac
 }
 
-step_rankprobe() {
-  : > "$OUT/rank_probe_sync.jsonl"
-  run rank_probe_nosync 240 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-    --master-port 29701 tools/probes/ipc_rank_probe.py --mib 64,300,300,300 --no-sync
-  run rank_probe_sync 240 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-    --master-port 29702 tools/probes/ipc_rank_probe.py --mib 64,300,300,300
-  grep -h '^{' "$OUT/rank_probe_nosync.log" "$OUT/rank_probe_sync.log" > "$OUT/rank_probe_sync.jsonl" || true
+step_selfloop() {
+  echo "== self-loop stand-in: HCCL_AMD_BENCH_SELFLOOP=1 python3 bench.py --gpus 8"
+  HCCL_AMD_BENCH_SELFLOOP=1 timeout -k 10 "${SELFLOOP_LIMIT:-600}" python3 bench.py --gpus 8 --steps 3 --warmup 1 \
+    > "$OUT/bench_selfloop_n8.json" 2> "$OUT/bench_selfloop_n8.err"
+  local rc=$?
+  echo "   rc=$rc"; cut -c1-400 "$OUT/bench_selfloop_n8.json"; tail -3 "$OUT/bench_selfloop_n8.err"
+  case $rc in 124|137|134|139) exit $rc ;; esac
 }
 
 for s in "$@"; do
