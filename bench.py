@@ -679,8 +679,9 @@ def _graph_us(call, calls: int = 50, replays: int = 5) -> float:
 
 def _xgmi_frac(busbw_GBps: float, world: int):
     """busbw as a fraction of the xGMI algorithmic-bus roofline a rank has (one 76.8 GB/s link per peer, at most 7);
-    None in the one-GPU harness mode, whose ranks share one device and have no xGMI in the path."""
-    if os.environ.get("HCCL_AMD_BENCH_HOST_EXCHANGE") == "1" or world < 2:
+    None in the one-GPU harness and self-loop modes, which have no xGMI in the path."""
+    if os.environ.get("HCCL_AMD_BENCH_HOST_EXCHANGE") == "1" or os.environ.get("HCCL_AMD_BENCH_SELFLOOP") == "1" \
+            or world < 2:
         return None
     return round(busbw_GBps / (min(world - 1, 7) * XGMI_LINK_GBPS), 4)
 
@@ -988,7 +989,8 @@ def bench_c3_algos(comm, send, recv, world) -> dict:
             comm.set_algo(algo)
             comm.set_ipc_blocks(blocks)
             try:
-                t = _timed(lambda: comm.all_reduce(send, recv, H.HcclReduceOp.SUM, s), 3, warmup=1)
+                # two warm-up calls: the eager first call and the graph capture of the second stay out of the timing
+                t = _timed(lambda: comm.all_reduce(send, recv, H.HcclReduceOp.SUM, s), 3, warmup=2)
             except H.HcclError as e:  # one schedule failing never hides the others
                 out[name] = {"error": str(e)}
                 continue
@@ -1017,7 +1019,7 @@ def bench_c3_algos(comm, send, recv, world) -> dict:
         saved = comm.get_config(H.Config.GRAPH_CACHE)
         comm.set_config(H.Config.GRAPH_CACHE, 0)
         try:
-            t = _timed(lambda: comm.all_reduce(send, recv, H.HcclReduceOp.SUM, s), 3, warmup=1)
+            t = _timed(lambda: comm.all_reduce(send, recv, H.HcclReduceOp.SUM, s), 3, warmup=2)
             out["RING_EAGER"] = {"ms": round(t * 1e3, 3),
                                  "busbw_GBps": round(C3_BYTES / t / 1e9 * 2 * (world - 1) / world, 2),
                                  "ran": H.Algo(comm.last_algo).name, "graph_cache": 0}
@@ -1191,8 +1193,11 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
     stream = torch.cuda.current_stream()
 
     def warm(c, algo):
+        # at least two untimed calls: a shape's first call runs eagerly (RCCL connects the program's peers) and its
+        # second captures the executor graph that later calls replay (HCCL_AMD_GRAPH_CACHE), so with fewer the capture
+        # would land inside the timed steps
         c.set_algo(algo)
-        for _ in range(args.warmup):
+        for _ in range(max(args.warmup, 2)):
             c.all_reduce(send, recv, H.HcclReduceOp.SUM, stream)
         torch.cuda.synchronize()
 
@@ -1369,7 +1374,7 @@ def _bench_allreduce(args, rank: int, world: int, local_rank: int) -> dict:
         extra["data_path_choice"] = {"error": f"{type(e).__name__}: {e}"}
     if not args.no_rccl_ref:
         wd.stage("rccl_allreduce_reference")
-        res["rccl_allreduce_reference"] = rccl_allreduce_reference(send, recv, world, args)
+        res["rccl_allreduce_reference"] = rccl_allreduce_reference(send, recv, dist_world, args)
     if not args.no_cpu_baseline and rank == 0:
         # the reference's CPU path on this box's host cores, beside the line (BASELINE.json north_star): the C2 leg
         # and this N's AllReduce program replayed on the host at a stated size

@@ -375,6 +375,13 @@ def comm_init_root_info(n_ranks: int, root_info: bytes, rank: int) -> Comm:
     return Comm(h.value)
 
 
+def ipc_idle_staging(release: bool = False) -> int:
+    """Bytes of the one-sided path's idle uncached blocks kept for reuse (HcclAmdIpcIdleStaging); release frees them."""
+    b = ctypes.c_uint64(0)
+    check("HcclAmdIpcIdleStaging", lib.HcclAmdIpcIdleStaging(1 if release else 0, ctypes.byref(b)))
+    return b.value
+
+
 def comm_init_selfloop(n_ranks: int, rank: int = 0) -> Comm:
     """A one-GPU stand-in for rank `rank` of an n_ranks world: its schedules run through a one-rank RCCL communicator
     with every peer mapped onto itself (HcclAmdCommInitSelfLoop; harnesses only: the data no longer means the

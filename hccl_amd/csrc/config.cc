@@ -78,6 +78,7 @@ CommConfig ReadCommConfig()
     c.ipcL2Scrub = !EnvIs("HCCL_AMD_IPC_L2_SCRUB", "0", false);
     c.foldTiming = EnvIs("HCCL_AMD_FOLD_TIMING", "1", false);
     if (EnvU64("HCCL_AMD_IPC_LL_BYTES", &v) && v <= kIpcLlMaxBytes) c.ipcLlBytes = v;
+    if (EnvU64("HCCL_AMD_INJECT_IPC_ALLOC_FAIL", &v) && v < (1u << 20)) c.injectIpcAllocFail = static_cast<int32_t>(v);
     return c;
 }
 

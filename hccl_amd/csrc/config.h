@@ -37,6 +37,8 @@ struct CommConfig {
     bool foldTiming = false;                      // HCCL_AMD_FOLD_TIMING: time the executor's folds (diagnostics)
     uint64_t ipcLlBytes = 64ull << 10;            // HCCL_AMD_IPC_LL_BYTES: one-shot AllReduces up to this many bytes
                                                   // per rank (at most 64 KiB) in the LL form (ipc_kernel_body.h)
+    int32_t injectIpcAllocFail = -1;              // HCCL_AMD_INJECT_IPC_ALLOC_FAIL=r (tests): rank r's one-sided
+                                                  // set-up allocations fail, as under memory pressure
 };
 
 // The configuration a communicator created now takes.

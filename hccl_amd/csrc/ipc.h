@@ -188,7 +188,6 @@ uint32_t IpcResidentBlocks(HcclDataType dt, HcclReduceOp op, bool rhd, bool ll, 
 
 // Writes back and invalidates every XCD's L2 at system scope (one maintenance block per CU); synchronous on `stream`.
 HcclResult ScrubL2(hipStream_t stream);
-void XSentinelCheck(const char* where);  // EXPERIMENT (r06)
 
 // Staging of the one-sided kernel comes in two tiers, each one uncached allocation per rank holding the four areas
 // (kIpcAreaIn, kIpcAreaRes, kIpcAreaAlt0, kIpcAreaAlt1), mapped by every peer, and each set up collectively by the

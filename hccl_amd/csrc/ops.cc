@@ -591,6 +591,13 @@ HcclResult HcclAmdCommDeviceBytes(HcclComm comm, uint64_t* bytes)
     return HCCL_SUCCESS;
 }
 
+HcclResult HcclAmdIpcIdleStaging(int32_t release, uint64_t* bytes)
+{
+    if (bytes == nullptr) return HCCL_E_PTR;
+    *bytes = IpcIdleBytes(release != 0);
+    return HCCL_SUCCESS;
+}
+
 HcclResult HcclAmdCommScratch(HcclComm comm, void** ptr, uint64_t* bytes)
 {
     Comm* c = AsComm(comm);

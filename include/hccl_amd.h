@@ -357,6 +357,13 @@ extern HcclResult HcclAmdCommScratch(HcclComm comm, void** ptr, uint64_t* bytes)
  * one, 2 x HCCL_BUFFSIZE, each at the first call that needs it). RCCL's own buffers are not included. */
 extern HcclResult HcclAmdCommDeviceBytes(HcclComm comm, uint64_t* bytes);
 
+/* The one-sided path's uncached allocations outlive the communicator that made them: a destroyed communicator's
+ * blocks stay with the process and serve the next communicator's set-up of the same size on the same device (the r03
+ * test order lost data when they were returned at every destroy and made anew). *bytes = the
+ * idle blocks' total size; release != 0 first frees them (after a device synchronisation of their devices). Call it
+ * with no one-sided collective in flight. */
+extern HcclResult HcclAmdIpcIdleStaging(int32_t release, uint64_t* bytes);
+
 /* Enqueues on `stream` a system-scope write-back and invalidate of every XCD's L2 of the current device (one
  * workgroup per CU runs buffer_wbl2 sc0 sc1 / buffer_inv sc0 sc1) and waits for it. Diagnostics: a kernel launched
  * after it reads every line from memory. */
@@ -387,9 +394,9 @@ extern HcclResult HcclAmdCommInitHostExchange(uint32_t nRanks, uint32_t rank, Hc
  * path): rank `rank`'s schedules run through a one-rank RCCL communicator with every peer mapped onto itself. Each
  * transport group's sends are paired with its receives of the same size (RCCL pairs messages to itself in posting
  * order), so every program keeps the schedule's shape (groups, pieces, staging, folds, waits, graph capture) and runs
- * through RCCL's kernels, while the data no longer means the collective. A group whose send and receive sizes differ
- * returns HCCL_E_NOT_SUPPORT. The one-sided kernel is unavailable (HCCL_E_NOT_SUPPORT; the small-call rule falls back
- * to the schedule). */
+ * through RCCL's kernels, while the data no longer means the collective. Sends and receives of a group whose sizes
+ * differ (a ragged last chunk) are paired in order at the smaller size; a surplus on either side is dropped. The
+ * one-sided kernel is unavailable (HCCL_E_NOT_SUPPORT; the small-call rule falls back to the schedule). */
 extern HcclResult HcclAmdCommInitSelfLoop(uint32_t nRanks, uint32_t rank, HcclComm* comm);
 
 #ifdef __cplusplus

@@ -292,11 +292,26 @@ def test_ownership_orders_follow_executor_loops(monkeypatch, op_type, algo, n, c
                             if np.float32(sum(np.float32(ops_[i]) for i in c)) == outs[q][st]]
                     runs.append((st, ln, fits[:3]))
                 diag.setdefault("bad_runs", {})[q] = runs
+                # every run of zero words in the staging as memory holds it now (random operands are never 0): where
+                # a receive's bytes were lost, and at what granularity (a 128-B line, a 4-KiB page, ...)
+                zw = words.view(np.uint32) == 0
+                edges = np.flatnonzero(np.diff(np.concatenate(([0], zw.astype(np.int8), [0]))))
+                recs = [(int(arr[i].dstOff), int(arr[i].count)) for i in range(nops)
+                        if arr[i].kind == H.IrKind.RECV and arr[i].dstBuf == 2]
+                zero_runs = []
+                for a0, a1 in zip(edges[0::2], edges[1::2]):
+                    if a1 - a0 < 16:
+                        continue
+                    in_recv = [o for o, c in recs if o < a1 and a0 < o + c]
+                    zero_runs.append({"off_B": int(a0) * 4, "len_B": int(a1 - a0) * 4, "addr_mod_4K": (ptr + int(a0) * 4) % 4096,
+                                      "addr_mod_64K": (ptr + int(a0) * 4) % 65536, "in_recv_at": in_recv[:2]})
                 diag["staging_now"][q] = {"at_bad": [float(words[int(b)]) for b in bad[:3]],
                                           "recv_offsets": recv_offs,
                                           "at_recv_plus_bad": {o: float(words[o + e]) for o in recv_offs
                                                                if o + e < len(words)},
-                                          "operands_at_bad": [float(x[e]) for x in xs]}
+                                          "operands_at_bad": [float(x[e]) for x in xs],
+                                          "scratch": [hex(ptr), nbytes],
+                                          "zero_runs": zero_runs[:40], "zero_runs_total": len(zero_runs)}
         for r in range(n):
             if op_type == RED and r != root:
                 assert not outs[r].any(), "non-root recvBuf written"

@@ -137,3 +137,34 @@ def test_large_tier_defaults_to_the_reference_buffer_contract(monkeypatch):
         torch.cuda.synchronize()
         for c in comms:
             c.destroy()
+
+
+@pytest.mark.parametrize("op_type,count", [(AR, 4099), (AR, (1 << 20) // 4), (RS, 1000), (RED, 5000)])
+def test_failed_ipc_allocation_falls_back_to_the_schedule(monkeypatch, op_type, count):
+    """when one rank's one-sided set-up cannot allocate, every rank agrees on HCCL_E_NOT_SUPPORT and the
+    small-call rule runs the schedule of the same family instead, on every rank alike: the call succeeds with the
+    schedule's bits (integer-valued data, so any order is exact) and nothing of the one-sided path is left allocated."""
+    monkeypatch.setenv("HCCL_AMD_SMALL_IPC_BYTES", str(MIB))
+    monkeypatch.setenv("HCCL_AMD_INJECT_IPC_ALLOC_FAIL", "2")
+    n = 4
+    comms = H.loopback_world(n)
+    try:
+        in_count = count * n if op_type == RS else count
+        xs = _ints(n, in_count)
+        used, outs = collective(comms, op_type, H.Algo.AUTO, O.FP32, O.SUM, xs, count, root=1)
+        assert not H.Algo(used).name.startswith("IPC"), H.Algo(used).name
+        total = sum(xs)
+        for r in range(n):
+            if op_type == RED and r != 1:
+                continue
+            want = total[r * count:(r + 1) * count] if op_type == RS else total
+            assert np.array_equal(outs[r], want), r
+        for c in comms:
+            assert c.device_bytes() == c.scratch()[1], "only the executor staging is held"
+        # a later small call takes the schedule at once (the one-sided path stays unavailable, on every rank)
+        used, outs = collective(comms, op_type, H.Algo.AUTO, O.FP32, O.SUM, xs, count, root=1)
+        assert not H.Algo(used).name.startswith("IPC")
+    finally:
+        torch.cuda.synchronize()
+        for c in comms:
+            c.destroy()

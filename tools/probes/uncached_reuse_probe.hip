@@ -9,12 +9,14 @@
 //      block; a copy kernel (16-B non-temporal loads/stores, 256 workgroups, as k_copy_units) fills it from a source
 //      holding pattern Q; then 256 workgroups (every XCD) read all of it with plain and non-temporal loads and count
 //      words != Q; then a host copy counts words != Q and classifies them (0, P, the sentinel, other); hipFree.
-// Output: one JSON line per configuration with totals. Build: hipcc --offload-arch=gfx950 -O2 -o uncached_reuse_probe
+// Output: one JSON line per configuration with totals. `uncached_reuse_probe fresh [iters]`: the fresh-allocation mode
+// below. Build: hipcc --offload-arch=gfx950 -O2 -o uncached_reuse_probe
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <vector>
 
 #define CHK(x)                                                                              \
@@ -83,8 +85,84 @@ __global__ __launch_bounds__(256) void k_read_all(const uint32_t* p, uint64_t wo
     }
 }
 
+// "fresh" mode (r06): does the first kernel that writes a freshly allocated buffer have its bytes kept? Per iteration:
+// optionally allocate and free a 1 GiB uncached block first (work for the driver's wipe of released VRAM), then
+// allocate S bytes (cached or uncached), launch at once a 256-workgroup kernel writing a pattern over all of it, then a
+// kernel that counts mismatching words from 256 workgroups on every XCD; then a host copy of the first and last 4 MiB.
+// A zero word where the pattern should be means the write was lost or overwritten after the fact.
+__global__ __launch_bounds__(256) void k_count(const uint32_t* p, uint64_t words, uint32_t pat, unsigned long long* bad,
+                                               unsigned long long* zero)
+{
+    unsigned long long b = 0, z = 0;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < words; i += gridDim.x * 256ull) {
+        const uint32_t x = p[i];
+        b += x != (pat ^ uint32_t(i));
+        z += x == 0;
+    }
+    atomicAdd(bad, b);
+    atomicAdd(zero, z);
+}
+
+int fresh(int iters)
+{
+    unsigned long long* cnt = nullptr;
+    CHK(hipMalloc(&cnt, 16));
+    const size_t sizes[] = {2ull << 20, 64ull << 20, 512ull << 20};
+    for (int unc = 0; unc < 2; ++unc) {
+        for (size_t S : sizes) {
+            for (int churn = 0; churn < 2; ++churn) {
+                long runsBad = 0, gpuBad = 0, gpuZero = 0, hostBad = 0;
+                for (int it = 0; it < iters; ++it) {
+                    if (churn) {
+                        void* big = nullptr;
+                        CHK(hipExtMallocWithFlags(&big, 1ull << 30, hipDeviceMallocUncached));
+                        hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, nullptr, static_cast<uint32_t*>(big),
+                                           uint64_t((1ull << 30) / 4), 0x77u);
+                        CHK(hipDeviceSynchronize());
+                        CHK(hipFree(big));
+                    }
+                    void* b = nullptr;
+                    if (unc) {
+                        CHK(hipExtMallocWithFlags(&b, S, hipDeviceMallocUncached));
+                    } else {
+                        CHK(hipMalloc(&b, S));
+                    }
+                    const uint32_t pat = 0x1C000000u | uint32_t(it * 131 + int(S >> 20));
+                    hipLaunchKernelGGL(k_fill, dim3(256), dim3(256), 0, nullptr, static_cast<uint32_t*>(b),
+                                       uint64_t(S / 4), pat);
+                    CHK(hipMemsetAsync(cnt, 0, 16, nullptr));
+                    hipLaunchKernelGGL(k_count, dim3(256), dim3(256), 0, nullptr, static_cast<const uint32_t*>(b),
+                                       uint64_t(S / 4), pat, cnt, cnt + 1);
+                    unsigned long long hc[2];
+                    CHK(hipMemcpy(hc, cnt, 16, hipMemcpyDeviceToHost));
+                    const size_t part = std::min<size_t>(S, 4ull << 20);
+                    std::vector<uint32_t> h(part / 4);
+                    long hb = 0;
+                    for (int end = 0; end < 2; ++end) {
+                        const size_t off = end ? S - part : 0;
+                        CHK(hipMemcpy(h.data(), static_cast<char*>(b) + off, part, hipMemcpyDeviceToHost));
+                        for (size_t i = 0; i < h.size(); ++i) hb += h[i] != (pat ^ uint32_t(off / 4 + i));
+                    }
+                    gpuBad += long(hc[0]);
+                    gpuZero += long(hc[1]);
+                    hostBad += hb;
+                    runsBad += (hc[0] != 0 || hb != 0);
+                    CHK(hipFree(b));
+                }
+                std::printf("{\"probe\": \"fresh_write\", \"uncached\": %d, \"bytes\": %zu, \"churn_1GiB_free\": %d, "
+                            "\"iters\": %d, \"iters_with_wrong_words\": %ld, \"gpu_wrong\": %ld, \"gpu_zero\": %ld, "
+                            "\"host_wrong_first_last_4MiB\": %ld}\n", unc, S, churn, iters, runsBad, gpuBad, gpuZero, hostBad);
+                std::fflush(stdout);
+            }
+        }
+    }
+    CHK(hipFree(cnt));
+    return 0;
+}
+
 int main(int argc, char** argv)
 {
+    if (argc > 1 && std::strcmp(argv[1], "fresh") == 0) return fresh(argc > 2 ? std::atoi(argv[2]) : 50);
     const int iters = argc > 1 ? std::atoi(argv[1]) : 200;
     const size_t flagBytes = (32ull << 10) + (4ull << 20);
     const size_t stgBytes = 2ull << 20;
