@@ -375,10 +375,11 @@ def comm_init_root_info(n_ranks: int, root_info: bytes, rank: int) -> Comm:
     return Comm(h.value)
 
 
-def ipc_idle_staging(release: bool = False) -> int:
-    """Bytes of the one-sided path's idle uncached blocks kept for reuse (HcclAmdIpcIdleStaging); release frees them."""
+def ipc_idle_staging() -> int:
+    """Bytes of the one-sided path's idle uncached blocks kept for reuse (HcclAmdIpcIdleStaging; they are never freed
+    while the process runs)."""
     b = ctypes.c_uint64(0)
-    check("HcclAmdIpcIdleStaging", lib.HcclAmdIpcIdleStaging(1 if release else 0, ctypes.byref(b)))
+    check("HcclAmdIpcIdleStaging", lib.HcclAmdIpcIdleStaging(0, ctypes.byref(b)))
     return b.value
 
 

@@ -326,9 +326,9 @@ void IpcRelease(Comm& c);
 // configuration, so equal on every rank. IpcDeviceBytes: the device bytes c's IPC path holds now.
 IpcTier IpcTierSizes(const Comm& c, int t);
 uint64_t IpcDeviceBytes(const Comm& c);
-// The process's idle uncached blocks of the IPC path (kept for reuse by later communicators), in bytes; release = true
-// frees them first (HcclAmdIpcIdleStaging).
-uint64_t IpcIdleBytes(bool release);
+// The process's idle uncached blocks of the IPC path (kept for reuse by later communicators), in bytes
+// (HcclAmdIpcIdleStaging).
+uint64_t IpcIdleBytes();
 
 Comm* AsComm(HcclComm c);
 

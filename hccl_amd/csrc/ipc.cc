@@ -21,15 +21,12 @@ namespace hccl_amd {
 namespace {
 
 // The uncached allocations of the IPC path (the staging tiers; flags and LL area) are kept for the life of the process
-// and handed to the next communicator's set-up that asks for the same size on the same device, instead of going back
-// to the runtime (HcclAmdIpcIdleStaging releases the idle ones on request). The r03 test order with the allocations
-// returned to the runtime at every destroy lost 512-B pieces of a later kernel's output, which read as 0 from memory
-// afterwards: r05 1 of 3, 0 of 3 and 1 of 1 runs passed; r06 (profiles/r06_release_experiment.txt) 2 of 3 on the r05
-// layout (3 of 3 with an L2 write-back + invalidate before every free), 3 of 3 on the r06 layout (2 of 3 with that L2
-// maintenance, so it is not the cure); with the pool every run of that order since r05 passed. A late writer into released blocks is ruled out (blocks kept and filled with a
-// sentinel: no word changed in any run), and so is the reallocation of a released block's address (no failing buffer
-// overlapped one); a one-thread probe of the same allocation sequence never lost a word. The mechanism is not
-// demonstrated; the pool keeps the order's allocations from being returned and re-made.
+// and handed to the next communicator's set-up that asks for the same size on the same device; they are never freed.
+// Freeing hipDeviceMallocUncached memory corrupts later GPU work on this stack: the r03 test order's allocation history
+// in a loop returned wrong results (ranks' operands missing) in 17 of 217 iterations with these blocks freed after
+// every destroy and in 0 of 223 with them kept, and a loop that freed uncached blocks allocated outside the library
+// faulted the GPU (memory aperture violation) where the same loop with cached blocks ran clean
+// (profiles/r06_release_stress.txt).
 struct UncachedPool {
     std::mutex mu;
     std::multimap<std::pair<int, size_t>, void*> idle;  // (device, bytes) -> allocation
@@ -65,22 +62,12 @@ void UncachedRelease(int device, void* ptr, size_t bytes)
 
 }  // namespace
 
-uint64_t IpcIdleBytes(bool release)
+uint64_t IpcIdleBytes()
 {
     UncachedPool& pool = Pool();
     std::lock_guard<std::mutex> lk(pool.mu);
     uint64_t b = 0;
     for (const auto& kv : pool.idle) b += kv.first.second;
-    if (!release || pool.idle.empty()) return b;
-    int dev0 = 0;
-    (void)hipGetDevice(&dev0);
-    for (const auto& kv : pool.idle) {
-        (void)hipSetDevice(kv.first.first);
-        (void)hipDeviceSynchronize();
-        (void)hipFree(kv.second);
-    }
-    (void)hipSetDevice(dev0);
-    pool.idle.clear();
     return b;
 }
 

@@ -594,8 +594,10 @@ HcclResult HcclAmdCommDeviceBytes(HcclComm comm, uint64_t* bytes)
 HcclResult HcclAmdIpcIdleStaging(int32_t release, uint64_t* bytes)
 {
     if (bytes == nullptr) return HCCL_E_PTR;
-    *bytes = IpcIdleBytes(release != 0);
-    return HCCL_SUCCESS;
+    *bytes = IpcIdleBytes();
+    // Freeing memory allocated with hipDeviceMallocUncached corrupts later GPU work on this stack (DESIGN.md §5b, item
+    // 5; profiles/r06_release_stress.txt): the idle blocks stay with the process.
+    return release != 0 ? HCCL_E_NOT_SUPPORT : HCCL_SUCCESS;
 }
 
 HcclResult HcclAmdCommScratch(HcclComm comm, void** ptr, uint64_t* bytes)

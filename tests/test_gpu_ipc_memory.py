@@ -168,3 +168,54 @@ def test_failed_ipc_allocation_falls_back_to_the_schedule(monkeypatch, op_type, 
         torch.cuda.synchronize()
         for c in comms:
             c.destroy()
+
+
+_IDLE_CHILD = r'''
+import ctypes, os, sys, json
+sys.path.insert(0, os.getcwd())
+import numpy as np, torch
+import hccl_amd as H
+from oracle import oracle as O
+from tests.test_gpu_collectives import AR, collective
+torch.cuda.set_device(0)
+out = {"idle_before": H.ipc_idle_staging()}
+xs = [(np.arange(100000) % 97 + r).astype(np.float32) for r in range(2)]
+exact = True
+for k in range(2):
+    comms = H.loopback_world(2)
+    used, outs = collective(comms, AR, H.Algo.IPC_TWOSHOT, O.FP32, O.SUM, xs, 100000)
+    exact = exact and all(np.array_equal(o, xs[0] + xs[1]) for o in outs)
+    out[f"idle_while_alive_{k}"] = H.ipc_idle_staging()
+    torch.cuda.synchronize()
+    for c in comms:
+        c.destroy()
+    out[f"idle_after_destroy_{k}"] = H.ipc_idle_staging()
+b = ctypes.c_uint64(0)
+out["release_rc"] = H.lib.HcclAmdIpcIdleStaging(1, ctypes.byref(b))
+out["release_reported"] = b.value
+out["idle_after_release"] = H.ipc_idle_staging()
+out["exact"] = bool(exact)
+print(json.dumps(out))
+'''
+
+
+def test_idle_staging_is_reported_and_reused_never_freed():
+    """HcclAmdIpcIdleStaging: a destroyed communicator's uncached blocks stay with the process (reported), the next
+    communicator's set-up of the same sizes takes them back (the idle total returns to 0 while it lives), and a request
+    to release them is refused (HCCL_E_NOT_SUPPORT) after reporting: freeing uncached memory corrupts later GPU work on
+    this stack (DESIGN.md §5b, item 5). In a child process, so that the counts start from zero."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _IDLE_CHILD], cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["idle_before"] == 0 and out["idle_while_alive_0"] == 0, out
+    idle = out["idle_after_destroy_0"]
+    assert idle > 0, out
+    assert out["idle_while_alive_1"] == 0, out  # the second world's set-up reused every block
+    assert out["idle_after_destroy_1"] == idle, out
+    assert out["release_rc"] == int(H.HcclResult.HCCL_E_NOT_SUPPORT) and out["release_reported"] == idle, out
+    assert out["idle_after_release"] == idle and out["exact"], out
