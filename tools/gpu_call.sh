@@ -5,7 +5,6 @@
 #   bench        bench.py default line (N = 1) -> gpurun_out/bench.json
 #   profile      tools/profile_round.sh $TAG (rocprofv3 trace + FETCH_SIZE + WRITE_SIZE of the N = 1 line)
 #   harness      bench.py's N > 1 path with $HARNESS_N ranks sharing the GPU (IPC-only communicators; a crash check)
-#   xrel         the r06 release experiment (tools/probes/release_experiment.sh; DESIGN.md §5b, correctness record 5)
 #   launcher     bench.py's N > 1 entry on a one-GPU box: a plain --gpus 8 (the refusal, exit 6) and the harness through
 #                the launcher (HCCL_AMD_BENCH_HOST_EXCHANGE=1 python3 bench.py --gpus 2: n_gpus 2)
 #   selfloop     the RCCL stand-in of the N > 1 line (HCCL_AMD_BENCH_SELFLOOP=1 bench.py --gpus 8: rank 0's programs
@@ -59,14 +58,6 @@ step_harness() {
     --warmup 1 > "$OUT/bench_harness_n$n.json" 2> "$OUT/bench_harness_n$n.err"
   local rc=$?
   echo "   rc=$rc"; tail -3 "$OUT/bench_harness_n$n.err"
-  case $rc in 124|137|134|139) exit $rc ;; esac
-}
-
-step_xrel() {
-  echo "== release experiment"
-  bash tools/probes/release_experiment.sh
-  local rc=$?
-  echo "   rc=$rc"
   case $rc in 124|137|134|139) exit $rc ;; esac
 }
 
