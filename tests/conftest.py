@@ -25,9 +25,10 @@ def _ensure_built():
 
 _ensure_built()
 
-# The one-sided kernel's staging areas are 512 MiB per rank by default; the IPC tests' multi-round counts were sized
-# for 128 MiB areas (a chunk wider than one area runs several staging rounds), so the suite keeps that size unless a
-# test sets its own (test_gpu_collectives.py::test_ipc_default_staging covers the default). Child processes inherit it.
+# The one-sided kernel's large staging tier has areas of HCCL_BUFFSIZE / 2 (100 MiB) by default; the IPC tests'
+# multi-round counts were sized for 128 MiB areas (a chunk wider than one area runs several staging rounds), so the
+# suite keeps that size unless a test sets its own (test_gpu_collectives.py::test_ipc_default_staging and
+# test_gpu_ipc_ranks.py::test_ipc_rank_mode_default_staging cover the default). Child processes inherit it.
 os.environ.setdefault("HCCL_AMD_IPC_STAGING_MIB", "128")
 # AllReduces of up to 1 MiB per rank run on the one-sided kernel by default (HCCL_AMD_SMALL_IPC_BYTES, same bits as the
 # schedule they stand for). The suite checks the schedules themselves at those sizes, so it turns the rule off unless a

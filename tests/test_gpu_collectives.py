@@ -142,8 +142,8 @@ def test_ipc_allreduce_o2_and_status(worlds, n, count):
 
 @pytest.mark.parametrize("n,count", [(2, (80 << 20) + 3), (4, (40 << 20) + 1), (8, 4099)])
 def test_ipc_default_staging(monkeypatch, n, count):
-    """The default 512 MiB staging areas (r03: one round where 128 MiB areas took several, 5-12 % faster,
-    profiles/r03_ipc_variant_ab_{policy,shapes}.jsonl): two-shot IPC AllReduce bit-exact with order O2, barrier status clean."""
+    """The default large staging tier (HCCL_BUFFSIZE / 2 = 100 MiB areas since r06; 512 MiB before): two-shot IPC
+    AllReduce bit-exact with order O2 over several staging rounds, barrier status clean."""
     monkeypatch.delenv("HCCL_AMD_IPC_STAGING_MIB", raising=False)
     comms = H.loopback_world(n)
     try:
