@@ -360,9 +360,9 @@ extern HcclResult HcclAmdCommDeviceBytes(HcclComm comm, uint64_t* bytes);
 /* The one-sided path's uncached allocations outlive the communicator that made them: a destroyed communicator's
  * blocks stay with the process and serve the next communicator's set-up of the same size on the same device. *bytes =
  * the idle blocks' total size. They are never freed while the process runs: freeing memory allocated with
- * hipDeviceMallocUncached corrupts later GPU work on this stack (kernels run with a former dispatch's arguments: lost
- * operands, memory aperture violations), so release != 0 returns HCCL_E_NOT_SUPPORT after
- * reporting. */
+ * hipDeviceMallocUncached corrupts later GPU work on this stack (lost operands and memory aperture violations after
+ * such frees), so release != 0 returns HCCL_E_NOT_SUPPORT after reporting. A block serves
+ * only a request of its own size: communicators of other sizes (rank count, HCCL_BUFFSIZE) allocate their own. */
 extern HcclResult HcclAmdIpcIdleStaging(int32_t release, uint64_t* bytes);
 
 /* Enqueues on `stream` a system-scope write-back and invalidate of every XCD's L2 of the current device (one
